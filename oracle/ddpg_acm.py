@@ -1,0 +1,78 @@
+"""ORACLE (test infrastructure only): one DDPG_AcM grad step, restated.
+
+Follows rltoolkit/acm/off_policy/ddpg_acm.py (reference @ v0):
+  compute_qfunc_targ :295-318  y = r + g(1-d) Qt(s', ACM(s', denorm mu_t(s')))
+  compute_pi_loss    :320-340  -Q(s, ACM(s, denorm mu(s))).mean() + c*MSE
+  update             :342-396  critic step, actor step, polyak on critic AND actor targets
+polyak: rltoolkit/algorithms/ddpg/ddpg.py:273-284.  The SPP-DDPG scripts inject
+BasicAcM (train/spp_ddpg_hcheetah.py:124) — ``acm_kind`` selects it.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import nets
+from .adam import OracleAdam
+
+
+class OracleDdpgAcm:
+    def __init__(self, ob, aout, ac, *, acm_critic=True, custom_loss=1.0, norm_closs=False, norm=None,
+                 actor_lim=1.0, acm_lim=1.0, acm_kind="basic", gamma=0.95, tau=0.005, actor_lr=5e-4,
+                 critic_lr=5e-4, params=None):
+        self.acm_critic, self.custom_loss, self.norm_closs, self.norm = acm_critic, custom_loss, norm_closs, norm
+        self.actor_lim = torch.as_tensor(actor_lim, dtype=torch.float32)
+        self.acm_lim = torch.as_tensor(acm_lim, dtype=torch.float32)
+        self.acm_kind, self.gamma, self.tau = acm_kind, gamma, tau
+        cin = ob + (ac if acm_critic else aout)
+        acm_lay = nets.basic_acm_layout(2 * ob, ac) if acm_kind == "basic" else nets.acm_layout(2 * ob, ac)
+        self.layouts = {"actor": nets.ddpg_actor_layout(ob, aout), "critic": nets.critic_layout(cin),
+                        "actor_targ": nets.ddpg_actor_layout(ob, aout), "critic_targ": nets.critic_layout(cin),
+                        "acm": acm_lay}
+        self.p = {k: {n: torch.as_tensor(params[k][n], dtype=torch.float32).clone()
+                      .requires_grad_(k in ("actor", "critic")) for n, _ in lay}
+                  for k, lay in self.layouts.items()}
+        self.opt = {"actor": OracleAdam(self.p["actor"].values(), actor_lr),
+                    "critic": OracleAdam(self.p["critic"].values(), critic_lr)}
+
+    def _acm(self, x):
+        if self.acm_kind == "basic":
+            return nets.basic_acm(self.p["acm"], x)
+        return nets.acm(self.p["acm"], x, self.acm_lim)
+
+    def update(self, obs, next_obs, action, reward, done, acm_action):
+        t = lambda a, dt=torch.float32: torch.as_tensor(np.asarray(a)).to(dt)  # noqa: E731
+        obs, next_obs, action, reward = t(obs), t(next_obs), t(action), t(reward)
+        done, acm_action = t(done, torch.int8), t(acm_action)
+        P, losses = self.p, {}
+        with torch.no_grad():
+            na = self.norm.denormalize(nets.ddpg_actor(P["actor_targ"], next_obs, self.actor_lim))
+            if self.acm_critic:
+                na = self._acm(torch.cat([next_obs, na], axis=1))
+            y = reward + self.gamma * (1 - done) * nets.ddpg_critic(P["critic_targ"], next_obs, na)
+        if self.acm_critic:
+            action = acm_action
+        lq = F.mse_loss(nets.ddpg_critic(P["critic"], obs, action), y)
+        losses["critic"] = lq.item()
+        self.opt["critic"].step(torch.autograd.grad(lq, list(P["critic"].values())))
+        a = nets.ddpg_actor(P["actor"], obs, self.actor_lim)
+        ad = self.norm.denormalize(a)
+        ca = self._acm(torch.cat([obs, ad], axis=1)) if self.acm_critic else ad
+        loss = -nets.ddpg_critic(P["critic"], obs, ca).mean()
+        losses["ddpg"], losses["dist"] = 0.0, 0.0
+        if self.custom_loss:
+            losses["ddpg"] = loss.item()
+            target, pred = (self.norm.normalize(next_obs), a) if self.norm_closs else (next_obs, ad)
+            dist = F.mse_loss(pred, target)
+            losses["dist"] = dist.item()
+            loss = loss + self.custom_loss * dist
+        losses["actor"] = loss.item()
+        self.opt["actor"].step(torch.autograd.grad(loss, list(P["actor"].values())))
+        with torch.no_grad():
+            for c, tg in (("critic", "critic_targ"), ("actor", "actor_targ")):
+                for n in P[c]:
+                    P[tg][n].mul_(1 - self.tau)
+                    P[tg][n].add_(self.tau * P[c][n])
+        return losses
+
+    def flat(self, k):
+        return nets.flatten(self.p[k]).numpy()

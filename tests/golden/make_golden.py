@@ -1,0 +1,433 @@
+"""Golden-vector generator: runs the REFERENCE rltoolkit on CPU, in the build
+container only (``/root/reference`` does not exist on the GPU box), and writes
+small .npz fixtures next to this file.  The fixtures (inputs + expected
+outputs) are data; no reference source is copied into the repository.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference pins gym 0.15 / mujoco-py / tensorboard, none of which exist
+here, so a minimal stand-in for those *dependencies* is installed first
+(SURVEY.md Appendix A): a synthetic fixed-shape env, a no-op SummaryWriter,
+``np.int = int``.  Only the reference's own code paths under test run:
+replay-ring indexing and sampling (rltoolkit/buffer/replay_buffer.py),
+SAC_AcM / DDPG_AcM ``update`` (rltoolkit/acm/off_policy/*.py), AcMTrainer
+``batch_update`` (rltoolkit/acm/acm.py:246-258), ``update_obs_mean_std``
+(replay_buffer.py:83-96) and PPO ``calculate_gae`` / ``_clip_loss``
+(rltoolkit/algorithms/ppo/ppo.py:117-150,194-204).
+
+Gaussian draws inside ``Normal.rsample`` come from torch's CPU generator and
+are not reproducible across implementations, so they are injected: the
+generator replaces ``torch.distributions.normal._standard_normal`` with a
+queue of seeded arrays that the tests regenerate.
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+os.makedirs("/tmp/spprl_golden", exist_ok=True)
+sys.argv[0] = "/tmp/spprl_golden/gen.py"  # reference logger mkdirs next to argv[0]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from weights import fill_params  # noqa: E402
+
+np.int = int  # reference targets numpy 1.18
+
+# ---------------------------------------------------------------- dependency stand-ins
+gym = types.ModuleType("gym")
+spaces = types.ModuleType("gym.spaces")
+
+
+class Box:
+    def __init__(self, low, high, shape, seed=0):
+        self.shape = shape
+        self.low = np.full(shape, low, np.float32)
+        self.high = np.full(shape, high, np.float32)
+        self._rng = np.random.RandomState(seed)
+
+    def sample(self):
+        return self._rng.uniform(self.low, self.high).astype(np.float32)
+
+
+class Discrete:
+    def __init__(self, n):
+        self.n = n
+
+
+spaces.Box, spaces.Discrete, gym.spaces = Box, Discrete, spaces
+SPECS = {"Pendulum-v0": (3, 1, 200), "Hopper-v2": (11, 3, 1000),
+         "HalfCheetah-v2": (17, 6, 1000), "Ant-v2": (111, 8, 1000)}
+
+
+class SynthEnv:
+    def __init__(self, name, seed=0):
+        ob, ac, T = SPECS[name]
+        self.observation_space = Box(-np.inf, np.inf, (ob,))
+        lim = 2.0 if name == "Pendulum-v0" else 1.0
+        self.action_space = Box(-lim, lim, (ac,), seed)
+        self._max_episode_steps = T
+
+
+gym.make = lambda name: SynthEnv(name)
+sys.modules["gym"] = gym
+sys.modules["gym.spaces"] = spaces
+tb = types.ModuleType("torch.utils.tensorboard")
+
+
+class SummaryWriter:
+    def __init__(self, *a, **k):
+        pass
+
+    def __getattr__(self, n):
+        return lambda *a, **k: None
+
+
+tb.SummaryWriter = SummaryWriter
+sys.modules["torch.utils.tensorboard"] = tb
+pvd = types.ModuleType("pyvirtualdisplay")
+pvd.Display = object
+sys.modules["pyvirtualdisplay"] = pvd
+sys.path.insert(0, "/root/reference/rltoolkit")
+
+from rltoolkit.acm.models.basic_acm import BasicAcM  # noqa: E402
+from rltoolkit.acm.off_policy import DDPG_AcM, SAC_AcM  # noqa: E402
+from rltoolkit.algorithms.ppo.ppo import PPO  # noqa: E402
+from rltoolkit.buffer import BufferAcMOffPolicy, Memory  # noqa: E402
+
+torch.set_num_threads(1)
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, sum(a.size for a in arrays.values()), "values")
+
+
+# ---------------------------------------------------------------- MT19937 randint
+def gen_randint():
+    out = {}
+    cases = []
+    for seed in (0, 1, 7, 12345, 2**31 - 1, 4294967295):
+        for n in (1, 2, 3, 7, 100, 1000, 1024, 1025, 65537, 10**6, 10**7, 2**31 - 1):
+            cases.append((seed, n))
+    seeds = np.array([c[0] for c in cases], np.uint64)
+    ns = np.array([c[1] for c in cases], np.int64)
+    K = 257
+    vals = np.zeros((len(cases), K), np.int64)
+    for i, (s, n) in enumerate(cases):
+        rs = np.random.RandomState(s)
+        vals[i] = rs.randint(0, n, K)
+    out.update(seeds=seeds, ns=ns, vals=vals)
+    # interleaved draws from one stream (sample_batch called repeatedly)
+    rs = np.random.RandomState(42)
+    seq_n = np.array([100, 5000, 3, 999999, 100, 17], np.int64)
+    seq = [rs.randint(0, n, 64) for n in seq_n]
+    out.update(seq_seed=np.array(42), seq_n=seq_n, seq_vals=np.stack(seq))
+    save("mt19937_randint.npz", **out)
+
+
+# ---------------------------------------------------------------- replay ring (Q6)
+def gen_replay():
+    out = {}
+    # (a) SURVEY Q6 trace: size 10, 5 episodes of 3 steps
+    # (b) size 50, ragged episodes 1..9 steps, 40 episodes, ob=3, aout=3, ac=2
+    for tag, size, ob, aout, ac, ep_lens, seed in (
+        ("a", 10, 2, 2, 1, [3] * 5, 0),
+        ("b", 50, 3, 3, 2, list(np.random.RandomState(3).randint(1, 10, 40)), 1),
+        ("c", 64, 11, 11, 3, list(np.random.RandomState(4).randint(1, 30, 25)), 2),
+    ):
+        rng = np.random.RandomState(seed)
+        buf = BufferAcMOffPolicy(size, ob, aout, acm_act_shape=ac)
+        ops = []  # (kind, a, b): kind 0 = add_obs(reset), 1 = step
+        obs_log, act_log, acm_log, rew_log, done_log, end_log = [], [], [], [], [], []
+        states = []
+        for L in ep_lens:
+            o = rng.randn(1, ob).astype(np.float32)
+            prev = buf.add_obs(torch.from_numpy(o))
+            obs_log.append(o[0])
+            ops.append((0, prev, -1))
+            for t in range(L):
+                acm = rng.uniform(-1, 1, ac).astype(np.float32)
+                buf.add_acm_action(acm)
+                a = torch.from_numpy(rng.randn(1, aout).astype(np.float32))
+                o = rng.randn(1, ob).astype(np.float32)
+                nxt = buf.add_obs(torch.from_numpy(o))
+                r = float(rng.randn())
+                end = t == L - 1
+                done = bool(end and rng.rand() < 0.5)
+                buf.add_timestep(prev, nxt, a, r, done, end)
+                ops.append((1, prev, nxt))
+                obs_log.append(o[0])
+                act_log.append(a.numpy()[0])
+                acm_log.append(acm)
+                rew_log.append(r)
+                done_log.append(done)
+                end_log.append(end)
+                states.append((buf.obs_idx, buf.ts_idx, buf.current_len))
+                prev = nxt
+        p = "r%s_" % tag
+        out[p + "dims"] = np.array([size, ob, aout, ac])
+        out[p + "ops"] = np.array(ops, np.int64)
+        out[p + "obs"] = np.array(obs_log, np.float32)
+        out[p + "act"] = np.array(act_log, np.float32)
+        out[p + "acm"] = np.array(acm_log, np.float32)
+        out[p + "rew"] = np.array(rew_log, np.float32)
+        out[p + "done"] = np.array(done_log, np.bool_)
+        out[p + "end"] = np.array(end_log, np.bool_)
+        out[p + "states"] = np.array(states, np.int64)
+        L = buf.current_len
+        out[p + "obs_idx"] = buf._obs_idx[:L].astype(np.int64)
+        out[p + "next_obs_idx"] = buf._next_obs_idx[:L].astype(np.int64)
+        # sample_batch after np.random.seed(s)  (replay_buffer.py:233-261,385-398)
+        for s in (0, 5):
+            B = 33
+            np.random.seed(s)
+            o, no, a, r, d, acm = buf.sample_batch(B)
+            np.random.seed(s)
+            idx = np.random.randint(0, len(buf), B)
+            q = p + "s%d_" % s
+            out[q + "idx"] = idx.astype(np.int64)
+            out[q + "obs"] = o.numpy()
+            out[q + "next_obs"] = no.numpy()
+            out[q + "act"] = a.numpy()
+            out[q + "rew"] = r.numpy()
+            out[q + "done"] = d.numpy()
+            out[q + "acm"] = acm.numpy()
+        # ACM regression batch (replay_buffer.py:404-430)
+        np.random.seed(9)
+        o, no, acm = buf.sample_acm_batch(17)
+        out[p + "acmb_obs"], out[p + "acmb_next_obs"], out[p + "acmb_acm"] = (
+            o.numpy(), no.numpy(), acm.numpy())
+        # obs statistics (replay_buffer.py:83-96), twice for running max/min
+        def stats():  # None (len <= 10: stats skipped) -> NaN row
+            return np.stack([np.full(ob, np.nan, np.float32) if t is None else t.numpy()
+                             for t in (buf.obs_mean, buf.obs_std, buf.max_obs, buf.min_obs)])
+
+        buf.update_obs_mean_std()
+        out[p + "st1"] = stats()
+        buf._obs[buf._obs_idx[: buf.current_len]] *= 0.5
+        buf.update_obs_mean_std()
+        out[p + "st2"] = stats()
+    save("replay_ring.npz", **out)
+
+
+# ---------------------------------------------------------------- eps injection
+class EpsQueue:
+    def __init__(self):
+        self.q = []
+
+    def __call__(self, shape, dtype, device):
+        e = self.q.pop(0)
+        assert tuple(e.shape) == tuple(shape), (e.shape, shape)
+        return torch.from_numpy(e).to(dtype)
+
+
+EPS = EpsQueue()
+torch.distributions.normal._standard_normal = EPS
+
+
+def named_shapes(module):
+    return [(k, tuple(v.shape)) for k, v in module.state_dict().items()]
+
+
+def load(module, seed):
+    vals = fill_params(named_shapes(module), seed)
+    module.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+
+
+def flat_params(module):
+    return np.concatenate([v.detach().numpy().ravel() for v in module.state_dict().values()])
+
+
+def make_batch(rng, B, ob, aout, ac, done_p=0.15):
+    obs = (rng.randn(B, ob) * 1.3).astype(np.float32)
+    next_obs = (rng.randn(B, ob) * 1.3).astype(np.float32)
+    act = rng.uniform(-1.2, 1.2, (B, aout)).astype(np.float32)
+    rew = rng.randn(B).astype(np.float32)
+    done = (rng.rand(B) < done_p).astype(np.int8)
+    acm = rng.uniform(-1, 1, (B, ac)).astype(np.float32)
+    return obs, next_obs, act, rew, done, acm
+
+
+# ---------------------------------------------------------------- SAC_AcM.update
+SAC_VARIANTS = {
+    # name: env, B, flags, steps, store_adam
+    "sac_hopper_paper": ("Hopper-v2", 100, dict(acm_critic=True, custom_loss=0.2, norm_closs=False,
+                                                 min_max_denormalize=True, denormalize_actor_out=True), 2, True),
+    "sac_hopper_normcl": ("Hopper-v2", 37, dict(acm_critic=True, custom_loss=0.5, norm_closs=True,
+                                                 min_max_denormalize=True, denormalize_actor_out=True), 1, False),
+    "sac_hopper_plain": ("Hopper-v2", 64, dict(acm_critic=False, custom_loss=0.0,
+                                                min_max_denormalize=False, denormalize_actor_out=False), 1, False),
+    "sac_hcheetah_paper": ("HalfCheetah-v2", 45, dict(acm_critic=True, custom_loss=0.2, norm_closs=False,
+                                                       min_max_denormalize=True, denormalize_actor_out=True), 1, False),
+}
+
+
+def gen_sac(name, env, B, flags, steps, store_adam, seed):
+    torch.manual_seed(0)
+    m = SAC_AcM(env_name=env, gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2,
+                buffer_size=1000, acm_pre_train_samples=10, acm_val_buffer_size=None,
+                update_batch_size=B, use_gpu=False, **flags)
+    ob, aout, ac = m.ob_dim, m.actor_output_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic_1": m._critic_1, "critic_2": m._critic_2,
+            "critic_1_targ": m.critic_1_targ, "critic_2_targ": m.critic_2_targ, "acm": m.acm}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    lo = -rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    mu = (rng.randn(ob) * 0.3).astype(np.float32)
+    sd = rng.uniform(0.5, 1.5, ob).astype(np.float32)
+    m.replay_buffer.min_obs, m.replay_buffer.max_obs = torch.from_numpy(lo), torch.from_numpy(hi)
+    m.replay_buffer.obs_mean, m.replay_buffer.obs_std = torch.from_numpy(mu), torch.from_numpy(sd)
+    out = dict(dims=np.array([ob, aout, ac, B]), seed=np.array(seed),
+               norm=np.stack([lo, hi, mu, sd]), actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32),
+               acm_ac_lim=np.asarray(m.acm.ac_lim, np.float32),
+               log_alpha0=np.array(float(m.log_alpha)), alpha0=np.array(m.alpha),
+               target_entropy=np.array(m.target_entropy), tau=np.array(m.tau), gamma=np.array(m.gamma))
+    ys, logps = [], []
+    orig_targ, orig_pi = m.compute_qfunc_targ, m.compute_pi_loss
+
+    def targ(*a, **k):
+        y = orig_targ(*a, **k)
+        ys.append(y.detach().numpy().copy())
+        return y
+
+    def pi(obs, sa, slp, nobs):
+        logps.append(slp.detach().numpy().copy())
+        return orig_pi(obs, sa, slp, nobs)
+
+    m.compute_qfunc_targ, m.compute_pi_loss = targ, pi
+    losses = []
+    for s in range(steps):
+        obs, next_obs, act, rew, done, acm = make_batch(rng, B, ob, aout, ac)
+        eps1 = rng.randn(B, aout).astype(np.float32)
+        eps2 = rng.randn(B, aout).astype(np.float32)
+        EPS.q = [eps1, eps2]
+        m.update(torch.from_numpy(obs), torch.from_numpy(next_obs), torch.from_numpy(act),
+                 torch.from_numpy(rew), torch.from_numpy(done), torch.from_numpy(acm))
+        assert not EPS.q
+        losses.append([m.loss.get(k, 0.0) for k in ("critic_1", "critic_2", "actor", "sac", "dist")])
+    out["y"] = np.stack(ys)
+    out["logp"] = np.stack(logps)
+    out["losses"] = np.array(losses)
+    out["log_alpha"] = np.array(float(m.log_alpha))
+    out["alpha"] = np.array(m.alpha)
+    for k, mod in nets.items():
+        if k != "acm":
+            out["post_" + k] = flat_params(mod)
+    if store_adam:
+        for k, opt, mod in (("actor", m.actor_optimizer, m._actor), ("critic_1", m.critic_1_optimizer, m._critic_1)):
+            st = [opt.state[p] for p in mod.parameters()]
+            out["m_" + k] = np.concatenate([s["exp_avg"].numpy().ravel() for s in st])
+            out["v_" + k] = np.concatenate([s["exp_avg_sq"].numpy().ravel() for s in st])
+    save(name + ".npz", **out)
+
+
+# ---------------------------------------------------------------- DDPG_AcM.update
+def gen_ddpg(seed=11):
+    torch.manual_seed(0)
+    env = "HalfCheetah-v2"
+    m = DDPG_AcM(env_name=env, gamma=0.95, actor_lr=5e-4, critic_lr=5e-4, buffer_size=1000,
+                 acm_pre_train_samples=10, acm_val_buffer_size=None, update_batch_size=50,
+                 custom_loss=1.0, norm_closs=False, acm_critic=True, min_max_denormalize=True,
+                 denormalize_actor_out=True, act_noise=0.05, use_gpu=False)
+    m.acm = BasicAcM(34, 6, False)
+    ob, aout, ac, B = m.ob_dim, m.actor_output_dim, m.ac_dim, 50
+    nets = {"actor": m._actor, "critic": m._critic, "actor_targ": m.actor_targ,
+            "critic_targ": m.critic_targ, "acm": m.acm}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    lo = -rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    m.replay_buffer.min_obs, m.replay_buffer.max_obs = torch.from_numpy(lo), torch.from_numpy(hi)
+    out = dict(dims=np.array([ob, aout, ac, B]), seed=np.array(seed), norm=np.stack([lo, hi]),
+               actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32), tau=np.array(m.tau),
+               gamma=np.array(m.gamma))
+    losses = []
+    for s in range(2):
+        obs, next_obs, act, rew, done, acm = make_batch(rng, B, ob, aout, ac)
+        m.update(torch.from_numpy(obs), torch.from_numpy(next_obs), torch.from_numpy(act),
+                 torch.from_numpy(rew), torch.from_numpy(done), torch.from_numpy(acm))
+        losses.append([m.loss.get(k, 0.0) for k in ("critic", "actor", "ddpg", "dist")])
+    out["losses"] = np.array(losses)
+    for k, mod in nets.items():
+        if k != "acm":
+            out["post_" + k] = flat_params(mod)
+    save("ddpg_hcheetah_paper.npz", **out)
+
+
+# ---------------------------------------------------------------- AcMTrainer.batch_update
+def gen_acm(seed=21):
+    torch.manual_seed(0)
+    m = SAC_AcM(env_name="Hopper-v2", acm_lr=1e-3, acm_pre_train_samples=10, acm_val_buffer_size=None,
+                buffer_size=100, use_gpu=False)
+    load(m.acm, seed)
+    rng = np.random.RandomState(seed)
+    xs, ys, ls = [], [], []
+    for s in range(3):
+        x = (rng.randn(100, 22) * 1.2).astype(np.float32)
+        y = rng.uniform(-1, 1, (100, 3)).astype(np.float32)
+        ls.append(m.batch_update(torch.from_numpy(x), torch.from_numpy(y)))
+    out = dict(seed=np.array(seed), losses=np.array(ls), post_acm=flat_params(m.acm),
+               ac_lim=np.asarray(m.acm.ac_lim, np.float32))
+    save("acm_step.npz", **out)
+
+
+# ---------------------------------------------------------------- PPO GAE / clip
+def gen_ppo(seed=31):
+    rng = np.random.RandomState(seed)
+    buf = Memory()
+    T = 0
+    gam, lam = 0.99, 0.95
+    for ep in range(6):
+        L = int(rng.randint(1, 15))
+        o = torch.from_numpy(rng.randn(1, 3).astype(np.float32))
+        prev = buf.add_obs(o)
+        for t in range(L):
+            o = torch.from_numpy(rng.randn(1, 3).astype(np.float32))
+            nxt = buf.add_obs(o)
+            end = t == L - 1
+            done = bool(end and rng.rand() < 0.5)
+            buf.add_timestep(prev, nxt, np.zeros(1), np.zeros(1), float(rng.randn()), done, end)
+            prev = nxt
+            T += 1
+        buf.end_rollout()
+    buf.update_obs_mean_std()
+    w = np.array([0.7, -1.1, 0.4], np.float32)
+
+    def critic_func(obs, *a):
+        if len(obs.shape) == 2:
+            return obs @ torch.from_numpy(w)
+        return (obs @ torch.from_numpy(w)).reshape(())
+
+    ppo = PPO(env_name="Pendulum-v0", gamma=gam, gae_lambda=lam)
+    ppo._critic = critic_func
+    q = ppo.calculate_q_val(buf)
+    adv = ppo.calculate_gae(buf, q)
+    out = dict(obs=buf.norm_obs.numpy(), next_obs=buf.norm_next_obs.numpy(),
+               rew=np.array(buf.rewards, np.float32), done=np.array(buf.done, np.float32),
+               end=np.array(buf.end, np.float32), w=w, gamma=np.array(gam), lam=np.array(lam),
+               q=q.numpy(), adv=adv.numpy())
+    lp_old = rng.randn(64).astype(np.float32)
+    lp_new = (lp_old + 0.3 * rng.randn(64)).astype(np.float32)
+    A = rng.randn(64).astype(np.float32)
+    ppo_e = PPO(env_name="Pendulum-v0", epsilon=0.2)
+    cl = ppo_e._clip_loss(torch.from_numpy(lp_old), torch.from_numpy(lp_new), torch.from_numpy(A))
+    out.update(clip_lp_old=lp_old, clip_lp_new=lp_new, clip_adv=A, clip_loss=np.array(cl.item()))
+    save("ppo_gae_clip.npz", **out)
+
+
+if __name__ == "__main__":
+    gen_randint()
+    gen_replay()
+    for i, (name, (env, B, flags, steps, adam)) in enumerate(SAC_VARIANTS.items()):
+        gen_sac(name, env, B, flags, steps, adam, seed=1 + i)
+    gen_ddpg()
+    gen_acm()
+    gen_ppo()

@@ -1,0 +1,76 @@
+"""Rebuilds the inputs of the golden fixtures (tests/golden/make_golden.py)
+from their numpy seeds, so fixtures only carry expected outputs."""
+import os
+
+import numpy as np
+import torch
+
+from weights import fill_params
+from oracle import nets
+from oracle.nets import Norm
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+SAC_CASES = {
+    "sac_hopper_paper": dict(seed=1, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max=True, steps=2),
+    "sac_hopper_normcl": dict(seed=2, acm_critic=True, custom_loss=0.5, norm_closs=True, min_max=True, steps=1),
+    "sac_hopper_plain": dict(seed=3, acm_critic=False, custom_loss=0.0, norm_closs=False, min_max=False, steps=1),
+    "sac_hcheetah_paper": dict(seed=4, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max=True, steps=1),
+}
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def make_batch(rng, B, ob, aout, ac, done_p=0.15):
+    obs = (rng.randn(B, ob) * 1.3).astype(np.float32)
+    next_obs = (rng.randn(B, ob) * 1.3).astype(np.float32)
+    act = rng.uniform(-1.2, 1.2, (B, aout)).astype(np.float32)
+    rew = rng.randn(B).astype(np.float32)
+    done = (rng.rand(B) < done_p).astype(np.int8)
+    acm = rng.uniform(-1, 1, (B, ac)).astype(np.float32)
+    return obs, next_obs, act, rew, done, acm
+
+
+def sac_case(name):
+    """Returns (cfg, fixture, params{net: {name: arr}}, norm, steps[list of (batch, eps1, eps2)])."""
+    cfg = SAC_CASES[name]
+    fx = load(name)
+    ob, aout, ac, B = (int(v) for v in fx["dims"])
+    seed = cfg["seed"]
+    cin = ob + (ac if cfg["acm_critic"] else aout)
+    layouts = {"actor": nets.sac_actor_layout(ob, aout), "critic_1": nets.critic_layout(cin),
+               "critic_2": nets.critic_layout(cin), "critic_1_targ": nets.critic_layout(cin),
+               "critic_2_targ": nets.critic_layout(cin), "acm": nets.acm_layout(2 * ob, ac)}
+    params = {k: fill_params(lay, seed * 100 + i) for i, (k, lay) in enumerate(layouts.items())}
+    rng = np.random.RandomState(seed)
+    lo = -rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    mu = (rng.randn(ob) * 0.3).astype(np.float32)
+    sd = rng.uniform(0.5, 1.5, ob).astype(np.float32)
+    norm = Norm(cfg["min_max"], *(torch.from_numpy(v) for v in (lo, hi, mu, sd)))
+    steps = []
+    for _ in range(cfg["steps"]):
+        batch = make_batch(rng, B, ob, aout, ac)
+        e1 = rng.randn(B, aout).astype(np.float32)
+        e2 = rng.randn(B, aout).astype(np.float32)
+        steps.append((batch, e1, e2))
+    return cfg, fx, params, layouts, norm, steps
+
+
+def ddpg_case():
+    from oracle.nets import basic_acm_layout, critic_layout, ddpg_actor_layout
+    fx = load("ddpg_hcheetah_paper")
+    ob, aout, ac, B = (int(v) for v in fx["dims"])
+    seed = int(fx["seed"])
+    layouts = {"actor": ddpg_actor_layout(ob, aout), "critic": critic_layout(ob + ac),
+               "actor_targ": ddpg_actor_layout(ob, aout), "critic_targ": critic_layout(ob + ac),
+               "acm": basic_acm_layout(2 * ob, ac)}
+    params = {k: fill_params(lay, seed * 100 + i) for i, (k, lay) in enumerate(layouts.items())}
+    rng = np.random.RandomState(seed)
+    lo = -rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2.0, ob).astype(np.float32)
+    norm = Norm(True, torch.from_numpy(lo), torch.from_numpy(hi))
+    batches = [make_batch(rng, B, ob, aout, ac) for _ in range(2)]
+    return fx, params, layouts, norm, batches

@@ -1,0 +1,181 @@
+"""Pins the oracle (CPU restatement) against the golden vectors produced by the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from golden_cases import SAC_CASES, ddpg_case, load, sac_case
+from oracle import nets
+from oracle.acm import OracleAcmTrainer
+from oracle.ddpg_acm import OracleDdpgAcm
+from oracle.ppo import clip_loss, gae_affine, gae_loop, q_val
+from oracle.replay import OracleReplay
+from oracle.rng import OracleMT
+from oracle.sac_acm import OracleSacAcm
+from weights import fill_params
+
+
+def test_mt19937_randint_matches_numpy_golden():
+    fx = load("mt19937_randint")
+    for s, n, vals in zip(fx["seeds"], fx["ns"], fx["vals"]):
+        got = OracleMT(int(s)).randint(int(n), vals.shape[0])
+        np.testing.assert_array_equal(got, vals)
+    mt = OracleMT(int(fx["seq_seed"]))
+    for n, vals in zip(fx["seq_n"], fx["seq_vals"]):
+        np.testing.assert_array_equal(mt.randint(int(n), len(vals)), vals)
+
+
+def test_mt19937_randint_matches_installed_numpy():
+    for seed, n in ((3, 977), (2**32 - 1, 2**32), (99, 1)):
+        np.testing.assert_array_equal(OracleMT(seed).randint(n, 1000),
+                                      np.random.RandomState(seed).randint(0, n, 1000))
+
+
+def replay_from_fixture(fx, tag):
+    p = "r%s_" % tag
+    size, ob, aout, ac = (int(v) for v in fx[p + "dims"])
+    rb = OracleReplay(size, ob, aout, ac)
+    oi = si = 0
+    states = []
+    for kind, a, b in fx[p + "ops"]:
+        if kind == 0:
+            assert rb.add_obs(fx[p + "obs"][oi]) == a
+            oi += 1
+        else:
+            rb.add_acm_action(fx[p + "acm"][si])
+            assert rb.add_obs(fx[p + "obs"][oi]) == b
+            oi += 1
+            rb.add_timestep(a, b, fx[p + "act"][si], fx[p + "rew"][si], fx[p + "done"][si], fx[p + "end"][si])
+            si += 1
+            states.append((rb.obs_idx, rb.ts_idx, rb.current_len))
+    return rb, p, states
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_replay_ring_and_sampling(tag):
+    fx = load("replay_ring")
+    rb, p, states = replay_from_fixture(fx, tag)
+    np.testing.assert_array_equal(np.array(states), fx[p + "states"])
+    L = rb.current_len
+    np.testing.assert_array_equal(rb._obs_idx[:L], fx[p + "obs_idx"])
+    np.testing.assert_array_equal(rb._next_obs_idx[:L], fx[p + "next_obs_idx"])
+    for s in (0, 5):
+        q = p + "s%d_" % s
+        (o, no, a, r, d, acm), idx = rb.sample_batch(33, OracleMT(s))
+        np.testing.assert_array_equal(idx, fx[q + "idx"])
+        for got, key in ((o, "obs"), (no, "next_obs"), (a, "act"), (r, "rew"), (d, "done"), (acm, "acm")):
+            np.testing.assert_array_equal(got, fx[q + key])
+    (o, no, acm), _ = rb.sample_acm_batch(17, OracleMT(9))
+    np.testing.assert_array_equal(o, fx[p + "acmb_obs"])
+    np.testing.assert_array_equal(acm, fx[p + "acmb_acm"])
+    for key in ("st1", "st2"):
+        rb.update_obs_mean_std()
+        nan = np.full(rb.ob, np.nan, np.float32)
+        mx = nan if rb.max_obs is None else rb.max_obs
+        mn = nan if rb.min_obs is None else rb.min_obs
+        np.testing.assert_array_equal(np.stack([rb.obs_mean, rb.obs_std, mx, mn]), fx[p + key])
+        rb._obs[rb._obs_idx[: rb.current_len]] *= 0.5
+
+
+def test_q6_trace_from_survey():
+    fx = load("replay_ring")
+    rb, _, _ = replay_from_fixture(fx, "a")
+    assert list(zip(rb._obs_idx[:8], rb._next_obs_idx[:8])) == [
+        (0, 1), (2, 3), (3, 4), (4, 5), (6, 7), (7, 8), (8, 9), (9, 0)]
+    assert len(rb) == 8
+
+
+@pytest.mark.parametrize("name", list(SAC_CASES))
+def test_sac_acm_update_matches_reference(name):
+    cfg, fx, params, layouts, norm, steps = sac_case(name)
+    ob, aout, ac, B = (int(v) for v in fx["dims"])
+    o = OracleSacAcm(ob, aout, ac, acm_critic=cfg["acm_critic"], custom_loss=cfg["custom_loss"],
+                     norm_closs=cfg["norm_closs"], norm=norm, actor_lim=fx["actor_ac_lim"],
+                     acm_lim=fx["acm_ac_lim"], gamma=float(fx["gamma"]), tau=float(fx["tau"]),
+                     alpha=float(fx["alpha0"]), target_entropy=float(fx["target_entropy"]), params=params)
+    for i, (batch, e1, e2) in enumerate(steps):
+        losses = o.update(*batch, e1, e2)
+        np.testing.assert_allclose(o.last["y"].numpy(), fx["y"][i], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(o.last["logp"].numpy(), fx["logp"][i], rtol=1e-6, atol=1e-5)
+        got = [losses[k] for k in ("critic_1", "critic_2", "actor", "sac", "dist")]
+        np.testing.assert_allclose(got, fx["losses"][i], rtol=1e-6, atol=1e-7)
+    for k in ("actor", "critic_1", "critic_2", "critic_1_targ", "critic_2_targ"):
+        np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-6, atol=1e-7, err_msg=k)
+    assert o.alpha == pytest.approx(float(fx["alpha"]), rel=1e-12)
+    if "m_actor" in fx:
+        for k in ("actor", "critic_1"):
+            np.testing.assert_allclose(torch.cat([m.reshape(-1) for m in o.opt[k].m]).numpy(), fx["m_" + k],
+                                       rtol=1e-5, atol=1e-9)
+            np.testing.assert_allclose(torch.cat([v.reshape(-1) for v in o.opt[k].v]).numpy(), fx["v_" + k],
+                                       rtol=1e-5, atol=1e-12)
+
+
+def test_ddpg_acm_update_matches_reference():
+    fx, params, layouts, norm, batches = ddpg_case()
+    ob, aout, ac, B = (int(v) for v in fx["dims"])
+    o = OracleDdpgAcm(ob, aout, ac, norm=norm, actor_lim=fx["actor_ac_lim"], gamma=float(fx["gamma"]),
+                      tau=float(fx["tau"]), params=params)
+    for i, batch in enumerate(batches):
+        losses = o.update(*batch)
+        np.testing.assert_allclose([losses[k] for k in ("critic", "actor", "ddpg", "dist")], fx["losses"][i],
+                                   rtol=1e-6, atol=1e-7)
+    for k in ("actor", "critic", "actor_targ", "critic_targ"):
+        np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_acm_batch_update_matches_reference():
+    fx = load("acm_step")
+    seed = int(fx["seed"])
+    lay = nets.acm_layout(22, 3)
+    o = OracleAcmTrainer(22, 3, lr=1e-3, ac_lim=fx["ac_lim"], params=fill_params(lay, seed))
+    rng = np.random.RandomState(seed)
+    for i in range(3):
+        x = (rng.randn(100, 22) * 1.2).astype(np.float32)
+        y = rng.uniform(-1, 1, (100, 3)).astype(np.float32)
+        assert o.batch_update(x, y) == pytest.approx(float(fx["losses"][i]), rel=1e-6)
+    np.testing.assert_allclose(o.flat(), fx["post_acm"], rtol=1e-6, atol=1e-8)
+
+
+def test_gae_and_clip_match_reference():
+    fx = load("ppo_gae_clip")
+    w = fx["w"]
+    v_next = fx["next_obs"] @ w
+    v = fx["obs"] @ w
+    q = q_val(fx["rew"], fx["done"], v_next, float(fx["gamma"]))
+    np.testing.assert_allclose(q, fx["q"], rtol=1e-6, atol=1e-6)
+    delta = q - v
+    adv = gae_loop(delta, fx["done"], fx["end"], v_next, float(fx["gamma"]), float(fx["lam"]))
+    np.testing.assert_allclose(adv, fx["adv"], rtol=1e-5, atol=1e-5)
+    adv2 = gae_affine(delta, fx["done"], fx["end"], v_next, float(fx["gamma"]), float(fx["lam"]))
+    np.testing.assert_allclose(adv2, fx["adv"], rtol=1e-5, atol=1e-5)
+    assert clip_loss(fx["clip_lp_old"], fx["clip_lp_new"], fx["clip_adv"]) == pytest.approx(
+        float(fx["clip_loss"]), rel=1e-6)
+
+
+def test_gae_reference_kat():
+    """KAT of rltoolkit/algorithms/ppo/test/test_ppo.py:79-134 (gamma = lambda = 0.5)."""
+    rew = np.array(list(range(10)) + [1, 2], np.float64)
+    done = np.zeros(12)
+    done[[3, 6, 11]] = 1
+    end = done.copy()
+    end[9] = 1
+    obs = np.ones((12, 2)) * 5  # every obs 5 -> critic 10
+    v = obs[:, 0] * 2
+    q = q_val(rew, done, v, 0.5)
+    np.testing.assert_array_equal(q, [5, 6, 7, 3, 9, 10, 6, 12, 13, 14, 6, 2])
+    adv = gae_loop(q - v, done, end, v, 0.5, 0.5)
+    np.testing.assert_almost_equal(adv, [-6.2969, -5.1875, -4.75, -7, -1.25, -1, -4, 3.1562, 4.625, 6.5, -6, -8],
+                                   decimal=4)
+
+
+@pytest.mark.parametrize("case", [
+    ([-2.3, -5, -1.4, -1.5], [-2.3, -5, -1.4, -1.5], [1, 2.0, 3.0, 4.0], -2.5),
+    ([-1.0], [-1.0], [-1.0], 1),
+    ([-1.0], [-2.0], [-1.0], 0.8),
+    ([-2.0], [-1.0], [1.0], -1.2),
+    ([-1.0], [-2.0], [1.0], -0.3679),
+])
+def test_clip_loss_reference_kat(case):
+    """KATs of rltoolkit/algorithms/ppo/test/test_ppo.py:34-76."""
+    old, new, adv, want = case
+    assert clip_loss(np.float32(old), np.float32(new), np.float32(adv)) == pytest.approx(want, rel=1e-4)

@@ -1,0 +1,207 @@
+/* spprl.h — C-ABI of the MI355X-native SPP-RL hot path (libspprl.so).
+ *
+ * Replaces the Python-method boundary of rltoolkit (raznem/spp-rl @ v0) for the
+ * off-policy SPP rollout -> replay -> update loop.  Each entry
+ * point cites the reference interface it stands in for.
+ *
+ * Conventions
+ *   - Every function returns sppStatus (0 = OK); sppGetLastError() gives text.
+ *     No C++ exception crosses this boundary.
+ *   - Device buffers are CALLER-OWNED (e.g. torch tensors); handles own only
+ *     internal scratch.  All device work is stream-ordered on the hipStream_t
+ *     passed in (void* here so the header needs no HIP include) and async:
+ *     losses are written to device memory, nothing synchronises the host.
+ *   - One host thread per handle; one process per GPU.
+ *   - Matrices are row-major, float32, nn.Linear layout ([out][in]); each
+ *     network's parameters are ONE flat buffer in state_dict order (layouts
+ *     in DESIGN.md §Data layout).
+ */
+#ifndef SPPRL_H
+#define SPPRL_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int sppStatus;
+enum {
+  SPP_OK = 0,
+  SPP_E_INVALID_ARG = 1,
+  SPP_E_SHAPE = 2,
+  SPP_E_OOM = 3,
+  SPP_E_HIP = 4,
+  SPP_E_STATE = 5
+};
+
+/* Text of the last error raised on this thread ("" if none). */
+const char* sppGetLastError(void);
+int sppGetVersion(void);
+
+/* ------------------------------------------------------------------ RNG
+ * numpy legacy MT19937 stream: np.random.seed(s); np.random.randint(0, high, n)
+ * (index draw of rltoolkit/buffer/replay_buffer.py:234, :418).  Host-side,
+ * bit-exact.  */
+typedef struct sppMT19937* sppMTHandle;
+sppStatus sppMTCreate(sppMTHandle* out, uint32_t seed);
+sppStatus sppMTRandint(sppMTHandle h, int64_t high, int64_t n, int64_t* out_host);
+sppStatus sppMTDestroy(sppMTHandle h);
+
+/* Counter-based (Philox4x32-10) device streams for the vectorised path.
+ * Normal draws by Box-Muller; uniform ints by masked rejection. */
+sppStatus sppRandNormal(float* out_dev, int64_t n, uint64_t seed, uint64_t offset, void* stream);
+sppStatus sppRandIndex(int64_t* out_dev, int64_t n, int64_t high, uint64_t seed, uint64_t offset,
+                       void* stream);
+
+/* ------------------------------------------------------------------ replay ring
+ * BufferAcMOffPolicy (rltoolkit/buffer/replay_buffer.py:303-401) with the
+ * MetaReplayBuffer obs-index ring (:7-96): obs stored once per slot, each
+ * timestep keeps (obs_idx, next_obs_idx); wrap rule Q6 reproduced exactly.
+ * Storage lives in HBM, fp32 (exact: every stored value is an fp32 tensor
+ * value, the reference's fp64 store round-trips it unchanged — Q5). */
+typedef struct sppReplay* sppReplayHandle;
+sppStatus sppReplayCreate(sppReplayHandle* out, int64_t capacity, int ob, int aout, int ac, int device);
+sppStatus sppReplayDestroy(sppReplayHandle h);
+/* MetaReplayBuffer.add_obs (:56-60) for E rows at once; slots returned to host. */
+sppStatus sppReplayAddObs(sppReplayHandle h, const float* obs_dev /*[E][ob]*/, int E,
+                          int64_t* slots_host_out /*[E]*/, void* stream);
+/* add_acm_action (:332-333) + add_timestep (:65-75) + addition (:133-137), E
+ * transitions applied in env order (E = 1 is the reference exactly). */
+sppStatus sppReplayAddStep(sppReplayHandle h, const int64_t* prev_host, const int64_t* next_host, int E,
+                           const float* act_dev /*[E][aout]*/, const float* acm_dev /*[E][ac]*/,
+                           const float* rew_dev /*[E]*/, const uint8_t* done_dev /*[E]*/,
+                           const uint8_t* end_dev /*[E]*/, void* stream);
+/* obs_idx, ts_idx, current_len */
+sppStatus sppReplayState(sppReplayHandle h, int64_t* obs_idx, int64_t* ts_idx, int64_t* len);
+sppStatus sppReplayReset(sppReplayHandle h); /* reset_idx (:32-35) */
+/* _sample_batch / sample_batch gather (:233-261, :385-398) for given indices,
+ * reference row-major layout: obs, next_obs [B][ob], act [B][aout], rew [B],
+ * done [B] int8, acm [B][ac].  Any output pointer may be NULL. */
+sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx_dev, int B, float* obs, float* next_obs,
+                          float* act, float* rew, int8_t* done, float* acm, void* stream);
+/* update_obs_mean_std (:83-96): fp64 mean / std(ddof=0) over the live obs,
+ * exact np.percentile(.., 99 / 1, linear) by radix select, running max/min.
+ * Skipped (returns *updated = 0) when len <= 10.  max/min are read-modify-
+ * written (first_update != 0 overwrites them). */
+sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
+                            int first_update, void* stream);
+/* Raw device pointers of the ring (for the fused sample+update path). */
+typedef struct {
+  float* obs;          /* [capacity][ob]    */
+  int64_t* obs_idx;    /* [capacity]        */
+  int64_t* next_idx;   /* [capacity]        */
+  float* act;          /* [capacity][aout]  */
+  float* acm;          /* [capacity][ac]    */
+  float* rew;          /* [capacity]        */
+  uint8_t* done;       /* [capacity]        */
+  uint8_t* end;        /* [capacity]        */
+} sppReplayView;
+sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);
+
+/* ------------------------------------------------------------------ agent */
+enum { SPP_ALGO_SAC_ACM = 1 };
+enum { /* network ids for parameter binding (SAC_AcM) */
+  SPP_NET_ACTOR = 0, SPP_NET_CRITIC1 = 1, SPP_NET_CRITIC2 = 2,
+  SPP_NET_CRITIC1_TARG = 3, SPP_NET_CRITIC2_TARG = 4, SPP_NET_ACM = 5, SPP_NET_COUNT = 6
+};
+
+typedef struct {
+  int algo;                 /* SPP_ALGO_SAC_ACM */
+  int ob, aout, ac;         /* obs dim, actor output dim (= len(acm_ob_idx) = ob), env action dim */
+  int acm_critic;           /* critics see ACM(s, denorm a) (ac) instead of denorm a (aout) */
+  int min_max_denormalize;  /* memory.py:107-121 min-max vs z-score */
+  int norm_closs;           /* sac_acm.py:80-84 */
+  float custom_loss;        /* sac_acm.py:78-86 */
+  float gamma, tau;
+  float actor_lr, critic_lr, alpha_lr, acm_lr;
+  float target_entropy;     /* sac.py:104-106: -env ac_dim (Q4) */
+  int max_batch;            /* workspace sizing (update batch B) */
+} sppAgentConfig;
+
+typedef struct sppAgent* sppAgentHandle;
+sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int device);
+sppStatus sppAgentDestroy(sppAgentHandle h);
+/* Number of float32 parameters of network `net` (state_dict order). */
+sppStatus sppAgentNetSize(sppAgentHandle h, int net, int64_t* n);
+/* Bind caller-owned flat buffers.  grad / exp_avg / exp_avg_sq may be NULL for
+ * target and frozen networks. */
+sppStatus sppAgentBindNet(sppAgentHandle h, int net, float* params, float* grads, float* exp_avg,
+                          float* exp_avg_sq);
+/* Constant vectors: actor_ac_lim [aout] (acm.py:102-108), acm ac_lim [ac]. Host arrays, copied. */
+sppStatus sppAgentSetLimits(sppAgentHandle h, const float* actor_lim_host, const float* acm_lim_host);
+/* Replay normalizer (caller-owned device vectors [ob]; NULL allowed for unused pair). */
+sppStatus sppAgentBindNormalizer(sppAgentHandle h, const float* min_obs, const float* max_obs,
+                                 const float* obs_mean, const float* obs_std);
+/* Temperature state: alpha_state_dev = double[4] {log_alpha, exp_avg, exp_avg_sq, alpha};
+ * alpha_f32_dev = float[1] (the python float self.alpha, sac_acm.py:159). */
+sppStatus sppAgentBindAlpha(sppAgentHandle h, double* alpha_state_dev, float* alpha_f32_dev);
+/* Adam step counters (host). */
+sppStatus sppAgentSetSteps(sppAgentHandle h, int64_t actor_step, int64_t critic_step, int64_t alpha_step,
+                           int64_t acm_step);
+sppStatus sppAgentGetSteps(sppAgentHandle h, int64_t* steps4);
+
+/* Update batch in the reference row-major layout (sample_batch output). */
+typedef struct {
+  int B;
+  const float* obs;       /* [B][ob]   */
+  const float* next_obs;  /* [B][ob]   */
+  const float* action;    /* [B][aout] (unused when acm_critic) */
+  const float* reward;    /* [B]       */
+  const int8_t* done;     /* [B]       */
+  const float* acm_action;/* [B][ac]   */
+} sppBatch;
+
+/* Loss vector written by the update (device float[8]):
+ * {critic_1, critic_2, actor, sac, dist, alpha_loss, alpha, 0}. */
+#define SPP_NUM_LOSSES 8
+
+/* SAC_AcM.update (rltoolkit/acm/off_policy/sac_acm.py:89-162): one full grad
+ * step.  eps_next / eps_cur [B][aout] are the standard-normal draws of the two
+ * rsample calls (sac_acm.py:44, :137); NULL -> drawn on device from (seed, step). */
+sppStatus sppSacAcmUpdate(sppAgentHandle h, const sppBatch* batch, const float* eps_next, const float* eps_cur,
+                          float* losses_dev, void* stream);
+/* The same step split at its two exchange points for data-parallel training:
+ * grads -> (caller all-reduces the flat grad buffers, averaging) -> apply. */
+sppStatus sppSacAcmCriticGrads(sppAgentHandle h, const sppBatch* batch, const float* eps_next,
+                               float* losses_dev, void* stream);
+sppStatus sppSacAcmCriticApply(sppAgentHandle h, void* stream);
+sppStatus sppSacAcmActorGrads(sppAgentHandle h, const float* eps_cur, float* losses_dev, void* stream);
+sppStatus sppSacAcmActorApply(sppAgentHandle h, float* losses_dev, void* stream);
+/* Fused replay sample + gather into the agent's staging area (device indices). */
+sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int B,
+                                  void* stream);
+/* Update on the staged batch (after sppAgentStageFromReplay), eps drawn on
+ * device from (seed, counter). */
+sppStatus sppSacAcmUpdateStaged(sppAgentHandle h, uint64_t seed, uint64_t counter, float* losses_dev,
+                                void* stream);
+
+/* AcMTrainer.batch_update (rltoolkit/acm/acm.py:246-258): x [B][2ob], y [B][ac]
+ * -> MSE loss (device float) and one Adam step on the bound ACM net. */
+sppStatus sppAcmRegressStep(sppAgentHandle h, const float* x, const float* y, int B, float* loss_dev,
+                            void* stream);
+
+/* Rollout action (rltoolkit/acm/off_policy/ddpg_acm.py:40-50 noise_action +
+ * off_policy.py:50-54 initial_act + :89-106 process_action):
+ *   mode 0 random : a = lim * eps                      (initial_act)
+ *   mode 1 noisy  : a = clip(tanh(mu + sigma*eps)*lim + act_noise*lim*noise, +-1.1 lim)
+ *   mode 2 det    : a = clip(tanh(mu)*lim, +-1.1 lim)
+ * then a_d = denormalize(a) if denormalize_actor_out, env action = ACM(cat(obs, a_d)).
+ * target_state_out receives a_d (what the buffer stores as `action`). */
+sppStatus sppPolicyAct(sppAgentHandle h, const float* obs /*[E][ob]*/, int E, const float* eps /*[E][aout]*/,
+                       const float* noise /*[E][aout]*/, float act_noise, int mode, int denormalize_actor_out,
+                       float* target_state_out /*[E][aout]*/, float* env_action_out /*[E][ac]*/, void* stream);
+
+/* Synthetic fixed-shape env (SURVEY.md Appendix A SynthEnv), E instances in
+ * lockstep on device: s' = tanh(A s) + 0.1*resize(a, ob); r = -|a|^2 + s'[0]. */
+sppStatus sppSynthEnvStep(const float* A /*[ob][ob]*/, const float* obs /*[E][ob]*/, const float* action /*[E][ac]*/,
+                          int E, int ob, int ac, float* next_obs, float* reward, void* stream);
+
+/* Debug / layout check: y = act(x W^T + b) through the MFMA register-tile path.
+ * x [B][K], W [N][K], b [N], y [B][N]; act 0 none, 1 relu, 2 tanh. */
+sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,
+                        void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPPRL_H */

@@ -25,7 +25,9 @@ class OracleAcmTrainer:
         if y.dim() < 2:
             y = y.reshape(len(y), -1)
         loss = F.mse_loss(nets.acm(self.p, x, self.lim), y)
-        self.opt.step(torch.autograd.grad(loss, list(self.p.values())))
+        g = torch.autograd.grad(loss, list(self.p.values()))
+        self.last_grad = torch.cat([t.reshape(-1) for t in g]).numpy()
+        self.opt.step(g)
         return loss.item()
 
     def flat(self):

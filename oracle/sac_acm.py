@@ -65,11 +65,14 @@ class OracleSacAcm:
             y = reward + self.gamma * (1 - done) * (torch.min(q1t, q2t) - self.alpha * lp2)
         if self.acm_critic:
             action = acm_action
+        grads = {}
         for k in ("critic_1", "critic_2"):
             q = nets.sac_critic(P[k], obs, action)
             loss = F.mse_loss(q, y)
             losses[k] = loss.item()
-            self.opt[k].step(torch.autograd.grad(loss, list(P[k].values())))
+            g = torch.autograd.grad(loss, list(P[k].values()))
+            grads[k] = torch.cat([x.reshape(-1) for x in g]).numpy()
+            self.opt[k].step(g)
         a, lp, _ = nets.sac_actor(P["actor"], obs, self.actor_lim, eps_cur)
         ad = self.norm.denormalize(a)
         ca = self._acm(torch.cat([obs, ad], axis=1)) if self.acm_critic else ad
@@ -86,7 +89,9 @@ class OracleSacAcm:
             losses["dist"] = dist.item()
             loss = loss + self.custom_loss * dist
         losses["actor"] = loss.item()
-        self.opt["actor"].step(torch.autograd.grad(loss, list(P["actor"].values())))
+        g = torch.autograd.grad(loss, list(P["actor"].values()))
+        grads["actor"] = torch.cat([x.reshape(-1) for x in g]).numpy()
+        self.opt["actor"].step(g)
         with torch.no_grad():
             for c, tg in (("critic_1", "critic_1_targ"), ("critic_2", "critic_2_targ")):
                 for n in P[c]:
@@ -97,7 +102,7 @@ class OracleSacAcm:
         self.opt_alpha.step(torch.autograd.grad(alpha_loss, [self.log_alpha]))
         self.alpha = self.log_alpha.exp().item()
         losses["alpha_loss"] = alpha_loss.item()
-        self.last = {"y": y, "logp": lpd}
+        self.last = {"y": y, "logp": lpd, "grads": grads}
         return losses
 
     def flat(self, k):

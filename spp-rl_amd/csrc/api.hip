@@ -1,0 +1,1085 @@
+// libspprl C-ABI implementation (unity build: kernels included below).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/spprl.h"
+#include "internal.h"
+#include "replay.h"
+#include "sac_kernels.h"
+
+#include "dw.hip"
+#include "optim.hip"
+#include "replay.hip"
+#include "sac.hip"
+
+namespace spp {
+
+static thread_local std::string g_err;
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+const char* get_error() { return g_err.c_str(); }
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ================================================================== MT19937 (numpy legacy)
+struct MT {
+  uint32_t mt[624];
+  int mti;
+  void seed(uint32_t s) {
+    mt[0] = s;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    mti = 624;
+  }
+  uint32_t next() {
+    if (mti >= 624) {
+      for (int k = 0; k < 624; k++) {
+        uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+        mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      mti = 0;
+    }
+    uint32_t y = mt[mti++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+};
+
+}  // namespace spp
+
+struct sppMT19937 {
+  spp::MT mt;
+};
+
+using namespace spp;
+
+// ================================================================== replay handle
+struct sppReplay {
+  ReplayDev d{};
+  int device = 0;
+  int64_t obs_idx = 0, ts_idx = 0, len = 0;
+  // pinned ring for per-step index uploads
+  static constexpr int kRing = 4;
+  int64_t* pinned[kRing] = {};
+  int64_t* dev_meta[kRing] = {};
+  hipEvent_t ev[kRing] = {};
+  int ring_cap = 0, ring_pos = 0;
+  // obs-stats scratch
+  double* st_part = nullptr;
+  double* st_mean = nullptr;
+  double* st_std = nullptr;
+  uint32_t* st_state = nullptr;
+  uint32_t* st_hist = nullptr;
+};
+
+extern "C" {
+
+const char* sppGetLastError(void) { return get_error(); }
+int sppGetVersion(void) { return 1; }
+
+sppStatus sppMTCreate(sppMTHandle* out, uint32_t seed) {
+  SPP_REQUIRE(out, SPP_E_INVALID_ARG, "null out");
+  auto* h = new sppMT19937;
+  h->mt.seed(seed);
+  *out = h;
+  return SPP_OK;
+}
+sppStatus sppMTRandint(sppMTHandle h, int64_t high, int64_t n, int64_t* out) {
+  SPP_REQUIRE(h && out && high >= 1 && high <= (int64_t)1 << 32, SPP_E_INVALID_ARG, "randint: bad args (high=%lld)",
+              (long long)high);
+  const uint64_t rng = (uint64_t)(high - 1);
+  if (rng == 0) {
+    for (int64_t i = 0; i < n; ++i) out[i] = 0;
+    return SPP_OK;
+  }
+  uint64_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t v;
+    do { v = h->mt.next() & (uint32_t)mask; } while (v > rng);
+    out[i] = v;
+  }
+  return SPP_OK;
+}
+sppStatus sppMTDestroy(sppMTHandle h) {
+  delete h;
+  return SPP_OK;
+}
+
+sppStatus sppRandNormal(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream) {
+  SPP_REQUIRE(out || n == 0, SPP_E_INVALID_ARG, "null out");
+  if (n == 0) return SPP_OK;
+  const int64_t groups = (n + 3) / 4;
+  hipLaunchKernelGGL(k_rand_normal, dim3(cdiv(groups, 256)), dim3(256), 0, S(stream), out, n, seed, offset);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+sppStatus sppRandIndex(int64_t* out, int64_t n, int64_t high, uint64_t seed, uint64_t offset, void* stream) {
+  SPP_REQUIRE((out || n == 0) && high >= 1, SPP_E_INVALID_ARG, "bad args");
+  if (n == 0) return SPP_OK;
+  hipLaunchKernelGGL(k_rand_index, dim3(cdiv(n, 256)), dim3(256), 0, S(stream), out, n, high, seed, offset);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// ------------------------------------------------------------------ replay
+sppStatus sppReplayCreate(sppReplayHandle* out, int64_t cap, int ob, int aout, int ac, int device) {
+  SPP_REQUIRE(out && cap > 0 && ob > 0 && aout > 0 && ac > 0, SPP_E_INVALID_ARG, "replay create: bad args");
+  SPP_CHECK_HIP(hipSetDevice(device));
+  auto* h = new sppReplay;
+  h->device = device;
+  ReplayDev& d = h->d;
+  d.cap = cap;
+  d.ob = ob;
+  d.aout = aout;
+  d.ac = ac;
+  hipError_t e = hipSuccess;
+  e = e ? e : hipMalloc(&d.obs, sizeof(float) * cap * ob);
+  e = e ? e : hipMalloc(&d.obs_idx, sizeof(int64_t) * cap);
+  e = e ? e : hipMalloc(&d.next_idx, sizeof(int64_t) * cap);
+  e = e ? e : hipMalloc(&d.act, sizeof(float) * cap * aout);
+  e = e ? e : hipMalloc(&d.acm, sizeof(float) * cap * ac);
+  e = e ? e : hipMalloc(&d.rew, sizeof(float) * cap);
+  e = e ? e : hipMalloc(&d.done, cap);
+  e = e ? e : hipMalloc(&d.end, cap);
+  e = e ? e : hipMemset(d.obs, 0, sizeof(float) * cap * ob);
+  e = e ? e : hipMemset(d.obs_idx, 0, sizeof(int64_t) * cap);
+  e = e ? e : hipMemset(d.next_idx, 0, sizeof(int64_t) * cap);
+  if (e != hipSuccess) {
+    set_error("replay alloc (%lld x %d): %s", (long long)cap, ob, hipGetErrorString(e));
+    delete h;
+    return SPP_E_OOM;
+  }
+  for (int i = 0; i < sppReplay::kRing; ++i) SPP_CHECK_HIP(hipEventCreateWithFlags(&h->ev[i], hipEventDisableTiming));
+  *out = h;
+  return SPP_OK;
+}
+
+sppStatus sppReplayDestroy(sppReplayHandle h) {
+  if (!h) return SPP_OK;
+  hipSetDevice(h->device);
+  hipDeviceSynchronize();
+  ReplayDev& d = h->d;
+  hipFree(d.obs); hipFree(d.obs_idx); hipFree(d.next_idx); hipFree(d.act); hipFree(d.acm);
+  hipFree(d.rew); hipFree(d.done); hipFree(d.end);
+  for (int i = 0; i < sppReplay::kRing; ++i) {
+    if (h->pinned[i]) hipHostFree(h->pinned[i]);
+    if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
+    hipEventDestroy(h->ev[i]);
+  }
+  hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_std); hipFree(h->st_state); hipFree(h->st_hist);
+  delete h;
+  return SPP_OK;
+}
+
+sppStatus sppReplayAddObs(sppReplayHandle h, const float* obs, int E, int64_t* slots, void* stream) {
+  SPP_REQUIRE(h && obs && E > 0 && E <= h->d.cap, SPP_E_INVALID_ARG, "add_obs: bad args");
+  const int64_t base = h->obs_idx;
+  hipLaunchKernelGGL(k_replay_add_obs, dim3(cdiv((int64_t)E * h->d.ob, 256)), dim3(256), 0, S(stream), h->d.obs,
+                     h->d.cap, h->d.ob, obs, E, base);
+  SPP_CHECK_HIP(hipGetLastError());
+  for (int e = 0; e < E; ++e) {
+    if (slots) slots[e] = (base + e) % h->d.cap;
+  }
+  h->obs_idx = (base + E) % h->d.cap;
+  return SPP_OK;
+}
+
+sppStatus sppReplayAddStep(sppReplayHandle h, const int64_t* prev, const int64_t* next, int E, const float* act,
+                           const float* acm, const float* rew, const uint8_t* done, const uint8_t* end, void* stream) {
+  SPP_REQUIRE(h && prev && next && E > 0 && rew && done && end, SPP_E_INVALID_ARG, "add_step: bad args");
+  if (E > h->ring_cap) {
+    hipDeviceSynchronize();
+    for (int i = 0; i < sppReplay::kRing; ++i) {
+      if (h->pinned[i]) hipHostFree(h->pinned[i]);
+      if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
+      SPP_CHECK_HIP(hipHostMalloc(&h->pinned[i], sizeof(int64_t) * 3 * E));
+      SPP_CHECK_HIP(hipMalloc(&h->dev_meta[i], sizeof(int64_t) * 3 * E));
+    }
+    h->ring_cap = E;
+  }
+  const int slot = h->ring_pos;
+  h->ring_pos = (h->ring_pos + 1) % sppReplay::kRing;
+  SPP_CHECK_HIP(hipEventSynchronize(h->ev[slot]));  // the copy that last used this slot is done
+  int64_t* m = h->pinned[slot];
+  // add_timestep wrap rule (replay_buffer.py:65-75) applied sequentially in env order
+  for (int e = 0; e < E; ++e) {
+    SPP_REQUIRE(prev[e] >= 0 && prev[e] < h->d.cap && next[e] >= 0 && next[e] < h->d.cap, SPP_E_INVALID_ARG,
+                "add_step: slot out of range");
+    m[e] = prev[e];
+    m[E + e] = next[e];
+    m[2 * E + e] = h->ts_idx;
+    if (next[e] < h->ts_idx) {
+      h->len = h->ts_idx + 1;
+      h->ts_idx = 0;
+    } else {
+      h->ts_idx += 1;
+    }
+    h->len = std::max(h->ts_idx, h->len);
+    SPP_REQUIRE(h->ts_idx <= h->d.cap, SPP_E_STATE, "add_step: ts ring overflow (obs ring too small)");
+    if (h->ts_idx == h->d.cap) h->ts_idx = h->d.cap - 1;  // unreachable with the reference wrap rule
+  }
+  SPP_CHECK_HIP(hipMemcpyAsync(h->dev_meta[slot], m, sizeof(int64_t) * 3 * E, hipMemcpyHostToDevice, S(stream)));
+  SPP_CHECK_HIP(hipEventRecord(h->ev[slot], S(stream)));
+  hipLaunchKernelGGL(k_replay_add_step, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), h->d, h->dev_meta[slot], E, act,
+                     acm, rew, done, end);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppReplayState(sppReplayHandle h, int64_t* obs_idx, int64_t* ts_idx, int64_t* len) {
+  SPP_REQUIRE(h, SPP_E_INVALID_ARG, "null handle");
+  if (obs_idx) *obs_idx = h->obs_idx;
+  if (ts_idx) *ts_idx = h->ts_idx;
+  if (len) *len = h->len;
+  return SPP_OK;
+}
+sppStatus sppReplayReset(sppReplayHandle h) {
+  SPP_REQUIRE(h, SPP_E_INVALID_ARG, "null handle");
+  h->obs_idx = h->ts_idx = h->len = 0;
+  return SPP_OK;
+}
+
+sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx, int B, float* obs, float* nobs, float* act,
+                          float* rew, int8_t* done, float* acm, void* stream) {
+  SPP_REQUIRE(h && idx && B > 0, SPP_E_INVALID_ARG, "gather: bad args");
+  hipLaunchKernelGGL(k_replay_gather_rm, dim3(cdiv(B, 256)), dim3(256), 0, S(stream), h->d, idx, B, obs, nobs, act,
+                     rew, done, acm);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* v) {
+  SPP_REQUIRE(h && v, SPP_E_INVALID_ARG, "null");
+  v->obs = h->d.obs;
+  v->obs_idx = h->d.obs_idx;
+  v->next_idx = h->d.next_idx;
+  v->act = h->d.act;
+  v->acm = h->d.acm;
+  v->rew = h->d.rew;
+  v->done = h->d.done;
+  v->end = h->d.end;
+  return SPP_OK;
+}
+
+sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
+                            int first_update, void* stream) {
+  SPP_REQUIRE(h && mean && std && max_obs && min_obs, SPP_E_INVALID_ARG, "obs_stats: bad args");
+  const int64_t len = h->len;
+  if (len <= 10) return SPP_OK;  // replay_buffer.py:84
+  SPP_REQUIRE(len < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats: len too large");
+  const int ob = h->d.ob;
+  const int nblk = 256, thr = 256;
+  const int G = std::min(ob, 16);
+  if (!h->st_part) {
+    SPP_CHECK_HIP(hipMalloc(&h->st_part, sizeof(double) * nblk * ob));
+    SPP_CHECK_HIP(hipMalloc(&h->st_mean, sizeof(double) * ob));
+    SPP_CHECK_HIP(hipMalloc(&h->st_std, sizeof(double) * ob));
+    SPP_CHECK_HIP(hipMalloc(&h->st_state, sizeof(uint32_t) * ob * 4 * 3));
+    SPP_CHECK_HIP(hipMalloc(&h->st_hist, sizeof(uint32_t) * nblk * G * 4 * 256));
+  }
+  hipStream_t st = S(stream);
+  hipLaunchKernelGGL(k_stats_moments, dim3(nblk), dim3(thr), thr * sizeof(double), st, h->d, len,
+                     (const double*)nullptr, h->st_part, 0);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(128), 0, st, h->st_part, nblk, ob, len, h->st_mean, 0);
+  hipLaunchKernelGGL(k_stats_moments, dim3(nblk), dim3(thr), thr * sizeof(double), st, h->d, len,
+                     (const double*)h->st_mean, h->st_part, 1);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(128), 0, st, h->st_part, nblk, ob, len, h->st_std, 1);
+  hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(128), 0, st, h->st_state, ob, len);
+  for (int col0 = 0; col0 < ob; col0 += G) {
+    const int nc = std::min(G, ob - col0);
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      hipLaunchKernelGGL(k_stats_hist, dim3(nblk), dim3(thr), nc * 4 * 256 * sizeof(uint32_t), st, h->d, len, col0,
+                         nc, shift, (const uint32_t*)h->st_state, h->st_hist);
+      hipLaunchKernelGGL(k_stats_select, dim3(nc * 4), dim3(256), 0, st, (const uint32_t*)h->st_hist, nblk, col0, nc,
+                         shift, h->st_state);
+    }
+  }
+  hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(128), 0, st, (const uint32_t*)h->st_state,
+                     (const double*)h->st_mean, (const double*)h->st_std, ob, len, mean, std, max_obs, min_obs,
+                     first_update);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppSynthEnvStep(const float* A, const float* obs, const float* action, int E, int ob, int ac,
+                          float* next_obs, float* reward, void* stream) {
+  SPP_REQUIRE(A && obs && action && next_obs && reward && E > 0, SPP_E_INVALID_ARG, "synth env: bad args");
+  hipLaunchKernelGGL(k_synth_env, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), A, obs, action, E, ob, ac, next_obs,
+                     reward);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+}  // extern "C"
+
+// ================================================================== agent
+namespace spp {
+
+struct NetBufs {
+  float *p = nullptr, *g = nullptr, *m = nullptr, *v = nullptr;
+  int64_t n = 0;
+};
+
+template <typename T>
+struct DevArray {
+  T* ptr = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    n = count;
+    return hipMalloc(&ptr, sizeof(T) * std::max<size_t>(count, 1));
+  }
+  void release() {
+    if (ptr) hipFree(ptr);
+    ptr = nullptr;
+  }
+};
+
+// dims -> kernel instantiation
+struct KernelSet {
+  void (*critic)(SacArgs);
+  void (*actor)(SacArgs, AcmScratch);
+  void (*act)(SacArgs, ActArgs);
+  void (*acmreg)(SacArgs, AcmRegArgs);
+};
+template <int OB, int AOUT, int AC, bool ACMC>
+KernelSet make_kset() {
+  using C = Cfg<OB, AOUT, AC, ACMC>;
+  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>};
+}
+static bool find_kset(int ob, int aout, int ac, bool acmc, KernelSet* ks) {
+#define SPP_KS(o, a, c)                                                    \
+  if (ob == o && aout == a && ac == c) {                                   \
+    *ks = acmc ? make_kset<o, a, c, true>() : make_kset<o, a, c, false>(); \
+    return true;                                                           \
+  }
+  SPP_KS(11, 11, 3)   // Hopper-v2
+  SPP_KS(17, 17, 6)   // HalfCheetah-v2
+  SPP_KS(111, 111, 8) // Ant
+  SPP_KS(3, 3, 1)     // Pendulum-v0 (tests)
+#undef SPP_KS
+  return false;
+}
+
+}  // namespace spp
+
+struct sppAgent {
+  sppAgentConfig cfg{};
+  int device = 0, num_cu = 256;
+  KernelSet ks{};
+  NetBufs net[SPP_NET_COUNT];
+  int64_t nsize[SPP_NET_COUNT] = {};
+  int cin = 0, Bmax = 0, Bpmax = 0;
+  int64_t steps[4] = {0, 0, 0, 0};  // actor, critic, alpha, acm
+  const float *lo = nullptr, *hi = nullptr, *mean = nullptr, *std = nullptr;
+  double* alpha_state = nullptr;
+  float* alpha_f32 = nullptr;
+  DevArray<float> limits;  // [aout] actor lim | [ac] acm lim
+  // packed images
+  DevArray<float4> pk;     // all matrix images
+  DevArray<float> pv;      // all vector images
+  std::vector<PackJob> pj_actor, pj_acm, pj_targ, pj_critic_fwd, pj_critic_all, pj_acmreg;
+  std::vector<VecJob> vj_actor, vj_acm, vj_targ, vj_critic;
+  DevArray<PackJob> d_pj;
+  DevArray<VecJob> d_vj;
+  // job-table offsets inside d_pj / d_vj
+  int o_actor = 0, o_acm = 0, o_targ = 0, o_cfwd = 0, o_call = 0, o_acmreg = 0;
+  int vo_actor = 0, vo_acm = 0, vo_targ = 0, vo_critic = 0;
+  ActorDev actor{};
+  CriticDev critic[2]{}, targ[2]{};
+  AcmDev acm{};
+  const float4* acm_W1n = nullptr;  // ACM W1 natural input packing (regression)
+  // scratch
+  DevArray<float> scratch;
+  float *S = nullptr, *S2 = nullptr, *ACT = nullptr, *AENV = nullptr, *R = nullptr, *DN = nullptr, *EPS1 = nullptr,
+        *EPS2 = nullptr;
+  float *H1[2] = {}, *H2[2] = {}, *D1[2] = {}, *D2[2] = {}, *DQ[2] = {};
+  float *AH1 = nullptr, *AH2 = nullptr, *AD1 = nullptr, *AD2 = nullptr, *ADH = nullptr;
+  float *Z1 = nullptr, *Z2 = nullptr, *T3 = nullptr, *part = nullptr;
+  float *aux = nullptr;  // [4] alpha grad operand (all-reduced in DP)
+  // ACM regression scratch
+  float *RX = nullptr, *RZ1 = nullptr, *RZ2 = nullptr, *RP1 = nullptr, *RP2 = nullptr, *RP3 = nullptr;
+  // weight-gradient job sets: [0] SAC (critic phase, actor phase), [1] ACM regression
+  struct DwSet {
+    DevArray<float> slab;
+    DevArray<DwJob> jobs;
+    DevArray<int> items;
+    int B = -1;
+    int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
+  } dws[2];
+  DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
+  int cur_B = -1;            // staged batch size
+};
+
+namespace spp {
+
+static int64_t sac_actor_size(int ob, int aout) { return 256LL * ob + 256 + 65536 + 256 + 2LL * (aout * 256 + aout); }
+static int64_t critic_size(int cin) { return 256LL * cin + 256 + 65536 + 256 + 256 + 1; }
+static int64_t acm_size(int in, int ac) { return 64LL * in + 64 + 32 * 64 + 32 + (int64_t)ac * 32 + ac; }
+
+static MapDesc nat(int n) { return MapDesc{MAP_NAT, n, 0, 0, 0}; }
+static MapDesc cat(int n0, int n1) { return MapDesc{MAP_CAT, n0, blocks_of(n0), n1, n0}; }
+static MapDesc pair(int n) { return MapDesc{MAP_PAIR, n, 0, 0, 0}; }
+
+}  // namespace spp
+
+// Build all pack jobs (the parameter pointers must be bound).
+static sppStatus build_packs(sppAgent* a) {
+  const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
+  const int ca = a->cfg.acm_critic ? ac : aout;
+  const int cin = ob + ca;
+  for (int k = 0; k < SPP_NET_COUNT; ++k)
+    SPP_REQUIRE(a->net[k].p, SPP_E_STATE, "network %d parameters not bound", k);
+  // sizes: count float4 and vector slots first
+  struct MatSpec {
+    std::vector<PackJob>* list;
+    PackJob job;
+    const float4** slot;
+  };
+  struct VecSpec {
+    std::vector<VecJob>* list;
+    VecJob job;
+    const float** slot;
+  };
+  std::vector<MatSpec> ms;
+  std::vector<VecSpec> vs;
+  auto M = [&](std::vector<PackJob>* list, const float* W, const float* W2, int split, int ld, int trans, int coff,
+               MapDesc out, MapDesc in, int NBO, int NBI, const float4** slot) {
+    PackJob j{W, W2, split, ld, trans, coff, out, in, NBO, NBI, nullptr};
+    ms.push_back({list, j, slot});
+  };
+  auto V = [&](std::vector<VecJob>* list, const float* v, const float* v2, int split, MapDesc m, int NB,
+               const float** slot) {
+    VecJob j{v, v2, split, m, NB, nullptr};
+    vs.push_back({list, j, slot});
+  };
+  // ---- actor (sac/models.py:12-22): fc1 [256][ob], fc2, fc_prob [aout][256], fc_scale
+  {
+    const float* P = a->net[SPP_NET_ACTOR].p;
+    const float *W1 = P, *b1 = W1 + 256 * ob, *W2 = b1 + 256, *b2 = W2 + 65536, *Wp = b2 + 256, *bp = Wp + aout * 256,
+                *Ws = bp + aout, *bs = Ws + aout * 256;
+    M(&a->pj_actor, W1, nullptr, 1 << 30, ob, 0, 0, nat(256), nat(ob), 8, blocks_of(ob), &a->actor.W1);
+    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &a->actor.W2);
+    M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh);
+    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T);
+    M(&a->pj_actor, Wp, Ws, aout, 256, 1, 0, nat(256), pair(aout), 8, (aout + 15) / 16, &a->actor.WhT);
+    V(&a->vj_actor, b1, nullptr, 1 << 30, nat(256), 8, &a->actor.b1P);
+    V(&a->vj_actor, b2, nullptr, 1 << 30, nat(256), 8, &a->actor.b2P);
+    V(&a->vj_actor, bp, bs, aout, nat(2 * aout), blocks_of(2 * aout), &a->actor.bhP);
+  }
+  // ---- ACM (basic_model.py:108-117): fc1 [64][2ob], fc2 [32][64], fc3 [ac][32]
+  {
+    const float* P = a->net[SPP_NET_ACM].p;
+    const int in = 2 * ob;
+    const float *W1 = P, *b1 = W1 + 64 * in, *W2 = b1 + 64, *b2 = W2 + 32 * 64, *W3 = b2 + 32, *b3 = W3 + ac * 32;
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), cat(ob, aout), 2, blocks_of(ob) + blocks_of(aout),
+      &a->acm.W1);
+    M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 0, 0, nat(32), nat(64), 1, 2, &a->acm.W2);
+    M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 0, 0, nat(ac), nat(32), 1, 1, &a->acm.W3);
+    M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 1, 0, nat(32), nat(ac), 1, 1, &a->acm.W3T);
+    M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 1, 0, nat(64), nat(32), 2, 1, &a->acm.W2T);
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(64), blocks_of(aout), 2, &a->acm.W1Ta);
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), nat(in), 2, blocks_of(in), &a->acm_W1n);
+    V(&a->vj_acm, b1, nullptr, 1 << 30, nat(64), 2, &a->acm.b1P);
+    V(&a->vj_acm, b2, nullptr, 1 << 30, nat(32), 1, &a->acm.b2P);
+    V(&a->vj_acm, b3, nullptr, 1 << 30, nat(ac), 1, &a->acm.b3P);
+  }
+  // ---- critics and targets (sac/models.py:75-91): fc1 [256][cin], fc2, fc3 [1][256]
+  for (int t = 0; t < 4; ++t) {
+    const int netid = t < 2 ? SPP_NET_CRITIC1 + t : SPP_NET_CRITIC1_TARG + (t - 2);
+    CriticDev& cd = t < 2 ? a->critic[t] : a->targ[t - 2];
+    const float* P = a->net[netid].p;
+    const float *W1 = P, *b1 = W1 + 256 * cin, *W2 = b1 + 256, *b2 = W2 + 65536, *w3 = b2 + 256, *b3 = w3 + 256;
+    std::vector<PackJob>* fl = t < 2 ? &a->pj_critic_fwd : &a->pj_targ;
+    std::vector<VecJob>* vl = t < 2 ? &a->vj_critic : &a->vj_targ;
+    M(fl, W1, nullptr, 1 << 30, cin, 0, 0, nat(256), cat(ob, ca), 8, blocks_of(ob) + blocks_of(ca), &cd.W1);
+    M(fl, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &cd.W2);
+    if (t < 2) {
+      M(fl, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &cd.W2T);
+      M(fl, W1, nullptr, 1 << 30, cin, 1, ob, nat(ca), nat(256), blocks_of(ca), 8, &cd.W1Ta);
+    }
+    V(vl, b1, nullptr, 1 << 30, nat(256), 8, &cd.b1P);
+    V(vl, b2, nullptr, 1 << 30, nat(256), 8, &cd.b2P);
+    V(vl, w3, nullptr, 1 << 30, nat(256), 8, &cd.w3P);
+    cd.b3 = b3;
+  }
+  // allocate images
+  size_t nf4 = 0, nvf = 0;
+  for (auto& m : ms) nf4 += (size_t)m.job.NBO * m.job.NBI * 4 * 64;
+  for (auto& v : vs) nvf += (size_t)v.job.NB * 32;
+  a->pk.release();
+  a->pv.release();
+  SPP_CHECK_HIP(a->pk.alloc(nf4));
+  SPP_CHECK_HIP(a->pv.alloc(nvf));
+  size_t of = 0, ov = 0;
+  for (auto& m : ms) {
+    m.job.dst = a->pk.ptr + of;
+    *m.slot = m.job.dst;
+    of += (size_t)m.job.NBO * m.job.NBI * 4 * 64;
+    m.list->push_back(m.job);
+  }
+  for (auto& v : vs) {
+    v.job.dst = a->pv.ptr + ov;
+    *v.slot = v.job.dst;
+    ov += (size_t)v.job.NB * 32;
+    v.list->push_back(v.job);
+  }
+  // critics: "all" list = fwd list (already includes transposes)
+  a->pj_critic_all = a->pj_critic_fwd;
+  // device job tables: [actor | acm | targ | critic]
+  std::vector<PackJob> all;
+  a->o_actor = (int)all.size(); all.insert(all.end(), a->pj_actor.begin(), a->pj_actor.end());
+  a->o_acm = (int)all.size(); all.insert(all.end(), a->pj_acm.begin(), a->pj_acm.end());
+  a->o_targ = (int)all.size(); all.insert(all.end(), a->pj_targ.begin(), a->pj_targ.end());
+  a->o_cfwd = (int)all.size(); all.insert(all.end(), a->pj_critic_fwd.begin(), a->pj_critic_fwd.end());
+  std::vector<VecJob> vall;
+  a->vo_actor = (int)vall.size(); vall.insert(vall.end(), a->vj_actor.begin(), a->vj_actor.end());
+  a->vo_acm = (int)vall.size(); vall.insert(vall.end(), a->vj_acm.begin(), a->vj_acm.end());
+  a->vo_targ = (int)vall.size(); vall.insert(vall.end(), a->vj_targ.begin(), a->vj_targ.end());
+  a->vo_critic = (int)vall.size(); vall.insert(vall.end(), a->vj_critic.begin(), a->vj_critic.end());
+  a->d_pj.release();
+  a->d_vj.release();
+  SPP_CHECK_HIP(a->d_pj.alloc(all.size()));
+  SPP_CHECK_HIP(a->d_vj.alloc(vall.size()));
+  SPP_CHECK_HIP(hipMemcpy(a->d_pj.ptr, all.data(), sizeof(PackJob) * all.size(), hipMemcpyHostToDevice));
+  SPP_CHECK_HIP(hipMemcpy(a->d_vj.ptr, vall.data(), sizeof(VecJob) * vall.size(), hipMemcpyHostToDevice));
+  return SPP_OK;
+}
+
+static void launch_pack(sppAgent* a, int off, int n, int voff, int vn, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_pack_matrix, dim3(64, n), dim3(256), 0, st, (const PackJob*)(a->d_pj.ptr + off));
+  if (vn > 0) hipLaunchKernelGGL(k_pack_vector, dim3(1, vn), dim3(256), 0, st, (const VecJob*)(a->d_vj.ptr + voff));
+}
+
+// (Re)build a weight-gradient job set for batch size B.
+//   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
+static sppStatus build_dw(sppAgent* a, int set, int B) {
+  const int Bp = (int)round_up(B, 32);
+  const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
+  const int ca = a->cfg.acm_critic ? ac : aout, cin = ob + ca;
+  std::vector<DwJob> jobs;
+  auto J = [&](const float* A, int N, const float* X0, int K0, const float* X1, int K1, float* dW, float* db) {
+    DwJob j{};
+    j.A = A; j.N = N; j.X0 = X0; j.K0 = K0; j.X1 = X1; j.K1 = K1; j.dW = dW; j.db = db; j.Bp = Bp;
+    const double work = (double)Bp * ((N + 31) & ~31) * (((K0 + K1) + 31) & ~31);
+    int ns = (int)std::ceil(work / (256.0 * 256.0 * 2048.0));
+    ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
+    j.split_len = (int)round_up(cdiv(Bp, ns), 32);
+    j.nsplit = cdiv(Bp, j.split_len);
+    j.slab_stride = (int64_t)N * (K0 + K1) + N;
+    jobs.push_back(j);
+  };
+  sppAgent::DwSet& D = a->dws[set];
+  int nph = 0;
+  if (set == 0) {
+    // critic phase: fc1 (delta1 x [s|a]), fc2 (delta2 x h1), fc3 (dq x h2)  per critic
+    for (int i = 0; i < 2; ++i) {
+      float* G = a->net[SPP_NET_CRITIC1 + i].g;
+      float *gW1 = G, *gb1 = gW1 + 256 * cin, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gw3 = gb2 + 256, *gb3 = gw3 + 256;
+      J(a->D1[i], 256, a->S, ob, a->cfg.acm_critic ? a->AENV : a->ACT, ca, gW1, gb1);
+      J(a->D2[i], 256, a->H1[i], 256, nullptr, 0, gW2, gb2);
+      J(a->DQ[i], 1, a->H2[i], 256, nullptr, 0, gw3, gb3);
+    }
+    D.j0[0] = 0;
+    D.nj[0] = (int)jobs.size();
+    float* G = a->net[SPP_NET_ACTOR].g;
+    float *gW1 = G, *gb1 = gW1 + 256 * ob, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gWp = gb2 + 256,
+          *gbp = gWp + aout * 256, *gWs = gbp + aout, *gbs = gWs + aout * 256;
+    J(a->AD1, 256, a->S, ob, nullptr, 0, gW1, gb1);
+    J(a->AD2, 256, a->AH1, 256, nullptr, 0, gW2, gb2);
+    J(a->ADH, aout, a->AH2, 256, nullptr, 0, gWp, gbp);
+    J(a->ADH + (int64_t)aout * Bp, aout, a->AH2, 256, nullptr, 0, gWs, gbs);
+    D.j0[1] = D.nj[0];
+    D.nj[1] = (int)jobs.size() - D.nj[0];
+    nph = 2;
+  } else {
+    float* G = a->net[SPP_NET_ACM].g;
+    const int in = 2 * ob;
+    float *gW1 = G, *gb1 = gW1 + 64 * in, *gW2 = gb1 + 64, *gb2 = gW2 + 32 * 64, *gW3 = gb2 + 32, *gb3 = gW3 + ac * 32;
+    J(a->RP1, 64, a->RX, in, nullptr, 0, gW1, gb1);
+    J(a->RP2, 32, a->RZ1, 64, nullptr, 0, gW2, gb2);
+    J(a->RP3, ac, a->RZ2, 32, nullptr, 0, gW3, gb3);
+    D.j0[0] = 0;
+    D.nj[0] = (int)jobs.size();
+    nph = 1;
+  }
+  // slabs: phases run back to back on one stream -> they share one arena
+  size_t need = 0;
+  for (int ph = 0; ph < nph; ++ph) {
+    size_t off = 0;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+      if (jobs[j].nsplit > 1) {
+        jobs[j].slab = nullptr;
+        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+      }
+    }
+    need = std::max(need, off);
+  }
+  if (need > D.slab.n) {
+    D.slab.release();
+    SPP_CHECK_HIP(D.slab.alloc(need));
+  }
+  std::vector<int> items;
+  for (int ph = 0; ph < nph; ++ph) {
+    size_t off = 0;
+    std::vector<int> jj, ss;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+      if (jobs[j].nsplit > 1) {
+        jobs[j].slab = D.slab.ptr + off;
+        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+      }
+      for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
+        jj.push_back(j - D.j0[ph]);
+        ss.push_back(sp);
+      }
+    }
+    D.ioff[ph] = (int)items.size();
+    D.nitems[ph] = (int)jj.size();
+    items.insert(items.end(), jj.begin(), jj.end());
+    items.insert(items.end(), ss.begin(), ss.end());
+  }
+  D.jobs.release();
+  D.items.release();
+  SPP_CHECK_HIP(D.jobs.alloc(jobs.size()));
+  SPP_CHECK_HIP(D.items.alloc(items.size()));
+  SPP_CHECK_HIP(hipMemcpy(D.jobs.ptr, jobs.data(), sizeof(DwJob) * jobs.size(), hipMemcpyHostToDevice));
+  SPP_CHECK_HIP(hipMemcpy(D.items.ptr, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
+  D.B = B;
+  return SPP_OK;
+}
+
+static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) {
+  sppAgent::DwSet& D = a->dws[set];
+  const int* ij = D.items.ptr + D.ioff[ph];
+  const int* is = ij + D.nitems[ph];
+  const DwJob* jobs = D.jobs.ptr + D.j0[ph];
+  hipLaunchKernelGGL(k_dw, dim3(D.nitems[ph]), dim3(kDwThreads), 0, st, jobs, ij, is);
+  hipLaunchKernelGGL(k_dw_reduce, dim3(64, D.nj[ph]), dim3(256), 0, st, jobs);
+}
+
+// Adam job table [critic1, critic2 (+polyak targets) | actor | acm]; pointers only.
+static sppStatus build_adam(sppAgent* a) {
+  AdamJob jobs[4];
+  for (int i = 0; i < 2; ++i) {
+    NetBufs& n = a->net[SPP_NET_CRITIC1 + i];
+    jobs[i] = AdamJob{n.p, n.g, n.m, n.v, a->net[SPP_NET_CRITIC1_TARG + i].p, n.n};
+  }
+  NetBufs& na = a->net[SPP_NET_ACTOR];
+  jobs[2] = AdamJob{na.p, na.g, na.m, na.v, nullptr, na.n};
+  NetBufs& nm = a->net[SPP_NET_ACM];
+  jobs[3] = AdamJob{nm.p, nm.g, nm.m, nm.v, nullptr, nm.n};
+  if (!a->d_adam.ptr) SPP_CHECK_HIP(a->d_adam.alloc(4));
+  SPP_CHECK_HIP(hipMemcpy(a->d_adam.ptr, jobs, sizeof(jobs), hipMemcpyHostToDevice));
+  return SPP_OK;
+}
+
+static void launch_adam(sppAgent* a, int first, int count, int64_t n, int64_t step, float lr, float tau,
+                        hipStream_t st) {
+  const double bc1 = 1.0 - std::pow(0.9, (double)step), bc2s = std::sqrt(1.0 - std::pow(0.999, (double)step));
+  hipLaunchKernelGGL(k_adam, dim3(std::max(1, std::min(cdiv(n, 256 * 4), 1024)), count), dim3(256), 0, st,
+                     (const AdamJob*)(a->d_adam.ptr + first), (float)(-(lr / bc1)), (float)bc2s, tau);
+}
+
+static SacArgs make_args(sppAgent* a, int B) {
+  SacArgs p{};
+  p.B = B;
+  p.Bp = (int)round_up(B, 32);
+  p.inv_B = 1.f / (float)B;
+  p.S = a->S; p.S2 = a->S2; p.ACT = a->ACT; p.AENV = a->AENV; p.R = a->R; p.DN = a->DN;
+  p.EPS1 = a->EPS1; p.EPS2 = a->EPS2;
+  p.min_max = a->cfg.min_max_denormalize;
+  p.lo = a->lo; p.hi = a->hi; p.mean = a->mean; p.std = a->std;
+  p.actor_lim = a->limits.ptr;
+  p.acm_lim = a->limits.ptr + a->cfg.aout;
+  p.gamma = a->cfg.gamma;
+  p.custom_loss = a->cfg.custom_loss;
+  p.norm_closs = a->cfg.norm_closs;
+  p.alpha = a->alpha_f32;
+  p.actor = a->actor;
+  for (int i = 0; i < 2; ++i) {
+    p.critic[i] = a->critic[i];
+    p.targ[i] = a->targ[i];
+    p.H1[i] = a->H1[i]; p.H2[i] = a->H2[i]; p.D1[i] = a->D1[i]; p.D2[i] = a->D2[i]; p.DQ[i] = a->DQ[i];
+  }
+  p.acm = a->acm;
+  p.AH1 = a->AH1; p.AH2 = a->AH2; p.AD1 = a->AD1; p.AD2 = a->AD2; p.ADH = a->ADH;
+  p.part = a->part;
+  return p;
+}
+
+static int phase_grid(sppAgent* a, int Bp) {
+  const int ntiles = Bp / 32;
+  return std::max(1, std::min(cdiv(ntiles, kWavesPerWG), a->num_cu));
+}
+
+static sppStatus check_ready(sppAgent* a) {
+  SPP_REQUIRE(a->alpha_state && a->alpha_f32, SPP_E_STATE, "alpha not bound");
+  SPP_REQUIRE(a->cfg.min_max_denormalize ? (a->lo && a->hi) : (a->mean && a->std), SPP_E_STATE,
+              "normalizer not bound");
+  SPP_REQUIRE(a->limits.ptr, SPP_E_STATE, "limits not set");
+  if (!a->pk.ptr) {
+    sppStatus s = build_packs(a);
+    if (s) return s;
+    if ((s = build_adam(a))) return s;
+    a->dws[0].B = a->dws[1].B = -1;
+  }
+  return SPP_OK;
+}
+
+extern "C" {
+
+sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int device) {
+  SPP_REQUIRE(out && cfg, SPP_E_INVALID_ARG, "null arg");
+  SPP_REQUIRE(cfg->algo == SPP_ALGO_SAC_ACM, SPP_E_INVALID_ARG, "unsupported algo %d", cfg->algo);
+  SPP_REQUIRE(cfg->max_batch > 0, SPP_E_INVALID_ARG, "max_batch must be > 0");
+  KernelSet ks;
+  SPP_REQUIRE(find_kset(cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, &ks), SPP_E_SHAPE,
+              "no kernel instantiation for (ob=%d, aout=%d, ac=%d)", cfg->ob, cfg->aout, cfg->ac);
+  SPP_CHECK_HIP(hipSetDevice(device));
+  auto a = std::make_unique<sppAgent>();
+  a->cfg = *cfg;
+  a->device = device;
+  a->ks = ks;
+  hipDeviceProp_t prop;
+  SPP_CHECK_HIP(hipGetDeviceProperties(&prop, device));
+  a->num_cu = prop.multiProcessorCount;
+  const int ob = cfg->ob, aout = cfg->aout, ac = cfg->ac;
+  a->cin = ob + (cfg->acm_critic ? ac : aout);
+  a->nsize[SPP_NET_ACTOR] = sac_actor_size(ob, aout);
+  a->nsize[SPP_NET_CRITIC1] = a->nsize[SPP_NET_CRITIC2] = critic_size(a->cin);
+  a->nsize[SPP_NET_CRITIC1_TARG] = a->nsize[SPP_NET_CRITIC2_TARG] = critic_size(a->cin);
+  a->nsize[SPP_NET_ACM] = acm_size(2 * ob, ac);
+  a->Bmax = cfg->max_batch;
+  const int64_t Bp = round_up(cfg->max_batch, 32);
+  a->Bpmax = (int)Bp;
+  const int64_t ntiles = Bp / 32;
+  // scratch arena
+  const int64_t per = Bp;
+  int64_t total = 0;
+  auto take = [&](int64_t rows) { int64_t o = total; total += rows * per; return o; };
+  const int64_t oS = take(ob), oS2 = take(ob), oACT = take(aout), oAENV = take(ac), oR = take(1), oDN = take(1),
+                oE1 = take(aout), oE2 = take(aout);
+  int64_t oH1[2], oH2[2], oD1[2], oD2[2], oDQ[2];
+  for (int i = 0; i < 2; ++i) {
+    oH1[i] = take(256); oH2[i] = take(256); oD1[i] = take(256); oD2[i] = take(256); oDQ[i] = take(1);
+  }
+  const int64_t oAH1 = take(256), oAH2 = take(256), oAD1 = take(256), oAD2 = take(256), oADH = take(2 * aout),
+                oZ1 = take(64), oZ2 = take(32), oT3 = take(ac);
+  const int64_t oRX = take(2 * ob), oRZ1 = take(64), oRZ2 = take(32), oRP1 = take(64), oRP2 = take(32),
+                oRP3 = take(ac);
+  const int64_t oPart = total;
+  total += ntiles * kParts + 64;
+  const int64_t oAux = total;
+  total += 16;
+  hipError_t e = a->scratch.alloc(total);
+  if (e != hipSuccess) {
+    set_error("scratch alloc %.2f GB: %s", total * 4.0 / 1e9, hipGetErrorString(e));
+    return SPP_E_OOM;
+  }
+  SPP_CHECK_HIP(hipMemset(a->scratch.ptr, 0, sizeof(float) * total));
+  float* b = a->scratch.ptr;
+  a->S = b + oS; a->S2 = b + oS2; a->ACT = b + oACT; a->AENV = b + oAENV; a->R = b + oR; a->DN = b + oDN;
+  a->EPS1 = b + oE1; a->EPS2 = b + oE2;
+  for (int i = 0; i < 2; ++i) {
+    a->H1[i] = b + oH1[i]; a->H2[i] = b + oH2[i]; a->D1[i] = b + oD1[i]; a->D2[i] = b + oD2[i]; a->DQ[i] = b + oDQ[i];
+  }
+  a->AH1 = b + oAH1; a->AH2 = b + oAH2; a->AD1 = b + oAD1; a->AD2 = b + oAD2; a->ADH = b + oADH;
+  a->Z1 = b + oZ1; a->Z2 = b + oZ2; a->T3 = b + oT3;
+  a->RX = b + oRX; a->RZ1 = b + oRZ1; a->RZ2 = b + oRZ2; a->RP1 = b + oRP1; a->RP2 = b + oRP2; a->RP3 = b + oRP3;
+  a->part = b + oPart;
+  a->aux = b + oAux;
+  SPP_CHECK_HIP(a->limits.alloc(aout + ac));
+  *out = a.release();
+  return SPP_OK;
+}
+
+sppStatus sppAgentDestroy(sppAgentHandle a) {
+  if (!a) return SPP_OK;
+  hipSetDevice(a->device);
+  hipDeviceSynchronize();
+  a->limits.release(); a->pk.release(); a->pv.release(); a->d_pj.release(); a->d_vj.release();
+  a->scratch.release(); a->d_adam.release();
+  for (auto& D : a->dws) { D.slab.release(); D.jobs.release(); D.items.release(); }
+  delete a;
+  return SPP_OK;
+}
+
+sppStatus sppAgentNetSize(sppAgentHandle a, int net, int64_t* n) {
+  SPP_REQUIRE(a && n && net >= 0 && net < SPP_NET_COUNT, SPP_E_INVALID_ARG, "bad net id");
+  *n = a->nsize[net];
+  return SPP_OK;
+}
+
+sppStatus sppAgentBindNet(sppAgentHandle a, int net, float* p, float* g, float* m, float* v) {
+  SPP_REQUIRE(a && net >= 0 && net < SPP_NET_COUNT && p, SPP_E_INVALID_ARG, "bind: bad args");
+  const bool trainable = net == SPP_NET_ACTOR || net == SPP_NET_CRITIC1 || net == SPP_NET_CRITIC2 || net == SPP_NET_ACM;
+  SPP_REQUIRE(!trainable || (g && m && v), SPP_E_INVALID_ARG, "bind: trainable net %d needs grad/m/v", net);
+  const bool changed = a->net[net].p != p || a->net[net].g != g;
+  a->net[net] = NetBufs{p, g, m, v, a->nsize[net]};
+  if (changed) {  // pack tables and gradient jobs hold these pointers
+    a->pk.release();
+    a->pj_actor.clear(); a->pj_acm.clear(); a->pj_targ.clear(); a->pj_critic_fwd.clear(); a->pj_critic_all.clear();
+    a->vj_actor.clear(); a->vj_acm.clear(); a->vj_targ.clear(); a->vj_critic.clear();
+  }
+  return SPP_OK;
+}
+
+sppStatus sppAgentSetLimits(sppAgentHandle a, const float* actor_lim, const float* acm_lim) {
+  SPP_REQUIRE(a && actor_lim && acm_lim, SPP_E_INVALID_ARG, "null");
+  SPP_CHECK_HIP(hipMemcpy(a->limits.ptr, actor_lim, sizeof(float) * a->cfg.aout, hipMemcpyHostToDevice));
+  SPP_CHECK_HIP(hipMemcpy(a->limits.ptr + a->cfg.aout, acm_lim, sizeof(float) * a->cfg.ac, hipMemcpyHostToDevice));
+  return SPP_OK;
+}
+
+sppStatus sppAgentBindNormalizer(sppAgentHandle a, const float* lo, const float* hi, const float* mean,
+                                 const float* std) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  a->lo = lo; a->hi = hi; a->mean = mean; a->std = std;
+  return SPP_OK;
+}
+
+sppStatus sppAgentBindAlpha(sppAgentHandle a, double* st, float* af) {
+  SPP_REQUIRE(a && st && af, SPP_E_INVALID_ARG, "null");
+  a->alpha_state = st;
+  a->alpha_f32 = af;
+  return SPP_OK;
+}
+
+sppStatus sppAgentSetSteps(sppAgentHandle a, int64_t s0, int64_t s1, int64_t s2, int64_t s3) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  a->steps[0] = s0; a->steps[1] = s1; a->steps[2] = s2; a->steps[3] = s3;
+  return SPP_OK;
+}
+sppStatus sppAgentGetSteps(sppAgentHandle a, int64_t* s) {
+  SPP_REQUIRE(a && s, SPP_E_INVALID_ARG, "null");
+  for (int i = 0; i < 4; ++i) s[i] = a->steps[i];
+  return SPP_OK;
+}
+
+static sppStatus stage(sppAgentHandle a, const sppBatch* bt, const float* e1, const float* e2, hipStream_t st) {
+  SPP_REQUIRE(bt && bt->B > 0 && bt->B <= a->Bmax, SPP_E_SHAPE, "batch B=%d outside (0, max_batch=%d]",
+              bt ? bt->B : -1, a->Bmax);
+  SPP_REQUIRE(bt->obs && bt->next_obs && bt->reward && bt->done && bt->acm_action, SPP_E_INVALID_ARG,
+              "batch: null field");
+  SPP_REQUIRE(a->cfg.acm_critic || bt->action, SPP_E_INVALID_ARG, "batch.action required without acm_critic");
+  StageArgs s{};
+  s.B = bt->B; s.Bp = (int)round_up(bt->B, 32); s.ob = a->cfg.ob; s.aout = a->cfg.aout; s.ac = a->cfg.ac;
+  s.obs = bt->obs; s.next_obs = bt->next_obs; s.act = bt->action; s.rew = bt->reward; s.acm = bt->acm_action;
+  s.done = bt->done; s.eps1 = e1; s.eps2 = e2;
+  s.S = a->S; s.S2 = a->S2; s.ACT = a->ACT; s.AENV = a->AENV; s.R = a->R; s.DN = a->DN; s.EPS1 = a->EPS1;
+  s.EPS2 = a->EPS2;
+  hipLaunchKernelGGL(k_stage_batch, dim3(cdiv(s.Bp, 256)), dim3(256), 0, st, s);
+  a->cur_B = bt->B;
+  return SPP_OK;
+}
+
+static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_t st) {
+  const int B = a->cur_B;
+  SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
+  sppStatus s = check_ready(a);
+  if (s) return s;
+  if (a->dws[0].B != B) {
+    s = build_dw(a, 0, B);
+    if (s) return s;
+  }
+  // pack actor, ACM, targets, critics (current weights)
+  launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size() + a->pj_targ.size() + a->pj_critic_fwd.size()),
+              a->vo_actor, (int)(a->vj_actor.size() + a->vj_acm.size() + a->vj_targ.size() + a->vj_critic.size()), st);
+  SacArgs p = make_args(a, B);
+  const int grid = phase_grid(a, p.Bp);
+  hipLaunchKernelGGL(a->ks.critic, dim3(grid), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
+  launch_dw(a, 0, 0, st);
+  hipLaunchKernelGGL(k_finalize_critic, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppSacAcmCriticGrads(sppAgentHandle a, const sppBatch* bt, const float* eps_next, float* losses,
+                               void* stream) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  SPP_REQUIRE(eps_next, SPP_E_INVALID_ARG, "eps_next required (use the staged API for device draws)");
+  sppStatus s = stage(a, bt, eps_next, nullptr, S(stream));
+  if (s) return s;
+  return critic_grads_staged(a, losses, S(stream));
+}
+
+sppStatus sppSacAcmCriticApply(sppAgentHandle a, void* stream) {
+  SPP_REQUIRE(a && a->d_adam.ptr, SPP_E_STATE, "agent not ready");
+  a->steps[1] += 1;
+  launch_adam(a, 0, 2, a->net[SPP_NET_CRITIC1].n, a->steps[1], a->cfg.critic_lr, a->cfg.tau, S(stream));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
+  const int B = a->cur_B;
+  SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
+  // repack the updated critics
+  launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), a->vo_critic, (int)a->vj_critic.size(), st);
+  SacArgs p = make_args(a, B);
+  AcmScratch z{a->Z1, a->Z2, a->T3};
+  const int grid = phase_grid(a, p.Bp);
+  hipLaunchKernelGGL(a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
+  SPP_CHECK_HIP(hipGetLastError());
+  launch_dw(a, 0, 1, st);
+  (void)losses;
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppSacAcmActorGrads(sppAgentHandle a, const float* eps_cur, float* losses, void* stream) {
+  SPP_REQUIRE(a && eps_cur, SPP_E_INVALID_ARG, "null");
+  const int B = a->cur_B;
+  SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
+  const int Bp = (int)round_up(B, 32);
+  hipLaunchKernelGGL(k_eps_copy_fm, dim3(cdiv((int64_t)a->cfg.aout * Bp, 256)), dim3(256), 0, S(stream), eps_cur,
+                     a->EPS2, a->cfg.aout, B, Bp);
+  return actor_grads(a, losses, S(stream));
+}
+
+static sppStatus actor_apply(sppAgentHandle a, float* losses, hipStream_t st) {
+  a->steps[0] += 1;
+  a->steps[2] += 1;
+  launch_adam(a, 2, 1, a->net[SPP_NET_ACTOR].n, a->steps[0], a->cfg.actor_lr, 0.f, st);
+  const int Bp = (int)round_up(a->cur_B, 32);
+  hipLaunchKernelGGL(k_finalize_actor_alpha, dim3(1), dim3(256), 0, st, (const float*)a->part, Bp / 32, a->cur_B,
+                     a->cfg.aout, a->cfg.custom_loss, (double)a->cfg.target_entropy, (double)a->cfg.alpha_lr,
+                     a->steps[2], a->alpha_state, a->alpha_f32, losses);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppSacAcmActorApply(sppAgentHandle a, float* losses, void* stream) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  return actor_apply(a, losses, S(stream));
+}
+
+sppStatus sppSacAcmUpdate(sppAgentHandle a, const sppBatch* bt, const float* eps_next, const float* eps_cur,
+                          float* losses, void* stream) {
+  SPP_REQUIRE(a && eps_next && eps_cur, SPP_E_INVALID_ARG, "eps required (use sppSacAcmUpdateStaged for device draws)");
+  hipStream_t st = S(stream);
+  sppStatus s = stage(a, bt, eps_next, eps_cur, st);
+  if (s) return s;
+  if ((s = critic_grads_staged(a, losses, st))) return s;
+  if ((s = sppSacAcmCriticApply(a, stream))) return s;
+  if ((s = actor_grads(a, losses, st))) return s;
+  return actor_apply(a, losses, st);
+}
+
+sppStatus sppAgentStageFromReplay(sppAgentHandle a, sppReplayHandle r, const int64_t* idx, int B, void* stream) {
+  SPP_REQUIRE(a && r && idx && B > 0 && B <= a->Bmax, SPP_E_INVALID_ARG, "stage_from_replay: bad args");
+  SPP_REQUIRE(r->d.ob == a->cfg.ob && r->d.ac == a->cfg.ac && r->d.aout == a->cfg.aout, SPP_E_SHAPE, "dims differ");
+  const int Bp = (int)round_up(B, 32);
+  hipLaunchKernelGGL(k_replay_stage_fm, dim3(cdiv(Bp, 256)), dim3(256), 0, S(stream), r->d, idx, B, Bp, a->S, a->S2,
+                     a->cfg.acm_critic ? nullptr : a->ACT, a->AENV, a->R, a->DN);
+  SPP_CHECK_HIP(hipGetLastError());
+  a->cur_B = B;
+  return SPP_OK;
+}
+
+sppStatus sppSacAcmUpdateStaged(sppAgentHandle a, uint64_t seed, uint64_t counter, float* losses, void* stream) {
+  SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "no staged batch");
+  hipStream_t st = S(stream);
+  const int B = a->cur_B, Bp = (int)round_up(B, 32);
+  const int64_t pairs = ((int64_t)a->cfg.aout * Bp + 1) / 2;
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, st, a->EPS1, a->cfg.aout, B, Bp, seed,
+                     2 * counter);
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, st, a->EPS2, a->cfg.aout, B, Bp, seed,
+                     2 * counter + 1);
+  sppStatus s;
+  if ((s = critic_grads_staged(a, losses, st))) return s;
+  if ((s = sppSacAcmCriticApply(a, stream))) return s;
+  if ((s = actor_grads(a, losses, st))) return s;
+  return actor_apply(a, losses, st);
+}
+
+sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, int B, float* loss, void* stream) {
+  SPP_REQUIRE(a && x && y && B > 0 && B <= a->Bmax, SPP_E_INVALID_ARG, "acm step: bad args");
+  hipStream_t st = S(stream);
+  sppStatus s = check_ready(a);
+  if (s) return s;
+  if (a->dws[1].B != B) {
+    if ((s = build_dw(a, 1, B))) return s;
+  }
+  launch_pack(a, a->o_acm, (int)a->pj_acm.size(), a->vo_acm, (int)a->vj_acm.size(), st);
+  SacArgs p = make_args(a, B);
+  p.acm.W1 = a->acm_W1n;
+  AcmRegArgs g{};
+  g.B = B; g.Bp = (int)round_up(B, 32); g.x = x; g.y = y;
+  g.XT = a->RX; g.Z1 = a->RZ1; g.Z2 = a->RZ2; g.P1 = a->RP1; g.P2 = a->RP2; g.P3 = a->RP3; g.part = a->part;
+  hipLaunchKernelGGL(a->ks.acmreg, dim3(phase_grid(a, g.Bp)), dim3(256), 0, st, p, g);
+  SPP_CHECK_HIP(hipGetLastError());
+  launch_dw(a, 1, 0, st);
+  hipLaunchKernelGGL(k_finalize_acm, dim3(1), dim3(256), 0, st, (const float*)a->part, g.Bp / 32, B, a->cfg.ac, loss);
+  a->steps[3] += 1;
+  launch_adam(a, 3, 1, a->net[SPP_NET_ACM].n, a->steps[3], a->cfg.acm_lr, 0.f, st);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* eps, const float* noise,
+                       float act_noise, int mode, int denorm_out, float* target_out, float* env_out, void* stream) {
+  SPP_REQUIRE(a && obs && E > 0 && target_out && env_out, SPP_E_INVALID_ARG, "policy_act: bad args");
+  SPP_REQUIRE(mode >= 0 && mode <= 2, SPP_E_INVALID_ARG, "mode");
+  SPP_REQUIRE(mode != 0 || eps, SPP_E_INVALID_ARG, "random mode needs eps");
+  hipStream_t st = S(stream);
+  sppStatus s = check_ready(a);
+  if (s) return s;
+  launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size()), a->vo_actor,
+              (int)(a->vj_actor.size() + a->vj_acm.size()), st);
+  SacArgs p = make_args(a, 32);
+  ActArgs g{E, mode, denorm_out, act_noise, obs, eps, noise, target_out, env_out};
+  const int grid = std::max(1, std::min(cdiv(cdiv(E, 32), kWavesPerWG), a->num_cu));
+  hipLaunchKernelGGL(a->ks.act, dim3(grid), dim3(256), 0, st, p, g);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,
+                        void* stream) {
+  SPP_REQUIRE(x && W && y && B > 0 && K > 0 && K <= 256 && N > 0 && N <= 256, SPP_E_INVALID_ARG, "debug dense: bad");
+  hipStream_t st = S(stream);
+  const int NBI = blocks_of(K), NBO = blocks_of(N);
+  float4* wf;
+  float* bp;
+  PackJob* dj;
+  VecJob* dv;
+  SPP_CHECK_HIP(hipMalloc(&wf, sizeof(float4) * NBO * NBI * 256));
+  SPP_CHECK_HIP(hipMalloc(&bp, sizeof(float) * NBO * 32));
+  SPP_CHECK_HIP(hipMalloc(&dj, sizeof(PackJob)));
+  SPP_CHECK_HIP(hipMalloc(&dv, sizeof(VecJob)));
+  PackJob pj{W, nullptr, 1 << 30, K, 0, 0, nat(N), nat(K), NBO, NBI, wf};
+  VecJob vj{b, nullptr, 1 << 30, nat(N), NBO, bp};
+  SPP_CHECK_HIP(hipMemcpy(dj, &pj, sizeof(pj), hipMemcpyHostToDevice));
+  SPP_CHECK_HIP(hipMemcpy(dv, &vj, sizeof(vj), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_pack_matrix, dim3(16, 1), dim3(256), 0, st, (const PackJob*)dj);
+  if (b) hipLaunchKernelGGL(k_pack_vector, dim3(1, 1), dim3(256), 0, st, (const VecJob*)dv);
+  const dim3 grid(cdiv(B, 32));
+  const float* bpp = b ? bp : nullptr;
+  switch (NBI) {
+#define SPP_DD(n) case n: hipLaunchKernelGGL(k_debug_dense<n>, grid, dim3(64), 0, st, (const float4*)wf, bpp, x, y, B, K, N, act); break;
+    SPP_DD(1) SPP_DD(2) SPP_DD(3) SPP_DD(4) SPP_DD(5) SPP_DD(6) SPP_DD(7) SPP_DD(8)
+#undef SPP_DD
+  }
+  SPP_CHECK_HIP(hipGetLastError());
+  SPP_CHECK_HIP(hipStreamSynchronize(st));
+  hipFree(wf); hipFree(bp); hipFree(dj); hipFree(dv);
+  return SPP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+// Fragment-image packing, fused Adam(+polyak), temperature step and loss
+// finalisation.
+//   Adam      torch.optim.Adam single-tensor step (rltoolkit/rl.py:62)
+//   polyak    rltoolkit/algorithms/sac/sac.py:186-199 (mul_ then add_, two roundings)
+//   alpha     sac.py:201-216 + sac_acm.py:153-159 (log_alpha is float64)
+#include "internal.h"
+
+namespace spp {
+
+__global__ void k_pack_matrix(const PackJob* __restrict__ jobs) {
+  const PackJob J = jobs[blockIdx.y];
+  const int64_t total = (int64_t)J.NBO * J.NBI * 4 * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    int64_t rest = i >> 6;
+    const int rq = (int)(rest & 3);
+    rest >>= 2;
+    const int ib = (int)(rest % J.NBI);
+    const int ob = (int)(rest / J.NBI);
+    int q, hh;
+    row_to_pos(lane & 31, q, hh);
+    const int n = map_index(J.out, ob, q, hh);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = map_index(J.in, ib, 4 * rq + j, lane >> 5);
+      float x = 0.f;
+      if (n >= 0 && k >= 0) {
+        const int row = J.trans ? k : n;
+        const int col = J.coff + (J.trans ? n : k);
+        const float* base = row < J.split ? J.W + (int64_t)row * J.ld : J.W2 + (int64_t)(row - J.split) * J.ld;
+        x = base[col];
+      }
+      v[j] = x;
+    }
+    J.dst[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__global__ void k_pack_vector(const VecJob* __restrict__ jobs) {
+  const VecJob J = jobs[blockIdx.y];
+  const int total = J.NB * 32;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int hh = i & 1, q = (i >> 1) & 15, ob = i >> 5;
+    const int idx = map_index(J.map, ob, q, hh);
+    float x = 0.f;
+    if (idx >= 0) x = idx < J.split ? J.v[idx] : J.v2[idx - J.split];
+    J.dst[i] = x;
+  }
+}
+
+// One Adam step per element (+ optional polyak of the matching target element).
+__global__ void k_adam(const AdamJob* __restrict__ jobs, float neg_step, float bc2s, float tau) {
+  const AdamJob J = jobs[blockIdx.y];
+  const float omb1 = 0.1f, b2 = 0.999f, omb2 = 0.001f, eps = 1e-8f;
+  const float omtau = (float)(1.0 - (double)tau);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = J.g[i];
+    float m = J.m[i], v = J.v[i];
+    m = fadd_rn(m, fmul_rn(omb1, fsub_rn(g, m)));                  // exp_avg.lerp_(g, 1-b1)
+    v = fadd_rn(fmul_rn(v, b2), fmul_rn(fmul_rn(omb2, g), g));     // mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = fadd_rn(fdiv_rn(sqrtf(v), bc2s), eps);   // (sqrt(v)/bc2s).add_(eps)
+    const float p = fadd_rn(J.p[i], fmul_rn(neg_step, fdiv_rn(m, denom)));  // addcdiv_
+    J.m[i] = m;
+    J.v[i] = v;
+    J.p[i] = p;
+    if (J.targ) {
+      const float t = fmul_rn(J.targ[i], omtau);
+      J.targ[i] = fadd_rn(t, fmul_rn(tau, p));
+    }
+  }
+}
+
+// Deterministic block reduction of per-tile partial sums (double accumulate).
+__device__ double block_sum(const float* part, int ntiles, int stride, int slot) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int t = threadIdx.x; t < ntiles; t += blockDim.x) s += (double)part[(int64_t)t * stride + slot];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// losses[0..1] = critic MSEs (sac_acm.py:117-123)
+__global__ void k_finalize_critic(const float* part, int ntiles, int B, float* losses) {
+  const double l0 = block_sum(part, ntiles, 8, 0);
+  const double l1 = block_sum(part, ntiles, 8, 1);
+  if (threadIdx.x == 0 && losses) {
+    losses[0] = (float)(l0 / B);
+    losses[1] = (float)(l1 / B);
+  }
+}
+
+// Actor losses + temperature Adam step (sac.py:201-216, sac_acm.py:153-159).
+// alpha_state = {log_alpha, m, v, alpha} (double)
+__global__ void k_finalize_actor_alpha(const float* part, int ntiles, int B, int aout, float custom_loss,
+                                       double target_entropy, double lr, int64_t step, double* alpha_state,
+                                       float* alpha_f32, float* losses) {
+  const double ssac = block_sum(part, ntiles, 8, 2);
+  const double sdist = block_sum(part, ntiles, 8, 3);
+  const double slp = block_sum(part, ntiles, 8, 4);
+  if (threadIdx.x != 0) return;
+  const double sac = ssac / B;
+  const double dist = sdist / ((double)B * aout);
+  const double actor = custom_loss != 0.f ? sac + (double)custom_loss * dist : sac;
+  const double la = alpha_state[0];
+  const double c = -(slp / B) - target_entropy;  // mean(-logpi - H)
+  const double g = exp(la) * c;                   // d/dlog_alpha of exp(log_alpha)*c
+  double m = alpha_state[1], v = alpha_state[2];
+  m = m + (1.0 - 0.9) * (g - m);
+  v = v * 0.999 + (1.0 - 0.999) * g * g;
+  const double bc1 = 1.0 - pow(0.9, (double)step), bc2s = sqrt(1.0 - pow(0.999, (double)step));
+  const double nla = la - (lr / bc1) * (m / (sqrt(v) / bc2s + 1e-8));
+  alpha_state[0] = nla;
+  alpha_state[1] = m;
+  alpha_state[2] = v;
+  alpha_state[3] = exp(nla);
+  *alpha_f32 = (float)exp(nla);
+  if (losses) {
+    losses[2] = (float)actor;
+    losses[3] = custom_loss != 0.f ? (float)sac : 0.f;
+    losses[4] = custom_loss != 0.f ? (float)dist : 0.f;
+    losses[5] = (float)(exp(la) * c);
+    losses[6] = (float)exp(nla);
+  }
+}
+
+// ACM regression loss (acm.py:253): mean over B*ac
+__global__ void k_finalize_acm(const float* part, int ntiles, int B, int ac, float* loss) {
+  const double s = block_sum(part, ntiles, 1, 0);
+  if (threadIdx.x == 0 && loss) *loss = (float)(s / ((double)B * ac));
+}
+
+}  // namespace spp

@@ -1,0 +1,860 @@
+// SAC_AcM per-sample kernels (gfx950).  One wave = 32 samples; one workgroup
+// = 4 waves (one per SIMD) with a private 40 KiB LDS image each.
+//
+//  k_sac_critic_phase   rltoolkit/acm/off_policy/sac_acm.py:30-58 (targets) and
+//                       :114-131 (both critics' forward + backward) -> per-sample
+//                       operands of the critic weight gradients
+//  k_sac_actor_phase    sac_acm.py:60-87 + :137-145 (actor loss through the
+//                       frozen ACM and both updated critics) -> actor grad operands
+//  k_policy_act         ddpg_acm.py:40-50, off_policy.py:50-54, :89-106 (rollout)
+//  k_acm_regress        acm.py:246-258 (ACM regression forward + backward)
+#include "sac_kernels.h"
+
+namespace spp {
+
+constexpr float kLog2 = 0.69314718055994530942f;
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // math.log(math.sqrt(2*pi))
+
+template <int OB_, int AOUT_, int AC_, bool ACMC_>
+struct Cfg {
+  static constexpr int OB = OB_, AOUT = AOUT_, AC = AC_;
+  static constexpr bool ACMC = ACMC_;
+  static constexpr int NB_OB = blocks_of(OB);
+  static constexpr int NB_AOUT = blocks_of(AOUT);
+  static constexpr int NB_H2 = blocks_of(2 * AOUT);      // heads output blocks (natural rows mu | logsig)
+  static constexpr int NB_PAIR = (AOUT + 15) / 16;        // heads in pairing layout
+  static constexpr int CA = ACMC ? AC : AOUT;             // critic action-input width
+  static constexpr int NB_CA = blocks_of(CA);
+  static constexpr int NB_CIN = NB_OB + NB_CA;
+  static constexpr int NB_ACMIN = NB_OB + NB_AOUT;
+  static constexpr uint64_t RV_X = rv_nat(OB, NB_OB);
+  static constexpr uint64_t RV_H = rv_nat(256, 8);
+  static constexpr uint64_t RV_CIN = rv_cat(OB, NB_OB, CA, NB_CA);
+  static constexpr uint64_t RV_ACMIN = rv_cat(OB, NB_OB, AOUT, NB_AOUT);
+  static constexpr uint64_t RV_Z1 = rv_nat(64, 2);
+  static constexpr uint64_t RV_Z2 = rv_nat(32, 1);
+  static constexpr uint64_t RV_AC = rv_nat(AC, 1);
+  static constexpr uint64_t RV_CA = rv_nat(CA, NB_CA);
+  static constexpr uint64_t RV_PAIR = rv_pair(AOUT, NB_PAIR);
+  static_assert(AC <= 32, "env action dim <= 32");
+  static_assert(2 * AOUT <= 256 && OB + AOUT <= 256, "dims");
+};
+
+constexpr int kWavesPerWG = 4;
+constexpr int kLdsPerWave = 256 * 32 + 64 * 32;  // BIG [256][32] + SMALL [64][32] floats
+
+__device__ __forceinline__ void setbits(uint64_t& lo, uint64_t& hi, int ob, uint32_t bits) {
+  if (ob < 4) lo |= (uint64_t)bits << (16 * ob);
+  else hi |= (uint64_t)bits << (16 * (ob - 4));
+}
+__device__ __forceinline__ bool getbit(uint64_t lo, uint64_t hi, int ob, int q) {
+  const uint64_t w = ob < 4 ? (lo >> (16 * ob)) : (hi >> (16 * (ob - 4)));
+  return (w >> q) & 1;
+}
+
+// memory.py:107-121 (denormalize) and :76-87 / utils.py:62-73 (normalize, force=True)
+__device__ __forceinline__ float denorm(const SacArgs& p, int j, float x) {
+  if (p.min_max) {
+    const float lo = p.lo[j], hi = p.hi[j];
+    const float mid = fadd_rn(hi, lo) * 0.5f, delta = fsub_rn(hi, lo) * 0.5f;
+    return fadd_rn(mid, fmul_rn(x, delta));
+  }
+  return fadd_rn(fmul_rn(fadd_rn(p.std[j], 1e-8f), x), p.mean[j]);
+}
+__device__ __forceinline__ float denorm_scale(const SacArgs& p, int j) {
+  if (p.min_max) return fsub_rn(p.hi[j], p.lo[j]) * 0.5f;
+  return fadd_rn(p.std[j], 1e-8f);
+}
+__device__ __forceinline__ float normalize(const SacArgs& p, int j, float x) {
+  if (p.min_max) {
+    const float lo = p.lo[j], hi = p.hi[j];
+    const float mid = fadd_rn(hi, lo) * 0.5f;
+    return fdiv_rn(fsub_rn(x, mid), fadd_rn(fsub_rn(hi, mid), 1e-8f));
+  }
+  return fminf(fmaxf(fdiv_rn(fsub_rn(x, p.mean[j]), fadd_rn(p.std[j], 1e-8f)), -10.f), 10.f);
+}
+__device__ __forceinline__ float softplus_t(float x) {  // torch softplus(beta=1, threshold=20)
+  return x > 20.f ? x : log1pf(expf(x));
+}
+
+// Pairing-layout tile of the actor heads from the LDS image rows [0, 2*AOUT)
+// pairing layout: block ib, register r<8 (mu) / r+8 (logsig), half h -> j = 16*ib + 8*h + r
+template <class C>
+__device__ __forceinline__ void load_pair(f32x16 (&t)[C::NB_PAIR], const float* lds) {
+  const int lane = lane_id(), h8 = 8 * (lane >> 5);
+  const float* pl = lds + h8 * 32 + (lane & 31);
+#pragma unroll
+  for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j0 = 16 * ib + (r & 7);
+      t[ib][r] = (j0 + h8 < C::AOUT) ? pl[((r < 8) ? j0 : C::AOUT + j0) * 32] : 0.f;
+    }
+}
+
+// Concatenated input tile: blocks [0, NB0) natural from global X (F0 units),
+// blocks [NB0, NB0+NB1) natural from the LDS image rows [0, F1).
+template <int NB0, int NB1>
+__device__ __forceinline__ void load_cat_gl(f32x16 (&t)[NB0 + NB1], const float* __restrict__ X, int F0, int ld,
+                                            int loff, const float* lds, int F1) {
+  const int lane = lane_id(), h4 = 4 * (lane >> 5);
+  const float* l = lds + h4 * 32 + (lane & 31);
+#pragma unroll
+  for (int ib = 0; ib < NB0; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u0 = 32 * ib + ru(r);
+      t[ib][r] = (u0 + h4 < F0) ? X[u0 * ld + loff] : 0.f;
+    }
+#pragma unroll
+  for (int ib = 0; ib < NB1; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u0 = 32 * ib + ru(r);
+      t[NB0 + ib][r] = (u0 + h4 < F1) ? l[u0 * 32] : 0.f;
+    }
+}
+// Concatenated input tile from two global feature-major arrays.
+template <int NB0, int NB1>
+__device__ __forceinline__ void load_cat_gg(f32x16 (&t)[NB0 + NB1], const float* __restrict__ X0, int F0,
+                                            const float* __restrict__ X1, int F1, int ld, int loff) {
+  const int h4 = 4 * (lane_id() >> 5);
+#pragma unroll
+  for (int ib = 0; ib < NB0; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u0 = 32 * ib + ru(r);
+      t[ib][r] = (u0 + h4 < F0) ? X0[u0 * ld + loff] : 0.f;
+    }
+#pragma unroll
+  for (int ib = 0; ib < NB1; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u0 = 32 * ib + ru(r);
+      t[NB0 + ib][r] = (u0 + h4 < F1) ? X1[u0 * ld + loff] : 0.f;
+    }
+}
+
+// Per-tile lane context: LDS images, sample column offsets.
+struct Lane {
+  int h, s, h4;
+  int ld, b, loff, poff;  // loff = 4h*ld + b (natural layout), poff = 8h*ld + b (pairing layout)
+  float *bl, *sl;         // BIG / SMALL image at this lane: image[urow*32] = unit (urow + 4h), sample s
+  float* pl;              // BIG at the pairing offset: pl[j0*32] = row j0 + 8h
+};
+__device__ __forceinline__ Lane make_lane(float* big, float* small, int ld, int b) {
+  Lane L;
+  int lane = lane_id();
+  asm volatile("" : "+v"(lane));  // keep lane-derived values inside the tile loop (no LICM + spill)
+  L.h = lane >> 5;
+  L.s = lane & 31;
+  L.h4 = 4 * L.h;
+  L.ld = ld;
+  L.b = b;
+  L.loff = L.h4 * ld + b;
+  L.poff = 8 * L.h * ld + b;
+  L.bl = big + L.h4 * 32 + L.s;
+  L.sl = small + L.h4 * 32 + L.s;
+  L.pl = big + 8 * L.h * 32 + L.s;
+  return L;
+}
+
+// Actor trunk: x -> relu(L1) -> relu(L2) -> heads (mu | logsig) into LDS rows [0, 2*AOUT).
+// Optionally stores h1 / h2 feature-major and returns ReLU masks.
+template <class C>
+__device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* __restrict__ X, int xld, int xoff,
+                                            const Lane& L, float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
+                                            uint64_t& m2lo, uint64_t& m2hi) {
+  {
+    f32x16 x[C::NB_OB];
+    gm_load<C::NB_OB>(x, X, C::OB, xld, xoff);
+    dense<C::NB_OB, C::RV_X>(A.W1, 8, x, A.b1P, [&](int ob, const f32x16& acc) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float v = fmaxf(acc[q], 0.f);
+        L.bl[ur * 32] = v;
+        if (H1g) H1g[ur * L.ld + L.loff] = v;
+        bits |= (uint32_t)(v > 0.f) << q;
+      }
+      setbits(m1lo, m1hi, ob, bits);
+    });
+  }
+  {
+    f32x16 hin[8];
+    lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
+    dense<8, C::RV_H>(A.W2, 8, hin, A.b2P, [&](int ob, const f32x16& acc) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float v = fmaxf(acc[q], 0.f);
+        L.bl[ur * 32] = v;
+        if (H2g) H2g[ur * L.ld + L.loff] = v;
+        bits |= (uint32_t)(v > 0.f) << q;
+      }
+      setbits(m2lo, m2hi, ob, bits);
+    });
+  }
+  {
+    f32x16 hin[8];
+    lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
+    dense<8, C::RV_H>(A.Wh, C::NB_H2, hin, A.bhP, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        if (ur + L.h4 < 2 * C::AOUT) L.bl[ur * 32] = acc[q];
+      }
+    });
+  }
+}
+
+// ACM forward (basic_model.py:118-126): in [s | a_d] -> tanh 64 -> tanh 32 -> tanh(ac)*lim.
+// Writes z1 / z2 / t3 feature-major if given; output c into SMALL rows [0, AC).
+template <class C>
+__device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin)[C::NB_ACMIN], const Lane& L,
+                                            float* Z1g, float* Z2g, float* T3g) {
+  float* small = L.sl - L.h4 * 32 - L.s;
+  dense<C::NB_ACMIN, C::RV_ACMIN>(p.acm.W1, 2, xin, p.acm.b1P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ur = 32 * ob + ru(q);
+      const float v = tanhf(acc[q]);
+      L.sl[ur * 32] = v;
+      if (Z1g) Z1g[ur * L.ld + L.loff] = v;
+    }
+  });
+  f32x16 z1[2];
+  lds_load<2>(z1, small);
+  dense<2, C::RV_Z1>(p.acm.W2, 1, z1, p.acm.b2P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float v = tanhf(acc[q]);
+      L.sl[ru(q) * 32] = v;
+      if (Z2g) Z2g[ru(q) * L.ld + L.loff] = v;
+    }
+  });
+  f32x16 z2[1];
+  lds_load<1>(z2, small);
+  dense<1, C::RV_Z2>(p.acm.W3, 1, z2, p.acm.b3P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = ru(q) + L.h4;
+      if (u < C::AC) {
+        const float t = tanhf(acc[q]);
+        L.sl[ru(q) * 32] = t * p.acm_lim[u];
+        if (T3g) T3g[ru(q) * L.ld + L.loff] = t;
+      }
+    }
+  });
+}
+
+// Critic forward through L2 with q = w3 . relu(h2) + b3 reduced per sample.
+template <class C>
+__device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN], const Lane& L,
+                                                float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
+                                                uint64_t& m2lo, uint64_t& m2hi) {
+  dense<C::NB_CIN, C::RV_CIN>(Q.W1, 8, xin, Q.b1P, [&](int ob, const f32x16& acc) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ur = 32 * ob + ru(q);
+      const float v = fmaxf(acc[q], 0.f);
+      L.bl[ur * 32] = v;
+      if (H1g) H1g[ur * L.ld + L.loff] = v;
+      bits |= (uint32_t)(v > 0.f) << q;
+    }
+    setbits(m1lo, m1hi, ob, bits);
+  });
+  f32x16 hin[8];
+  lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
+  float qp = 0.f;
+  dense<8, C::RV_H>(Q.W2, 8, hin, Q.b2P, [&](int ob, const f32x16& acc) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float v = fmaxf(acc[q], 0.f);
+      if (H2g) H2g[(32 * ob + ru(q)) * L.ld + L.loff] = v;
+      qp = fmaf(v, vec_at(Q.w3P, ob, q), qp);
+      bits |= (uint32_t)(v > 0.f) << q;
+    }
+    setbits(m2lo, m2hi, ob, bits);
+  });
+  return qp + __shfl_xor(qp, 32, 64) + *Q.b3;
+}
+
+// Squash (sac/models.py:37-52) of the pairing-layout heads tile with eps [aout][Bp].
+// Writes a_d = denormalize(tanh(u)*lim) into LDS rows [0, AOUT); returns logpi.
+template <class C>
+__device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&hd)[C::NB_PAIR],
+                                              const float* __restrict__ EPS, const Lane& L) {
+  float lp = 0.f, corr = 0.f;
+  const int h8 = 8 * L.h;
+#pragma unroll
+  for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int j0 = 16 * ib + r;
+      const int j = j0 + h8;
+      if (j < C::AOUT) {
+        const float mu = hd[ib][r];
+        const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
+        const float sc = expf(ls);
+        const float e = EPS[j0 * L.ld + L.poff];
+        const float u = fadd_rn(mu, fmul_rn(e, sc));
+        const float d = fsub_rn(u, mu);
+        const float var = fmul_rn(sc, sc);
+        lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(d, d), 2.f * var), logf(sc)), kLogSqrt2Pi);
+        corr += 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
+        const float a = fmul_rn(tanhf(u), p.actor_lim[j]);
+        L.pl[j0 * 32] = denorm(p, j, a);
+      }
+    }
+  const float tot = lp + __shfl_xor(lp, 32, 64);
+  const float tc = corr + __shfl_xor(corr, 32, 64);
+  return fsub_rn(tot, tc);
+}
+
+// ============================================================================ critic phase
+template <class C>
+__global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
+  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* big = smem + w * kLdsPerWave;
+  float* small = big + 256 * 32;
+  const int ntiles = p.Bp / 32;
+  const int ld = p.Bp;
+  const float alpha = *p.alpha;
+  for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
+    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const int b = L.b;
+    const bool valid = b < p.B;
+    uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    // ---- target action: a' ~ pi(s'), a'_d, logpi'   (sac_acm.py:44-45)
+    actor_trunk<C>(p.actor, p.S2, ld, L.loff, L, nullptr, nullptr, d0, d1, d2, d3);
+#ifdef SPP_CUT
+    if (SPP_CUT == 1) { p.part[tile] = L.bl[0]; continue; }
+#endif
+    float lp2;
+    {
+      f32x16 hd[C::NB_PAIR];
+      load_pair<C>(hd, big);
+      lp2 = squash_write<C>(p, hd, p.EPS1, L);
+    }
+    // ---- critic-target input: [s' | ACM(s', a'_d)] or [s' | a'_d]   (:46-48)
+    f32x16 tin[C::NB_CIN];
+    if constexpr (C::ACMC) {
+      f32x16 xin[C::NB_ACMIN];
+      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S2, C::OB, ld, L.loff, big, C::AOUT);
+      acm_forward<C>(p, xin, L, nullptr, nullptr, nullptr);
+      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB, ld, L.loff, small, C::AC);
+    } else {
+      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB, ld, L.loff, big, C::AOUT);
+    }
+#ifdef SPP_CUT
+    if (SPP_CUT == 2) { p.part[tile] = L.bl[0] + tin[0][3] + lp2; continue; }
+#endif
+    // ---- soft-min twin target (:50-56)
+    const float q1t = critic_forward<C>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    const float q2t = critic_forward<C>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    const float notdone = 1.f - p.DN[b];
+    const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
+#ifdef SPP_CUT
+    if (SPP_CUT == 3) { p.part[tile] = y; continue; }
+#endif
+    // ---- both critics: forward, MSE grad, backward to weight-gradient operands (:117-131)
+    float lq0 = 0.f, lq1 = 0.f;
+#pragma unroll 1
+    for (int i = 0; i < 2; ++i) {
+      uint64_t m1lo = 0, m1hi = 0, m2lo = 0, m2hi = 0;
+      f32x16 xin[C::NB_CIN];
+      load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, ld, L.loff);
+      const CriticDev& Q = p.critic[i];
+      const float q = critic_forward<C>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
+      const float diff = fsub_rn(q, y);
+      const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;  // d mse / dq
+      const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
+      if (i == 0) lq0 = lqi; else lq1 = lqi;
+      if (L.h == 0) p.DQ[i][b] = dq;
+#ifdef SPP_CUT
+      if (SPP_CUT == 4) continue;
+#endif
+      // delta2 = dq * w3 * relu'(h2): staged through the LDS image, stored feature-major
+      float* D2 = p.D2[i];
+      const float* w3 = opaque(Q.w3P);
+#pragma unroll 1
+      for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) {
+          const int ur = 32 * ob + ru(q2);
+          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * vec_at(w3, ob, q2) : 0.f;
+          L.bl[ur * 32] = v;
+          D2[ur * ld + L.loff] = v;
+        }
+      }
+      f32x16 din[8];
+      lds_load<8>(din, big);
+#ifdef SPP_CUT
+      if (SPP_CUT == 5) { p.part[tile] = din[3][5]; continue; }
+#endif
+      // delta1 = (W2^T delta2) * relu'(h1)
+      float* D1 = p.D1[i];
+      dense<8, C::RV_H>(Q.W2T, 8, din, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2)
+          D1[(32 * ob + ru(q2)) * ld + L.loff] = getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f;
+      });
+    }
+    const float s0 = wave_sum(lq0), s1 = wave_sum(lq1);
+    if (lane == 0) {
+      p.part[tile * kParts + 0] = s0;
+      p.part[tile * kParts + 1] = s1;
+    }
+  }
+}
+
+// ============================================================================ actor phase
+// Scratch for the frozen-ACM backward (feature-major, same-lane re-read).
+struct AcmScratch {
+  float *Z1, *Z2, *T3;
+};
+
+template <class C>
+__global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratch z) {
+  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* big = smem + w * kLdsPerWave;
+  float* small = big + 256 * 32;
+  const int ntiles = p.Bp / 32;
+  const int ld = p.Bp;
+  const float alpha = *p.alpha;
+  for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
+    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const int b = L.b;
+    const bool valid = b < p.B;
+    const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
+    // ---- a, logpi = actor(s)  (sac_acm.py:137)
+    uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
+    actor_trunk<C>(p.actor, p.S, ld, L.loff, L, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
+    f32x16 hd[C::NB_PAIR];
+    load_pair<C>(hd, big);
+    const float lp = squash_write<C>(p, hd, p.EPS2, L);  // a_d -> big rows [0, AOUT)
+    // ---- critic input [s | ACM(s, a_d)] or [s | a_d]  (:67-72)
+    f32x16 cin[C::NB_CIN];
+    if constexpr (C::ACMC) {
+      f32x16 xin[C::NB_ACMIN];
+      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S, C::OB, ld, L.loff, big, C::AOUT);
+      acm_forward<C>(p, xin, L, z.Z1, z.Z2, z.T3);
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB, ld, L.loff, small, C::AC);
+    } else {
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB, ld, L.loff, big, C::AOUT);
+    }
+    // ---- q = min(Q1, Q2)(s, c)  (:73-75), masks kept for the backward
+    uint64_t ma0 = 0, ma1 = 0, ma2 = 0, ma3 = 0, mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0;
+    const float q1 = critic_forward<C>(p.critic[0], cin, L, nullptr, nullptr, ma0, ma1, ma2, ma3);
+    const float q2 = critic_forward<C>(p.critic[1], cin, L, nullptr, nullptr, mb0, mb1, mb2, mb3);
+    const float qmin = fminf(q1, q2);
+    // torch.minimum backward: ties split the gradient in half
+    const float gq = valid ? -p.inv_B : 0.f;
+    const float dqa = q1 < q2 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
+    const float dqb = q2 < q1 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
+    // ---- back through both critics to their action input
+    f32x16 dca[C::NB_CA];
+#pragma unroll
+    for (int ib = 0; ib < C::NB_CA; ++ib) dca[ib] = zero16();
+#pragma unroll 1
+    for (int i = 0; i < 2; ++i) {
+      const CriticDev& Q = p.critic[i];
+      const uint64_t k0 = i ? mb0 : ma0, k1 = i ? mb1 : ma1, k2 = i ? mb2 : ma2, k3 = i ? mb3 : ma3;
+      const float dqi = i ? dqb : dqa;
+      const float* w3 = opaque(Q.w3P);
+#pragma unroll 1
+      for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * vec_at(w3, ob, q) : 0.f;
+      }
+      f32x16 din[8];
+      lds_load<8>(din, big);
+      dense<8, C::RV_H>(Q.W2T, 8, din, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
+      });
+      f32x16 d1[8];
+      lds_load<8>(d1, big);
+      dense<8, C::RV_H>(Q.W1Ta, C::NB_CA, d1, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int ib = 0; ib < C::NB_CA; ++ib)
+          if (ib == ob) dca[ib] += acc;
+      });
+    }
+    // ---- through the frozen ACM to d a_d  (basic_model.py:118-126 backward)
+    if constexpr (C::ACMC) {
+      f32x16 dp3[1];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = ru(q) + L.h4;
+        float v = 0.f;
+        if (u < C::AC) {
+          const float t = z.T3[ru(q) * ld + L.loff];
+          v = dca[0][q] * p.acm_lim[u] * (1.f - t * t);
+        }
+        dp3[0][q] = v;
+      }
+      dense<1, C::RV_AC>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float zz = z.Z2[ru(q) * ld + L.loff];
+          L.sl[ru(q) * 32] = acc[q] * (1.f - zz * zz);
+        }
+      });
+      f32x16 dp2[1];
+      lds_load<1>(dp2, small);
+      dense<1, C::RV_Z2>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int ur = 32 * ob + ru(q);
+          const float zz = z.Z1[ur * ld + L.loff];
+          L.sl[ur * 32] = acc[q] * (1.f - zz * zz);
+        }
+      });
+      f32x16 dp1[2];
+      lds_load<2>(dp1, small);
+      dense<2, C::RV_Z1>(p.acm.W1Ta, C::NB_AOUT, dp1, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int ur = 32 * ob + ru(q);
+          if (ur + L.h4 < C::AOUT) L.bl[ur * 32] = acc[q];
+        }
+      });
+    } else {
+#pragma unroll
+      for (int ib = 0; ib < C::NB_CA; ++ib)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int ur = 32 * ib + ru(q);
+          if (ur + L.h4 < C::AOUT) L.bl[ur * 32] = dca[ib][q];
+        }
+    }
+    // ---- heads backward in the pairing layout (squash, denorm, custom loss, logpi)
+    float sac_part = (valid && L.h == 0) ? fsub_rn(alpha * lp, qmin) : 0.f;
+    float dist_part = 0.f;
+    const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
+    const int h8 = 8 * L.h;
+#pragma unroll
+    for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j0 = 16 * ib + r;
+        const int j = j0 + h8;
+        float gmu = 0.f, gls = 0.f;
+        if (j < C::AOUT) {
+          const float mu = hd[ib][r];
+          const float lsr = hd[ib][r + 8];
+          const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
+          const float sc = expf(ls);
+          const float e = p.EPS2[j0 * ld + L.poff];
+          const float u = fadd_rn(mu, fmul_rn(e, sc));
+          const float d = fsub_rn(u, mu);
+          const float t = tanhf(u);
+          const float lim = p.actor_lim[j];
+          const float a = fmul_rn(t, lim);
+          float g_ad = L.pl[j0 * 32];  // from the critics through the ACM
+          float g_a = 0.f;
+          if (p.custom_loss != 0.f) {
+            const float s2 = p.S2[j0 * ld + L.poff];
+            if (p.norm_closs) {
+              const float df = fsub_rn(a, normalize(p, j, s2));
+              g_a += cl_scale * df;
+              dist_part += valid ? df * df : 0.f;
+            } else {
+              const float df = fsub_rn(denorm(p, j, a), s2);
+              g_ad += cl_scale * df;
+              dist_part += valid ? df * df : 0.f;
+            }
+          }
+          g_a += g_ad * denorm_scale(p, j);
+          const float var = fmul_rn(sc, sc);
+          const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
+          const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
+          gmu = gu + g_lp * d / var;
+          const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
+          gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
+          p.ADH[j0 * ld + L.poff] = gmu;
+          p.ADH[(C::AOUT + j0) * ld + L.poff] = gls;
+        }
+        hd[ib][r] = gmu;
+        hd[ib][r + 8] = gls;
+      }
+    // ---- dh2 = Wh^T dheads * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
+    dense<C::NB_PAIR, C::RV_PAIR>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
+        L.bl[ur * 32] = v;
+        p.AD2[ur * ld + L.loff] = v;
+      }
+    });
+    {
+      f32x16 d2[8];
+      lds_load<8>(d2, big);
+      dense<8, C::RV_H>(p.actor.W2T, 8, d2, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          p.AD1[(32 * ob + ru(q)) * ld + L.loff] = getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f;
+      });
+    }
+    const float ps = wave_sum(sac_part);
+    const float pd = wave_sum(dist_part);
+    const float pl = wave_sum((valid && L.h == 0) ? lp : 0.f);
+    if (lane == 0) {
+      p.part[tile * kParts + 2] = ps;
+      p.part[tile * kParts + 3] = pd;
+      p.part[tile * kParts + 4] = pl;
+    }
+  }
+}
+
+// ============================================================================ rollout action
+struct ActArgs {
+  int E, mode, denorm_out;
+  float act_noise;
+  const float *obs, *eps, *noise;  // row-major [E][ob], [E][aout]
+  float *target_out, *env_out;     // [E][aout], [E][ac]
+};
+
+template <class C>
+__global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
+  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* big = smem + w * kLdsPerWave;
+  float* small = big + 256 * 32;
+  const int ntiles = (a.E + 31) / 32;
+  for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
+    const int e = tile * 32 + (lane & 31);
+    const bool valid = e < a.E;
+    const int er = valid ? e : 0;
+    // row-major obs: element (unit u, env e) = obs[e*OB + u] -> ld = 1, offset 4h + e*OB
+    Lane L = make_lane(big, small, 1, er * C::OB);
+    if (a.mode != 0) {
+      uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+      actor_trunk<C>(p.actor, a.obs, 1, L.loff, L, nullptr, nullptr, d0, d1, d2, d3);
+    }
+    f32x16 hd[C::NB_PAIR];
+    if (a.mode != 0) load_pair<C>(hd, big);
+    const int h8 = 8 * L.h;
+#pragma unroll
+    for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j0 = 16 * ib + r;
+        const int j = j0 + h8;
+        if (j < C::AOUT) {
+          const float lim = p.actor_lim[j];
+          float act;
+          if (a.mode == 0) {
+            act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;  // off_policy.py:50-54
+          } else {
+            const float mu = hd[ib][r];
+            float u = mu;
+            if (a.mode == 1 && a.eps) {
+              const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
+              u = fadd_rn(mu, fmul_rn(valid ? a.eps[er * C::AOUT + j] : 0.f, expf(ls)));
+            }
+            act = fmul_rn(tanhf(u), lim);
+            if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
+            act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);  // ddpg_acm.py:43-45
+          }
+          if (a.denorm_out) act = denorm(p, j, act);
+          L.pl[j0 * 32] = act;
+          if (valid) a.target_out[er * C::AOUT + j] = act;
+        }
+      }
+    // env action = ACM(cat(obs, a))  (off_policy.py:89-106)
+    f32x16 xin[C::NB_ACMIN];
+    load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, a.obs, C::OB, 1, L.loff, big, C::AOUT);
+    acm_forward<C>(p, xin, L, nullptr, nullptr, nullptr);
+    if (L.h == 0 && valid)
+      for (int u = 0; u < C::AC; ++u) a.env_out[er * C::AC + u] = small[u * 32 + L.s];
+  }
+}
+
+// ============================================================================ ACM regression
+// acm.py:246-258: forward + MSE backward; writes the dW operands feature-major.
+struct AcmRegArgs {
+  int B, Bp;
+  const float *x, *y;                   // row-major [B][2ob], [B][ac]
+  float *XT, *Z1, *Z2, *P1, *P2, *P3;  // feature-major [.][Bp]
+  float* part;                          // [ntiles]
+};
+
+template <class C>
+__global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g) {
+  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* big = smem + w * kLdsPerWave;
+  float* small = big + 256 * 32;
+  const int ntiles = g.Bp / 32;
+  const int ld = g.Bp;
+  constexpr int IN = 2 * C::OB;
+  constexpr int NB_IN = blocks_of(IN);
+  constexpr uint64_t RV_IN = rv_nat(IN, NB_IN);
+  for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
+    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const int b = L.b;
+    const bool valid = b < g.B;
+    const int br = valid ? b : 0;
+    f32x16 xin[NB_IN];
+#pragma unroll
+    for (int ib = 0; ib < NB_IN; ++ib)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ur = 32 * ib + ru(r);
+        const int u = ur + L.h4;
+        const float v = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
+        xin[ib][r] = v;
+        if (u < IN) g.XT[ur * ld + L.loff] = v;
+      }
+    dense<NB_IN, RV_IN>(p.acm.W1, 2, xin, p.acm.b1P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float v = tanhf(acc[q]);
+        L.sl[ur * 32] = v;
+        g.Z1[ur * ld + L.loff] = v;
+      }
+    });
+    f32x16 z1[2];
+    lds_load<2>(z1, small);
+    dense<2, C::RV_Z1>(p.acm.W2, 1, z1, p.acm.b2P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float v = tanhf(acc[q]);
+        L.sl[ru(q) * 32] = v;
+        g.Z2[ru(q) * ld + L.loff] = v;
+      }
+    });
+    f32x16 z2[1];
+    lds_load<1>(z2, small);
+    float lsum = 0.f;
+    f32x16 p3[1];
+    const float sc = 2.f / ((float)g.B * (float)C::AC);
+    dense<1, C::RV_Z2>(p.acm.W3, 1, z2, p.acm.b3P, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = ru(q) + L.h4;
+        float v = 0.f;
+        if (u < C::AC && valid) {
+          const float t = tanhf(acc[q]);
+          const float lim = p.acm_lim[u];
+          const float df = fsub_rn(fmul_rn(t, lim), g.y[br * C::AC + u]);
+          lsum += df * df;
+          v = sc * df * lim * (1.f - t * t);
+        }
+        p3[0][q] = v;
+        if (u < C::AC) g.P3[ru(q) * ld + L.loff] = v;
+      }
+    });
+    dense<1, C::RV_AC>(p.acm.W3T, 1, p3, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float zz = z2[0][q];
+        const float v = acc[q] * (1.f - zz * zz);
+        L.sl[ru(q) * 32] = v;
+        g.P2[ru(q) * ld + L.loff] = v;
+      }
+    });
+    f32x16 p2[1];
+    lds_load<1>(p2, small);
+    dense<1, C::RV_Z2>(p.acm.W2T, 2, p2, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float zz = ob == 0 ? z1[0][q] : z1[1][q];
+        g.P1[ur * ld + L.loff] = acc[q] * (1.f - zz * zz);
+      }
+    });
+    const float ls = wave_sum(lsum);
+    if (lane == 0) g.part[tile] = ls;
+  }
+}
+
+// ============================================================================ staging
+// Row-major caller batch (sample_batch layout) -> feature-major padded scratch.
+struct StageArgs {
+  int B, Bp, ob, aout, ac;
+  const float *obs, *next_obs, *act, *rew, *acm;
+  const int8_t* done;
+  const float *eps1, *eps2;  // [B][aout] or NULL
+  float *S, *S2, *ACT, *AENV, *R, *DN, *EPS1, *EPS2;
+};
+__global__ void k_stage_batch(StageArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.Bp) return;
+  const bool v = b < a.B;
+  const int64_t ld = a.Bp;
+  for (int f = 0; f < a.ob; ++f) {
+    a.S[f * ld + b] = v ? a.obs[b * a.ob + f] : 0.f;
+    a.S2[f * ld + b] = v ? a.next_obs[b * a.ob + f] : 0.f;
+  }
+  for (int f = 0; f < a.aout; ++f) {
+    if (a.act) a.ACT[f * ld + b] = v ? a.act[b * a.aout + f] : 0.f;
+    if (a.eps1) a.EPS1[f * ld + b] = v ? a.eps1[b * a.aout + f] : 0.f;
+    if (a.eps2) a.EPS2[f * ld + b] = v ? a.eps2[b * a.aout + f] : 0.f;
+  }
+  for (int f = 0; f < a.ac; ++f) a.AENV[f * ld + b] = v ? a.acm[b * a.ac + f] : 0.f;
+  a.R[b] = v ? a.rew[b] : 0.f;
+  a.DN[b] = v ? (float)a.done[b] : 0.f;
+}
+
+// Caller eps [B][aout] -> feature-major [aout][Bp] (zero padded).
+__global__ void k_eps_copy_fm(const float* eps, float* E, int aout, int B, int Bp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)aout * Bp) return;
+  const int64_t j = i / Bp, b = i % Bp;
+  E[i] = b < B ? eps[b * aout + j] : 0.f;
+}
+
+// Device-side Gaussian eps straight into the feature-major layout (zero padded).
+__global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint64_t ctr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pair index
+  const int64_t n = (int64_t)aout * Bp;
+  if (2 * i >= n) return;
+  u32x4 r = philox(seed, ctr, (uint64_t)i);
+  float n0, n1;
+  box_muller(r.x, r.y, n0, n1);
+  for (int k = 0; k < 2; ++k) {
+    const int64_t idx = 2 * i + k;
+    if (idx < n) E[idx] = ((idx % Bp) < B) ? (k ? n1 : n0) : 0.f;
+  }
+}
+
+// ============================================================================ debug dense
+template <int NBI>
+__global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const float* bP, const float* x, float* y, int B,
+                                                    int K, int N, int act) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, s = lane & 31;
+  const int64_t b = (int64_t)blockIdx.x * 32 + s;
+  f32x16 in[NBI];
+#pragma unroll
+  for (int ib = 0; ib < NBI; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = 32 * ib + unit_of(r, h);
+      in[ib][r] = (u < K && b < B) ? x[b * K + u] : 0.f;
+    }
+  dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, bP, [&](int ob, const f32x16& acc) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * ob + unit_of(q, h);
+      float v = acc[q];
+      if (act == 1) v = fmaxf(v, 0.f);
+      if (act == 2) v = tanhf(v);
+      if (u < N && b < B) y[b * N + u] = v;
+    }
+  });
+}
+
+}  // namespace spp

@@ -1,0 +1,12 @@
+"""spprl — MI355X-native SPP-RL hot path (rollout -> HBM replay -> SAC_AcM update).
+
+Host side keeps rltoolkit's agent / buffer API; all device work runs in
+libspprl.so (hand-written HIP kernels for gfx950) through the C-ABI in
+include/spprl.h.
+"""
+from . import _lib, config, nets  # noqa: F401
+from ._lib import SppError, load  # noqa: F401
+from .replay import BufferAcMOffPolicy  # noqa: F401
+from .sac_acm import SAC_AcM  # noqa: F401
+
+__all__ = ["SAC_AcM", "BufferAcMOffPolicy", "SppError", "load"]

@@ -1,0 +1,35 @@
+"""Defaults of the hot path, mirroring rltoolkit/config.py (reference @ v0).
+
+Only the constants that shape the SPP off-policy rollout/update path are kept.
+"""
+GAMMA = 0.95
+DDPG_LR = 1e-3
+TAU = 0.005
+UPDATE_BATCH_SIZE = 100
+BUFFER_SIZE = int(1e6)
+RANDOM_FRAMES = 100
+UPDATE_FREQ = 50
+GRAD_STEPS = 50
+ACT_NOISE = 0.1
+ALPHA_LR = 1e-3
+ALPHA = 0.2
+ACM_LR = 3e-3
+ACM_BATCH_SIZE = 128
+ACM_UPDATE_FREQ = 1
+ACM_CRITIC = False
+MIN_MAX_DENORMALIZE = False
+DENORMALIZE_ACTOR_OUT = False
+NORM_CLOSS = True
+OBS_NORM = False
+MAX_ABS_OBS_VALUE = 10
+
+# gym env shapes the reference trains on (observation dim, action dim, action high,
+# episode limit); gym/mujoco themselves are not part of the hot path.
+ENV_SPECS = {
+    "Hopper-v2": (11, 3, 1.0, 1000),
+    "HalfCheetah-v2": (17, 6, 1.0, 1000),
+    "Walker2d-v2": (17, 6, 1.0, 1000),
+    "Ant-v2": (111, 8, 1.0, 1000),
+    "Ant-v3": (111, 8, 1.0, 1000),
+    "Pendulum-v0": (3, 1, 2.0, 200),
+}

@@ -1,0 +1,159 @@
+"""HBM-resident BufferAcMOffPolicy (rltoolkit/buffer/replay_buffer.py:303-401).
+
+Same method names and semantics as the reference, including the obs-index ring
+and its wrap rule (Q6).  Batched variants (``add_obs_batch`` / ``add_timestep_batch``)
+apply the reference recurrence to E lockstep envs in env order.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_handle
+
+
+class BufferAcMOffPolicy:
+    def __init__(self, size, obs_shape, act_shape, acm_act_shape, device="cuda", min_max_denormalize=False,
+                 obs_mean=None, obs_std=None, max_obs=None, min_obs=None, obs_norm=False, dtype=torch.float32):
+        _lib.load()
+        self.size, self.obs_shape, self.act_shape, self.acm_act_shape = int(size), obs_shape, act_shape, acm_act_shape
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.obs_norm = obs_norm
+        self.min_max_denormalize = min_max_denormalize
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        call("sppReplayCreate", ctypes.byref(h), self.size, obs_shape, act_shape, acm_act_shape, dev)
+        self._h = h
+        z = lambda v: None if v is None else torch.as_tensor(v, dtype=torch.float32, device=self.device)  # noqa
+        # ReplayBuffer.__init__ :113-115: identity z-score normaliser until the first stats update
+        self.obs_mean = z(obs_mean) if obs_mean is not None else torch.zeros(obs_shape, device=self.device)
+        self.obs_std = z(obs_std) if obs_std is not None else torch.ones(obs_shape, device=self.device)
+        self.max_obs = z(max_obs) if max_obs is not None else torch.zeros(obs_shape, device=self.device)
+        self.min_obs = z(min_obs) if min_obs is not None else torch.zeros(obs_shape, device=self.device)
+        self._have_minmax = max_obs is not None and min_obs is not None
+        self._pending_acm = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib.load().sppReplayDestroy(h)
+            self._h = None
+
+    # ------------------------------------------------------------------ state
+    def _state(self):
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        call("sppReplayState", self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    @property
+    def obs_idx(self):
+        return self._state()[0]
+
+    @property
+    def ts_idx(self):
+        return self._state()[1]
+
+    @property
+    def current_len(self):
+        return self._state()[2]
+
+    def __len__(self):
+        return self._state()[2]
+
+    def reset_idx(self):
+        call("sppReplayReset", self._h)
+
+    def view(self):
+        v = _lib.ReplayView()
+        call("sppReplayGetView", self._h, ctypes.byref(v))
+        return v
+
+    # ------------------------------------------------------------------ writes
+    def _dev(self, x, dtype=torch.float32):
+        return torch.as_tensor(x, dtype=dtype).to(self.device).contiguous()
+
+    def add_obs_batch(self, obs):
+        """obs [E, ob] -> slots (numpy int64 [E])"""
+        o = self._dev(obs).reshape(-1, self.obs_shape)
+        slots = np.empty(o.shape[0], np.int64)
+        call("sppReplayAddObs", self._h, ptr(o), o.shape[0], slots.ctypes.data_as(ctypes.c_void_p), stream_handle())
+        return slots
+
+    def add_obs(self, obs):
+        """MetaReplayBuffer.add_obs (:56-60)"""
+        return int(self.add_obs_batch(torch.as_tensor(obs).reshape(1, -1))[0])
+
+    def add_acm_action(self, acm_action):
+        """BufferAcMOffPolicy.add_acm_action (:332-333): stored at ts_idx by the next add_timestep."""
+        self._pending_acm = self._dev(acm_action).reshape(1, self.acm_act_shape)
+
+    def add_timestep_batch(self, prev, nxt, action, rew, done, end, acm_action=None):
+        E = len(prev)
+        prev = np.ascontiguousarray(prev, np.int64)
+        nxt = np.ascontiguousarray(nxt, np.int64)
+        act = self._dev(action).reshape(E, self.act_shape)
+        acm = self._dev(acm_action).reshape(E, self.acm_act_shape) if acm_action is not None else None
+        r = self._dev(rew).reshape(E)
+        d = self._dev(done, torch.uint8).reshape(E)
+        e = self._dev(end, torch.uint8).reshape(E)
+        call("sppReplayAddStep", self._h, prev.ctypes.data_as(ctypes.c_void_p), nxt.ctypes.data_as(ctypes.c_void_p),
+             E, ptr(act), ptr(acm), ptr(r), ptr(d), ptr(e), stream_handle())
+
+    def add_timestep(self, obs_idx, next_obs_idx, action, rew, done, end):
+        """add_timestep (:65-75) + ReplayBuffer.addition (:133-137)"""
+        acm = self._pending_acm
+        self._pending_acm = None
+        self.add_timestep_batch([obs_idx], [next_obs_idx], torch.as_tensor(action).reshape(1, -1), [float(rew)],
+                                [bool(done)], [bool(end)], acm)
+
+    # ------------------------------------------------------------------ reads
+    def gather(self, idx):
+        """Tuples for given indices, reference layout (sample_batch :385-398)."""
+        idx = torch.as_tensor(idx, dtype=torch.int64).to(self.device).contiguous()
+        B = idx.numel()
+        f = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa
+        obs, nobs, act, rew, acm = f(B, self.obs_shape), f(B, self.obs_shape), f(B, self.act_shape), f(B), f(
+            B, self.acm_act_shape)
+        done = torch.empty(B, dtype=torch.int8, device=self.device)
+        call("sppReplayGather", self._h, ptr(idx), B, ptr(obs), ptr(nobs), ptr(act), ptr(rew), ptr(done), ptr(acm),
+             stream_handle())
+        if self.obs_norm:
+            obs, nobs = self.normalize(obs), self.normalize(nobs)
+        return [obs, nobs, act, rew, done, acm]
+
+    def sample_batch(self, batch_size=64, device=None):
+        """idx = np.random.randint(0, len, B) from numpy's global stream (replay_buffer.py:234)."""
+        idx = np.random.randint(0, len(self), batch_size)
+        return self.gather(idx)
+
+    def sample_acm_batch(self, batch_size=64):
+        idx = np.random.randint(0, len(self), batch_size)
+        o, no, _, _, _, acm = self.gather(idx)
+        return [o, no, acm]
+
+    # ------------------------------------------------------------------ normaliser
+    def update_obs_mean_std(self):
+        """MetaReplayBuffer.update_obs_mean_std (:83-96), on device."""
+        if len(self) <= 10:
+            return
+        call("sppReplayObsStats", self._h, ptr(self.obs_mean), ptr(self.obs_std), ptr(self.max_obs),
+             ptr(self.min_obs), 0 if self._have_minmax else 1, stream_handle())
+        self._have_minmax = True
+
+    def normalize(self, obs, force=False):
+        if not (self.obs_norm or force):
+            return obs
+        if self.min_max_denormalize:
+            if not self._have_minmax:
+                return obs
+            mean = (self.max_obs + self.min_obs) / 2
+            return (obs - mean) / (self.max_obs - mean + 1e-8)
+        return torch.clamp((obs - self.obs_mean) / (self.obs_std + 1e-8), -10, 10)
+
+    def denormalize(self, obs):
+        if self.min_max_denormalize:
+            mean = (self.max_obs + self.min_obs) / 2
+            return mean + obs * ((self.max_obs - self.min_obs) / 2)
+        return (self.obs_std + 1e-8) * obs + self.obs_mean

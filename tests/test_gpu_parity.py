@@ -40,8 +40,9 @@ def test_dense_tile_matches_torch(K, N, act):
     W = torch.randn(N, K) / np.sqrt(K)
     b = torch.randn(N)
     y = torch.empty(B, N, device=DEV)
-    _lib.call("sppDebugDense", _lib.ptr(x.to(DEV)), _lib.ptr(W.to(DEV)), _lib.ptr(b.to(DEV)), _lib.ptr(y), B, K, N,
-              act, _lib.stream_handle())
+    xd, Wd, bd = x.to(DEV), W.to(DEV), b.to(DEV)  # keep the device copies alive across the call
+    _lib.call("sppDebugDense", _lib.ptr(xd), _lib.ptr(Wd), _lib.ptr(bd), _lib.ptr(y), B, K, N, act,
+              _lib.stream_handle())
     ref = x.double() @ W.double().T + b.double()
     if act == 1:
         ref = ref.clamp_min(0)

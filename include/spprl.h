@@ -161,12 +161,20 @@ typedef struct {
 sppStatus sppSacAcmUpdate(sppAgentHandle h, const sppBatch* batch, const float* eps_next, const float* eps_cur,
                           float* losses_dev, void* stream);
 /* The same step split at its two exchange points for data-parallel training:
- * grads -> (caller all-reduces the flat grad buffers, averaging) -> apply. */
+ * grads -> (caller all-reduces the flat grad buffers, averaging) -> apply.
+ * batch == NULL / eps == NULL use the staged batch / staged eps (see below).
+ * ActorGrads also writes the temperature-gradient operand mean(-logpi - H)
+ * into the bound alpha-grad scalar, which the caller all-reduces with the
+ * actor gradients; ActorApply consumes it. */
 sppStatus sppSacAcmCriticGrads(sppAgentHandle h, const sppBatch* batch, const float* eps_next,
                                float* losses_dev, void* stream);
 sppStatus sppSacAcmCriticApply(sppAgentHandle h, void* stream);
 sppStatus sppSacAcmActorGrads(sppAgentHandle h, const float* eps_cur, float* losses_dev, void* stream);
 sppStatus sppSacAcmActorApply(sppAgentHandle h, float* losses_dev, void* stream);
+/* Caller-owned device float[1] receiving mean(-logpi - H) (sac.py:214-216). */
+sppStatus sppAgentBindAlphaGrad(sppAgentHandle h, float* alpha_grad_dev);
+/* Draw both rsample eps tensors of the staged batch on device (Philox, (seed, counter)). */
+sppStatus sppSacAcmDrawEps(sppAgentHandle h, uint64_t seed, uint64_t counter, void* stream);
 /* Fused replay sample + gather into the agent's staging area (device indices). */
 sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int B,
                                   void* stream);
@@ -179,6 +187,20 @@ sppStatus sppSacAcmUpdateStaged(sppAgentHandle h, uint64_t seed, uint64_t counte
  * -> MSE loss (device float) and one Adam step on the bound ACM net. */
 sppStatus sppAcmRegressStep(sppAgentHandle h, const float* x, const float* y, int B, float* loss_dev,
                             void* stream);
+/* The same split for data-parallel use: grads (into the bound ACM grad buffer) / apply. */
+sppStatus sppAcmRegressGrads(sppAgentHandle h, const float* x, const float* y, int B, float* loss_dev,
+                             void* stream);
+sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
+/* ACM regression batch straight from the ring (rbuffer_sample_acm, replay_buffer.py:404-430 +
+ * acm_cat, acm.py:260-264): x = [obs | next_obs] [B][2ob], y = acm action [B][ac]. */
+sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
+
+/* Per-kernel device timing (HIP events on the launch stream), for measurement:
+ * kinds 0 critic-phase, 1 actor-phase, 2 weight-grad GEMMs, 3 Adam, 4 ACM regression.
+ * GetTiming synchronises on the recorded events, returns total ms and launch
+ * counts per kind, and clears them. */
+sppStatus sppAgentSetTiming(sppAgentHandle h, int enable);
+sppStatus sppAgentGetTiming(sppAgentHandle h, double* ms_out /*[5]*/, int64_t* count_out /*[5]*/);
 
 /* Rollout action (rltoolkit/acm/off_policy/ddpg_acm.py:40-50 noise_action +
  * off_policy.py:50-54 initial_act + :89-106 process_action):

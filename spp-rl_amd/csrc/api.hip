@@ -423,7 +423,23 @@ struct sppAgent {
   } dws[2];
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
+  float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
+  // per-kernel timing (HIP events on the launch stream)
+  bool timing = false;
+  std::vector<hipEvent_t> tev[5];
+  size_t tused[5] = {0, 0, 0, 0, 0};
 };
+
+static void tmark(sppAgent* a, int kind, hipStream_t st) {
+  if (!a->timing) return;
+  auto& v = a->tev[kind];
+  if (a->tused[kind] == v.size()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    v.push_back(e);
+  }
+  hipEventRecord(v[a->tused[kind]++], st);
+}
 
 namespace spp {
 
@@ -575,8 +591,8 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
   auto J = [&](const float* A, int N, const float* X0, int K0, const float* X1, int K1, float* dW, float* db) {
     DwJob j{};
     j.A = A; j.N = N; j.X0 = X0; j.K0 = K0; j.X1 = X1; j.K1 = K1; j.dW = dW; j.db = db; j.Bp = Bp;
-    const double work = (double)Bp * ((N + 31) & ~31) * (((K0 + K1) + 31) & ~31);
-    int ns = (int)std::ceil(work / (256.0 * 256.0 * 2048.0));
+    // every work item covers <= 2048 samples so no job's items serialise the launch
+    int ns = cdiv(Bp, 2048);
     ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
     j.split_len = (int)round_up(cdiv(Bp, ns), 32);
     j.nsplit = cdiv(Bp, j.split_len);
@@ -765,6 +781,8 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   a->nsize[SPP_NET_ACM] = acm_size(2 * ob, ac);
   a->Bmax = cfg->max_batch;
   const int64_t Bp = round_up(cfg->max_batch, 32);
+  SPP_REQUIRE(Bp * 256 < ((int64_t)1 << 31), SPP_E_SHAPE, "max_batch %d too large (32-bit scratch offsets)",
+              cfg->max_batch);
   a->Bpmax = (int)Bp;
   const int64_t ntiles = Bp / 32;
   // scratch arena
@@ -812,6 +830,8 @@ sppStatus sppAgentDestroy(sppAgentHandle a) {
   hipSetDevice(a->device);
   hipDeviceSynchronize();
   a->limits.release(); a->pk.release(); a->pv.release(); a->d_pj.release(); a->d_vj.release();
+  for (auto& v : a->tev)
+    for (auto e : v) hipEventDestroy(e);
   a->scratch.release(); a->d_adam.release();
   for (auto& D : a->dws) { D.slab.release(); D.jobs.release(); D.items.release(); }
   delete a;
@@ -901,9 +921,13 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
               a->vo_actor, (int)(a->vj_actor.size() + a->vj_acm.size() + a->vj_targ.size() + a->vj_critic.size()), st);
   SacArgs p = make_args(a, B);
   const int grid = phase_grid(a, p.Bp);
+  tmark(a, 0, st);
   hipLaunchKernelGGL(a->ks.critic, dim3(grid), dim3(256), 0, st, p);
+  tmark(a, 0, st);
   SPP_CHECK_HIP(hipGetLastError());
+  tmark(a, 2, st);
   launch_dw(a, 0, 0, st);
+  tmark(a, 2, st);
   hipLaunchKernelGGL(k_finalize_critic, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
@@ -912,16 +936,24 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
 sppStatus sppSacAcmCriticGrads(sppAgentHandle a, const sppBatch* bt, const float* eps_next, float* losses,
                                void* stream) {
   SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
-  SPP_REQUIRE(eps_next, SPP_E_INVALID_ARG, "eps_next required (use the staged API for device draws)");
-  sppStatus s = stage(a, bt, eps_next, nullptr, S(stream));
-  if (s) return s;
+  if (bt) {
+    sppStatus s = stage(a, bt, eps_next, nullptr, S(stream));
+    if (s) return s;
+  } else if (eps_next) {
+    const int Bp = (int)round_up(a->cur_B, 32);
+    SPP_REQUIRE(a->cur_B > 0, SPP_E_STATE, "no staged batch");
+    hipLaunchKernelGGL(k_eps_copy_fm, dim3(cdiv((int64_t)a->cfg.aout * Bp, 256)), dim3(256), 0, S(stream), eps_next,
+                       a->EPS1, a->cfg.aout, a->cur_B, Bp);
+  }
   return critic_grads_staged(a, losses, S(stream));
 }
 
 sppStatus sppSacAcmCriticApply(sppAgentHandle a, void* stream) {
   SPP_REQUIRE(a && a->d_adam.ptr, SPP_E_STATE, "agent not ready");
   a->steps[1] += 1;
+  tmark(a, 3, S(stream));
   launch_adam(a, 0, 2, a->net[SPP_NET_CRITIC1].n, a->steps[1], a->cfg.critic_lr, a->cfg.tau, S(stream));
+  tmark(a, 3, S(stream));
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -934,32 +966,80 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   SacArgs p = make_args(a, B);
   AcmScratch z{a->Z1, a->Z2, a->T3};
   const int grid = phase_grid(a, p.Bp);
+  tmark(a, 1, st);
   hipLaunchKernelGGL(a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
+  tmark(a, 1, st);
   SPP_CHECK_HIP(hipGetLastError());
+  tmark(a, 2, st);
   launch_dw(a, 0, 1, st);
-  (void)losses;
+  tmark(a, 2, st);
+  hipLaunchKernelGGL(k_actor_partials, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, a->cfg.aout,
+                     a->cfg.custom_loss, (double)a->cfg.target_entropy, a->alpha_grad ? a->alpha_grad : a->aux,
+                     losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
 
 sppStatus sppSacAcmActorGrads(sppAgentHandle a, const float* eps_cur, float* losses, void* stream) {
-  SPP_REQUIRE(a && eps_cur, SPP_E_INVALID_ARG, "null");
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
   const int B = a->cur_B;
   SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
   const int Bp = (int)round_up(B, 32);
-  hipLaunchKernelGGL(k_eps_copy_fm, dim3(cdiv((int64_t)a->cfg.aout * Bp, 256)), dim3(256), 0, S(stream), eps_cur,
-                     a->EPS2, a->cfg.aout, B, Bp);
+  if (eps_cur)
+    hipLaunchKernelGGL(k_eps_copy_fm, dim3(cdiv((int64_t)a->cfg.aout * Bp, 256)), dim3(256), 0, S(stream), eps_cur,
+                       a->EPS2, a->cfg.aout, B, Bp);
   return actor_grads(a, losses, S(stream));
+}
+
+sppStatus sppAgentBindAlphaGrad(sppAgentHandle a, float* g) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  a->alpha_grad = g;
+  return SPP_OK;
+}
+
+sppStatus sppSacAcmDrawEps(sppAgentHandle a, uint64_t seed, uint64_t counter, void* stream) {
+  SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "no staged batch");
+  const int B = a->cur_B, Bp = (int)round_up(B, 32);
+  const int64_t pairs = ((int64_t)a->cfg.aout * Bp + 1) / 2;
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, S(stream), a->EPS1, a->cfg.aout, B, Bp, seed,
+                     2 * counter);
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, S(stream), a->EPS2, a->cfg.aout, B, Bp, seed,
+                     2 * counter + 1);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAgentSetTiming(sppAgentHandle a, int enable) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
+  a->timing = enable != 0;
+  return SPP_OK;
+}
+
+sppStatus sppAgentGetTiming(sppAgentHandle a, double* ms, int64_t* cnt) {
+  SPP_REQUIRE(a && ms && cnt, SPP_E_INVALID_ARG, "null");
+  for (int k = 0; k < 5; ++k) {
+    double t = 0.0;
+    for (size_t i = 0; i + 1 < a->tused[k]; i += 2) {
+      SPP_CHECK_HIP(hipEventSynchronize(a->tev[k][i + 1]));
+      float e = 0.f;
+      SPP_CHECK_HIP(hipEventElapsedTime(&e, a->tev[k][i], a->tev[k][i + 1]));
+      t += e;
+    }
+    ms[k] = t;
+    cnt[k] = (int64_t)(a->tused[k] / 2);
+    a->tused[k] = 0;
+  }
+  return SPP_OK;
 }
 
 static sppStatus actor_apply(sppAgentHandle a, float* losses, hipStream_t st) {
   a->steps[0] += 1;
   a->steps[2] += 1;
+  tmark(a, 3, st);
   launch_adam(a, 2, 1, a->net[SPP_NET_ACTOR].n, a->steps[0], a->cfg.actor_lr, 0.f, st);
-  const int Bp = (int)round_up(a->cur_B, 32);
-  hipLaunchKernelGGL(k_finalize_actor_alpha, dim3(1), dim3(256), 0, st, (const float*)a->part, Bp / 32, a->cur_B,
-                     a->cfg.aout, a->cfg.custom_loss, (double)a->cfg.target_entropy, (double)a->cfg.alpha_lr,
-                     a->steps[2], a->alpha_state, a->alpha_f32, losses);
+  tmark(a, 3, st);
+  hipLaunchKernelGGL(k_alpha_step, dim3(1), dim3(64), 0, st, (const float*)(a->alpha_grad ? a->alpha_grad : a->aux),
+                     (double)a->cfg.alpha_lr, a->steps[2], a->alpha_state, a->alpha_f32, losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -995,21 +1075,17 @@ sppStatus sppAgentStageFromReplay(sppAgentHandle a, sppReplayHandle r, const int
 sppStatus sppSacAcmUpdateStaged(sppAgentHandle a, uint64_t seed, uint64_t counter, float* losses, void* stream) {
   SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "no staged batch");
   hipStream_t st = S(stream);
-  const int B = a->cur_B, Bp = (int)round_up(B, 32);
-  const int64_t pairs = ((int64_t)a->cfg.aout * Bp + 1) / 2;
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, st, a->EPS1, a->cfg.aout, B, Bp, seed,
-                     2 * counter);
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, st, a->EPS2, a->cfg.aout, B, Bp, seed,
-                     2 * counter + 1);
-  sppStatus s;
+  sppStatus s = sppSacAcmDrawEps(a, seed, counter, stream);
+  if (s) return s;
   if ((s = critic_grads_staged(a, losses, st))) return s;
   if ((s = sppSacAcmCriticApply(a, stream))) return s;
   if ((s = actor_grads(a, losses, st))) return s;
   return actor_apply(a, losses, st);
 }
 
-sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, int B, float* loss, void* stream) {
-  SPP_REQUIRE(a && x && y && B > 0 && B <= a->Bmax, SPP_E_INVALID_ARG, "acm step: bad args");
+sppStatus sppAcmRegressGrads(sppAgentHandle a, const float* x, const float* y, int B, float* loss, void* stream) {
+  SPP_REQUIRE(a && x && y && B > 0 && B <= a->Bmax, SPP_E_INVALID_ARG, "acm step: bad args (B=%d, max %d)", B,
+              a->Bmax);
   hipStream_t st = S(stream);
   sppStatus s = check_ready(a);
   if (s) return s;
@@ -1022,12 +1098,33 @@ sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, in
   AcmRegArgs g{};
   g.B = B; g.Bp = (int)round_up(B, 32); g.x = x; g.y = y;
   g.XT = a->RX; g.Z1 = a->RZ1; g.Z2 = a->RZ2; g.P1 = a->RP1; g.P2 = a->RP2; g.P3 = a->RP3; g.part = a->part;
+  tmark(a, 4, st);
   hipLaunchKernelGGL(a->ks.acmreg, dim3(phase_grid(a, g.Bp)), dim3(256), 0, st, p, g);
   SPP_CHECK_HIP(hipGetLastError());
   launch_dw(a, 1, 0, st);
+  tmark(a, 4, st);
   hipLaunchKernelGGL(k_finalize_acm, dim3(1), dim3(256), 0, st, (const float*)a->part, g.Bp / 32, B, a->cfg.ac, loss);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
+  SPP_REQUIRE(a && a->d_adam.ptr, SPP_E_STATE, "agent not ready");
   a->steps[3] += 1;
-  launch_adam(a, 3, 1, a->net[SPP_NET_ACM].n, a->steps[3], a->cfg.acm_lr, 0.f, st);
+  launch_adam(a, 3, 1, a->net[SPP_NET_ACM].n, a->steps[3], a->cfg.acm_lr, 0.f, S(stream));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, int B, float* loss, void* stream) {
+  sppStatus s = sppAcmRegressGrads(a, x, y, B, loss, stream);
+  if (s) return s;
+  return sppAcmRegressApply(a, stream);
+}
+
+sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx, int B, float* x, float* y, void* stream) {
+  SPP_REQUIRE(h && idx && x && y && B > 0, SPP_E_INVALID_ARG, "gather_acm: bad args");
+  hipLaunchKernelGGL(k_replay_gather_acm, dim3(cdiv(B, 256)), dim3(256), 0, S(stream), h->d, idx, B, x, y);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

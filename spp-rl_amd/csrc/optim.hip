@@ -97,21 +97,32 @@ __global__ void k_finalize_critic(const float* part, int ntiles, int B, float* l
   }
 }
 
-// Actor losses + temperature Adam step (sac.py:201-216, sac_acm.py:153-159).
-// alpha_state = {log_alpha, m, v, alpha} (double)
-__global__ void k_finalize_actor_alpha(const float* part, int ntiles, int B, int aout, float custom_loss,
-                                       double target_entropy, double lr, int64_t step, double* alpha_state,
-                                       float* alpha_f32, float* losses) {
+// Actor losses (sac_acm.py:77-86) and the temperature-gradient operand
+// c = mean(-logpi - H) (sac.py:214-216), written for an optional all-reduce.
+__global__ void k_actor_partials(const float* part, int ntiles, int B, int aout, float custom_loss,
+                                 double target_entropy, float* alpha_grad, float* losses) {
   const double ssac = block_sum(part, ntiles, 8, 2);
   const double sdist = block_sum(part, ntiles, 8, 3);
   const double slp = block_sum(part, ntiles, 8, 4);
   if (threadIdx.x != 0) return;
   const double sac = ssac / B;
   const double dist = sdist / ((double)B * aout);
-  const double actor = custom_loss != 0.f ? sac + (double)custom_loss * dist : sac;
+  *alpha_grad = (float)(-(slp / B) - target_entropy);
+  if (losses) {
+    losses[2] = (float)(custom_loss != 0.f ? sac + (double)custom_loss * dist : sac);
+    losses[3] = custom_loss != 0.f ? (float)sac : 0.f;
+    losses[4] = custom_loss != 0.f ? (float)dist : 0.f;
+  }
+}
+
+// Temperature Adam step on float64 log_alpha (sac.py:107-110, sac_acm.py:153-159).
+// alpha_state = {log_alpha, m, v, alpha}; g = exp(log_alpha) * c.
+__global__ void k_alpha_step(const float* alpha_grad, double lr, int64_t step, double* alpha_state, float* alpha_f32,
+                             float* losses) {
+  if (threadIdx.x != 0) return;
   const double la = alpha_state[0];
-  const double c = -(slp / B) - target_entropy;  // mean(-logpi - H)
-  const double g = exp(la) * c;                   // d/dlog_alpha of exp(log_alpha)*c
+  const double c = (double)*alpha_grad;
+  const double g = exp(la) * c;
   double m = alpha_state[1], v = alpha_state[2];
   m = m + (1.0 - 0.9) * (g - m);
   v = v * 0.999 + (1.0 - 0.999) * g * g;
@@ -123,10 +134,7 @@ __global__ void k_finalize_actor_alpha(const float* part, int ntiles, int B, int
   alpha_state[3] = exp(nla);
   *alpha_f32 = (float)exp(nla);
   if (losses) {
-    losses[2] = (float)actor;
-    losses[3] = custom_loss != 0.f ? (float)sac : 0.f;
-    losses[4] = custom_loss != 0.f ? (float)dist : 0.f;
-    losses[5] = (float)(exp(la) * c);
+    losses[5] = (float)g;
     losses[6] = (float)exp(nla);
   }
 }

@@ -69,6 +69,20 @@ __global__ void k_replay_stage_fm(ReplayDev r, const int64_t* __restrict__ idx, 
   DN[b] = v ? (float)r.done[t] : 0.f;
 }
 
+// rbuffer_sample_acm (:404-430) + AcMTrainer.acm_cat (acm.py:260-264)
+__global__ void k_replay_gather_acm(ReplayDev r, const int64_t* __restrict__ idx, int B, float* x, float* y) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int64_t t = idx[b];
+  const int64_t o = r.obs_idx[t], n = r.next_idx[t];
+  const int ob = r.ob;
+  for (int f = 0; f < ob; ++f) {
+    x[(int64_t)b * 2 * ob + f] = r.obs[o * ob + f];
+    x[(int64_t)b * 2 * ob + ob + f] = r.obs[n * ob + f];
+  }
+  for (int f = 0; f < r.ac; ++f) y[(int64_t)b * r.ac + f] = r.acm[t * r.ac + f];
+}
+
 // ---------------------------------------------------------------- obs statistics
 // update_obs_mean_std (:83-96) over X = obs[obs_idx[0:len)]
 __device__ __forceinline__ uint32_t fkey(float x) {

@@ -82,6 +82,13 @@ _SIGS = {
     "sppAcmRegressStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "sppPolicyAct": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p,
                              c_void_p, c_void_p]),
+    "sppAgentBindAlphaGrad": (c_int, [c_void_p, c_void_p]),
+    "sppSacAcmDrawEps": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "sppAcmRegressGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "sppAcmRegressApply": (c_int, [c_void_p, c_void_p]),
+    "sppReplayGatherAcm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "sppAgentSetTiming": (c_int, [c_void_p, c_int]),
+    "sppAgentGetTiming": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppSynthEnvStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -71,15 +71,26 @@ class SAC_AcM:
         self._h = h
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         self.params, self.grads, self.exp_avg, self.exp_avg_sq = {}, {}, {}, {}
+        sizes = {}
         for net, lay in self.layouts.items():
             n = ctypes.c_int64()
             call("sppAgentNetSize", self._h, net, ctypes.byref(n))
             assert n.value == nets.numel(lay), (net, n.value, nets.numel(lay))
+            sizes[net] = n.value
             self.params[net] = nets.linear_init_(torch.empty(n.value, device=self.device), lay, gen)
-            if net in (_lib.SPP_NET_ACTOR, _lib.SPP_NET_CRITIC1, _lib.SPP_NET_CRITIC2, _lib.SPP_NET_ACM):
-                self.grads[net] = torch.zeros(n.value, device=self.device)
-                self.exp_avg[net] = torch.zeros(n.value, device=self.device)
-                self.exp_avg_sq[net] = torch.zeros(n.value, device=self.device)
+        # gradient buckets = the data-parallel exchange units (one all-reduce each):
+        #   critic: [critic_1 | critic_2], actor: [actor | d alpha operand], acm: [acm]
+        c1, c2, na, nm = (sizes[_lib.SPP_NET_CRITIC1], sizes[_lib.SPP_NET_CRITIC2], sizes[_lib.SPP_NET_ACTOR],
+                          sizes[_lib.SPP_NET_ACM])
+        self.bucket_critic = torch.zeros(c1 + c2, device=self.device)
+        self.bucket_actor = torch.zeros(na + 1, device=self.device)
+        self.bucket_acm = torch.zeros(nm, device=self.device)
+        self.grads = {_lib.SPP_NET_CRITIC1: self.bucket_critic[:c1], _lib.SPP_NET_CRITIC2: self.bucket_critic[c1:],
+                      _lib.SPP_NET_ACTOR: self.bucket_actor[:na], _lib.SPP_NET_ACM: self.bucket_acm}
+        self.alpha_grad = self.bucket_actor[na:]
+        for net in self.grads:
+            self.exp_avg[net] = torch.zeros(sizes[net], device=self.device)
+            self.exp_avg_sq[net] = torch.zeros(sizes[net], device=self.device)
         # sac.py:127,136: targets start as deep copies of the critics
         self.params[_lib.SPP_NET_CRITIC1_TARG].copy_(self.params[_lib.SPP_NET_CRITIC1])
         self.params[_lib.SPP_NET_CRITIC2_TARG].copy_(self.params[_lib.SPP_NET_CRITIC2])
@@ -92,6 +103,7 @@ class SAC_AcM:
         self.alpha_state = torch.tensor([math.log(alpha), 0.0, 0.0, alpha], dtype=torch.float64, device=self.device)
         self.alpha_f32 = torch.tensor([alpha], dtype=torch.float32, device=self.device)
         call("sppAgentBindAlpha", self._h, ptr(self.alpha_state), ptr(self.alpha_f32))
+        call("sppAgentBindAlphaGrad", self._h, ptr(self.alpha_grad))
         self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
                                                 min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
         self.bind_normalizer(self.replay_buffer)
@@ -144,6 +156,40 @@ class SAC_AcM:
         idx = torch.as_tensor(idx, dtype=torch.int64).to(self.device).contiguous()
         call("sppAgentStageFromReplay", self._h, self.replay_buffer._h, ptr(idx), idx.numel(), stream_handle())
         call("sppSacAcmUpdateStaged", self._h, seed, counter, ptr(self._losses), stream_handle())
+
+    def update_from_replay_dp(self, idx, seed, counter, allreduce=None):
+        """The same grad step split at its exchange points: allreduce(bucket) averages a
+        flat gradient bucket across data-parallel ranks (RCCL) between grads and apply."""
+        st = stream_handle()
+        call("sppAgentStageFromReplay", self._h, self.replay_buffer._h, ptr(idx), idx.numel(), st)
+        call("sppSacAcmDrawEps", self._h, seed, counter, st)
+        call("sppSacAcmCriticGrads", self._h, None, None, ptr(self._losses), st)
+        if allreduce is not None:
+            allreduce(self.bucket_critic)
+        call("sppSacAcmCriticApply", self._h, st)
+        call("sppSacAcmActorGrads", self._h, None, ptr(self._losses), st)
+        if allreduce is not None:
+            allreduce(self.bucket_actor)
+        call("sppSacAcmActorApply", self._h, ptr(self._losses), st)
+
+    def acm_update_from_replay(self, idx, x, y, loss, allreduce=None):
+        """update_acm_batches body (acm.py:356-372) for one device-sampled batch."""
+        st = stream_handle()
+        B = idx.numel()
+        call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), B, ptr(x), ptr(y), st)
+        call("sppAcmRegressGrads", self._h, ptr(x), ptr(y), B, ptr(loss), st)
+        if allreduce is not None:
+            allreduce(self.bucket_acm)
+        call("sppAcmRegressApply", self._h, st)
+
+    def set_timing(self, on=True):
+        call("sppAgentSetTiming", self._h, int(on))
+
+    def get_timing(self):
+        ms = np.zeros(5, np.float64)
+        cnt = np.zeros(5, np.int64)
+        call("sppAgentGetTiming", self._h, ms.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p))
+        return ms, cnt
 
     @property
     def loss(self):

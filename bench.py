@@ -136,6 +136,7 @@ def main():
     import spprl
     from spprl import _lib
     from spprl._lib import call, ptr, stream_handle
+    from spprl.dp import make_allreduce, shard_seed
 
     E, rho, sigma = args.envs, args.rho, args.sigma
     B, BA = rho * E, sigma * E
@@ -143,17 +144,11 @@ def main():
                        acm_lr=1e-3, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
                        denormalize_actor_out=True, max_batch=max(B, BA), buffer_size=args.buffer, device=dev, seed=0)
     rb = ag.replay_buffer
-    allreduce = None
-    if world > 1:
-        inv = 1.0 / world
-
-        def allreduce(t):  # noqa: F811  (RCCL over xGMI; average)
-            dist.all_reduce(t)
-            t.mul_(inv)
+    allreduce = make_allreduce()  # RCCL over xGMI; None at N=1
 
     g = torch.Generator(device="cpu").manual_seed(1234)  # SynthEnv dynamics: shared across ranks
     A = (torch.randn(OB, OB, generator=g) * 0.05).to(dev)
-    seed = 1000 + rank
+    seed = shard_seed(1000, rank)
     st = stream_handle()
 
     # ---- pre-fill the replay shard (min(capacity, 1e6) rows of N(0,1) obs)

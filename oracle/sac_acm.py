@@ -49,11 +49,16 @@ class OracleSacAcm:
     def _acm(self, x):
         return nets.acm(self.p["acm"], x, self.acm_lim)
 
-    def update(self, obs, next_obs, action, reward, done, acm_action, eps_next, eps_cur):
-        t = lambda a, dt=torch.float32: torch.as_tensor(np.asarray(a)).to(dt)  # noqa: E731
+    @staticmethod
+    def _t(a, dt=torch.float32):
+        return torch.as_tensor(np.asarray(a)).to(dt)
+
+    def critic_grads(self, obs, next_obs, action, reward, done, acm_action, eps_next):
+        """compute_qfunc_targ (sac_acm.py:30-58) + both critic losses (:97-131).
+        Returns ({critic_k: [grad tensors]}, losses, y)."""
+        t = self._t
         obs, next_obs, action, reward = t(obs), t(next_obs), t(action), t(reward)
-        done, acm_action = t(done, torch.int8), t(acm_action)
-        eps_next, eps_cur = t(eps_next), t(eps_cur)
+        done, acm_action, eps_next = t(done, torch.int8), t(acm_action), t(eps_next)
         P, losses = self.p, {}
         with torch.no_grad():
             a2, lp2, _ = nets.sac_actor(P["actor"], next_obs, self.actor_lim, eps_next)
@@ -70,9 +75,19 @@ class OracleSacAcm:
             q = nets.sac_critic(P[k], obs, action)
             loss = F.mse_loss(q, y)
             losses[k] = loss.item()
-            g = torch.autograd.grad(loss, list(P[k].values()))
-            grads[k] = torch.cat([x.reshape(-1) for x in g]).numpy()
-            self.opt[k].step(g)
+            grads[k] = list(torch.autograd.grad(loss, list(P[k].values())))
+        return grads, losses, y
+
+    def critic_apply(self, grads):
+        for k in ("critic_1", "critic_2"):
+            self.opt[k].step(grads[k])
+
+    def actor_grads(self, obs, next_obs, eps_cur):
+        """compute_pi_loss (sac_acm.py:60-87) against the updated critics and the alpha-loss
+        gradient operand (sac.py:201-216).  Returns ([actor grads], alpha_grad, losses, logp)."""
+        t = self._t
+        obs, next_obs, eps_cur = t(obs), t(next_obs), t(eps_cur)
+        P, losses = self.p, {}
         a, lp, _ = nets.sac_actor(P["actor"], obs, self.actor_lim, eps_cur)
         ad = self.norm.denormalize(a)
         ca = self._acm(torch.cat([obs, ad], axis=1)) if self.acm_critic else ad
@@ -89,20 +104,35 @@ class OracleSacAcm:
             losses["dist"] = dist.item()
             loss = loss + self.custom_loss * dist
         losses["actor"] = loss.item()
-        g = torch.autograd.grad(loss, list(P["actor"].values()))
-        grads["actor"] = torch.cat([x.reshape(-1) for x in g]).numpy()
+        g = list(torch.autograd.grad(loss, list(P["actor"].values())))
+        lpd = lp.detach()
+        alpha_loss = (self.log_alpha.exp() * (-lpd - self.target_entropy)).mean()
+        losses["alpha_loss"] = alpha_loss.item()
+        (ga,) = torch.autograd.grad(alpha_loss, [self.log_alpha])
+        return g, ga, losses, lpd
+
+    def actor_apply(self, g, alpha_grad):
+        """Actor Adam step, polyak (sac.py:186-199, two roundings), alpha Adam step."""
+        P = self.p
         self.opt["actor"].step(g)
         with torch.no_grad():
             for c, tg in (("critic_1", "critic_1_targ"), ("critic_2", "critic_2_targ")):
                 for n in P[c]:
                     P[tg][n].mul_(1 - self.tau)
                     P[tg][n].add_(self.tau * P[c][n])
-        lpd = lp.detach()
-        alpha_loss = (self.log_alpha.exp() * (-lpd - self.target_entropy)).mean()
-        self.opt_alpha.step(torch.autograd.grad(alpha_loss, [self.log_alpha]))
+        self.opt_alpha.step([alpha_grad])
         self.alpha = self.log_alpha.exp().item()
-        losses["alpha_loss"] = alpha_loss.item()
-        self.last = {"y": y, "logp": lpd, "grads": grads}
+
+    def update(self, obs, next_obs, action, reward, done, acm_action, eps_next, eps_cur):
+        """SAC_AcM.update (sac_acm.py:89-162) = critic_grads, critic_apply, actor_grads, actor_apply."""
+        cg, losses, y = self.critic_grads(obs, next_obs, action, reward, done, acm_action, eps_next)
+        self.critic_apply(cg)
+        g, ga, l2, lpd = self.actor_grads(obs, next_obs, eps_cur)
+        losses.update(l2)
+        self.actor_apply(g, ga)
+        flat = lambda gs: torch.cat([x.reshape(-1) for x in gs]).numpy()  # noqa: E731
+        self.last = {"y": y, "logp": lpd, "grads": {"critic_1": flat(cg["critic_1"]), "critic_2": flat(cg["critic_2"]),
+                                                    "actor": flat(g)}}
         return losses
 
     def flat(self, k):

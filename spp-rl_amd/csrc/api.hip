@@ -391,14 +391,12 @@ struct sppAgent {
   DevArray<float> limits;  // [aout] actor lim | [ac] acm lim
   // packed images
   DevArray<float4> pk;     // all matrix images
-  DevArray<float> pv;      // all vector images
   std::vector<PackJob> pj_actor, pj_acm, pj_targ, pj_critic_fwd, pj_critic_all, pj_acmreg;
-  std::vector<VecJob> vj_actor, vj_acm, vj_targ, vj_critic;
   DevArray<PackJob> d_pj;
-  DevArray<VecJob> d_vj;
-  // job-table offsets inside d_pj / d_vj
+  // job-table offsets inside d_pj
   int o_actor = 0, o_acm = 0, o_targ = 0, o_cfwd = 0, o_call = 0, o_acmreg = 0;
-  int vo_actor = 0, vo_acm = 0, vo_targ = 0, vo_critic = 0;
+  // LDS constant-table segments (canonical bias / fc3 vectors, read at kernel start)
+  std::vector<TabSeg> tab;
   ActorDev actor{};
   CriticDev critic[2]{}, targ[2]{};
   AcmDev acm{};
@@ -466,22 +464,22 @@ static sppStatus build_packs(sppAgent* a) {
     PackJob job;
     const float4** slot;
   };
-  struct VecSpec {
-    std::vector<VecJob>* list;
-    VecJob job;
-    const float** slot;
-  };
   std::vector<MatSpec> ms;
-  std::vector<VecSpec> vs;
+  // ib = 1: ib-major image for dense_lds (256-input layers)
   auto M = [&](std::vector<PackJob>* list, const float* W, const float* W2, int split, int ld, int trans, int coff,
-               MapDesc out, MapDesc in, int NBO, int NBI, const float4** slot) {
-    PackJob j{W, W2, split, ld, trans, coff, out, in, NBO, NBI, nullptr};
+               MapDesc out, MapDesc in, int NBO, int NBI, const float4** slot, int ib = 0) {
+    PackJob j{W, W2, split, ld, trans, coff, out, in, NBO, NBI, ib, nullptr};
     ms.push_back({list, j, slot});
   };
-  auto V = [&](std::vector<VecJob>* list, const float* v, const float* v2, int split, MapDesc m, int NB,
-               const float** slot) {
-    VecJob j{v, v2, split, m, NB, nullptr};
-    vs.push_back({list, j, slot});
+  // LDS table: each vector starts on a 32-float boundary, zero padded to a whole block
+  a->tab.clear();
+  int toff = 0;
+  auto T = [&](const float* v, int n, const float* v2 = nullptr, int n2 = 0) {
+    const int off = toff, tot = (int)round_up(n + n2, 32);
+    a->tab.push_back(TabSeg{v, n, v2 ? n : tot, off, 0});
+    if (v2) a->tab.push_back(TabSeg{v2, n2, tot - n, off + n, 0});
+    toff += tot;
+    return off;
   };
   // ---- actor (sac/models.py:12-22): fc1 [256][ob], fc2, fc_prob [aout][256], fc_scale
   {
@@ -489,13 +487,13 @@ static sppStatus build_packs(sppAgent* a) {
     const float *W1 = P, *b1 = W1 + 256 * ob, *W2 = b1 + 256, *b2 = W2 + 65536, *Wp = b2 + 256, *bp = Wp + aout * 256,
                 *Ws = bp + aout, *bs = Ws + aout * 256;
     M(&a->pj_actor, W1, nullptr, 1 << 30, ob, 0, 0, nat(256), nat(ob), 8, blocks_of(ob), &a->actor.W1);
-    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &a->actor.W2);
-    M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh);
-    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T);
+    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &a->actor.W2, 1);
+    M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh, 1);
+    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T, 1);
     M(&a->pj_actor, Wp, Ws, aout, 256, 1, 0, nat(256), pair(aout), 8, (aout + 15) / 16, &a->actor.WhT);
-    V(&a->vj_actor, b1, nullptr, 1 << 30, nat(256), 8, &a->actor.b1P);
-    V(&a->vj_actor, b2, nullptr, 1 << 30, nat(256), 8, &a->actor.b2P);
-    V(&a->vj_actor, bp, bs, aout, nat(2 * aout), blocks_of(2 * aout), &a->actor.bhP);
+    a->actor.tb1 = T(b1, 256);
+    a->actor.tb2 = T(b2, 256);
+    a->actor.tbh = T(bp, aout, bs, aout);
   }
   // ---- ACM (basic_model.py:108-117): fc1 [64][2ob], fc2 [32][64], fc3 [ac][32]
   {
@@ -510,9 +508,9 @@ static sppStatus build_packs(sppAgent* a) {
     M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 1, 0, nat(64), nat(32), 2, 1, &a->acm.W2T);
     M(&a->pj_acm, W1, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(64), blocks_of(aout), 2, &a->acm.W1Ta);
     M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), nat(in), 2, blocks_of(in), &a->acm_W1n);
-    V(&a->vj_acm, b1, nullptr, 1 << 30, nat(64), 2, &a->acm.b1P);
-    V(&a->vj_acm, b2, nullptr, 1 << 30, nat(32), 1, &a->acm.b2P);
-    V(&a->vj_acm, b3, nullptr, 1 << 30, nat(ac), 1, &a->acm.b3P);
+    a->acm.tb1 = T(b1, 64);
+    a->acm.tb2 = T(b2, 32);
+    a->acm.tb3 = T(b3, ac);
   }
   // ---- critics and targets (sac/models.py:75-91): fc1 [256][cin], fc2, fc3 [1][256]
   for (int t = 0; t < 4; ++t) {
@@ -521,38 +519,30 @@ static sppStatus build_packs(sppAgent* a) {
     const float* P = a->net[netid].p;
     const float *W1 = P, *b1 = W1 + 256 * cin, *W2 = b1 + 256, *b2 = W2 + 65536, *w3 = b2 + 256, *b3 = w3 + 256;
     std::vector<PackJob>* fl = t < 2 ? &a->pj_critic_fwd : &a->pj_targ;
-    std::vector<VecJob>* vl = t < 2 ? &a->vj_critic : &a->vj_targ;
     M(fl, W1, nullptr, 1 << 30, cin, 0, 0, nat(256), cat(ob, ca), 8, blocks_of(ob) + blocks_of(ca), &cd.W1);
-    M(fl, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &cd.W2);
+    M(fl, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &cd.W2, 1);
     if (t < 2) {
-      M(fl, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &cd.W2T);
-      M(fl, W1, nullptr, 1 << 30, cin, 1, ob, nat(ca), nat(256), blocks_of(ca), 8, &cd.W1Ta);
+      M(fl, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &cd.W2T, 1);
+      M(fl, W1, nullptr, 1 << 30, cin, 1, ob, nat(ca), nat(256), blocks_of(ca), 8, &cd.W1Ta, 1);
     }
-    V(vl, b1, nullptr, 1 << 30, nat(256), 8, &cd.b1P);
-    V(vl, b2, nullptr, 1 << 30, nat(256), 8, &cd.b2P);
-    V(vl, w3, nullptr, 1 << 30, nat(256), 8, &cd.w3P);
+    cd.tb1 = T(b1, 256);
+    cd.tb2 = T(b2, 256);
+    cd.tw3 = T(w3, 256);
     cd.b3 = b3;
   }
+  SPP_REQUIRE(toff <= kTabMax && (int)a->tab.size() <= kTabSegs, SPP_E_SHAPE,
+              "LDS table too large (%d floats, %d segments)", toff, (int)a->tab.size());
   // allocate images
-  size_t nf4 = 0, nvf = 0;
+  size_t nf4 = 0;
   for (auto& m : ms) nf4 += (size_t)m.job.NBO * m.job.NBI * 4 * 64;
-  for (auto& v : vs) nvf += (size_t)v.job.NB * 32;
   a->pk.release();
-  a->pv.release();
   SPP_CHECK_HIP(a->pk.alloc(nf4));
-  SPP_CHECK_HIP(a->pv.alloc(nvf));
-  size_t of = 0, ov = 0;
+  size_t of = 0;
   for (auto& m : ms) {
     m.job.dst = a->pk.ptr + of;
     *m.slot = m.job.dst;
     of += (size_t)m.job.NBO * m.job.NBI * 4 * 64;
     m.list->push_back(m.job);
-  }
-  for (auto& v : vs) {
-    v.job.dst = a->pv.ptr + ov;
-    *v.slot = v.job.dst;
-    ov += (size_t)v.job.NB * 32;
-    v.list->push_back(v.job);
   }
   // critics: "all" list = fwd list (already includes transposes)
   a->pj_critic_all = a->pj_critic_fwd;
@@ -562,23 +552,14 @@ static sppStatus build_packs(sppAgent* a) {
   a->o_acm = (int)all.size(); all.insert(all.end(), a->pj_acm.begin(), a->pj_acm.end());
   a->o_targ = (int)all.size(); all.insert(all.end(), a->pj_targ.begin(), a->pj_targ.end());
   a->o_cfwd = (int)all.size(); all.insert(all.end(), a->pj_critic_fwd.begin(), a->pj_critic_fwd.end());
-  std::vector<VecJob> vall;
-  a->vo_actor = (int)vall.size(); vall.insert(vall.end(), a->vj_actor.begin(), a->vj_actor.end());
-  a->vo_acm = (int)vall.size(); vall.insert(vall.end(), a->vj_acm.begin(), a->vj_acm.end());
-  a->vo_targ = (int)vall.size(); vall.insert(vall.end(), a->vj_targ.begin(), a->vj_targ.end());
-  a->vo_critic = (int)vall.size(); vall.insert(vall.end(), a->vj_critic.begin(), a->vj_critic.end());
   a->d_pj.release();
-  a->d_vj.release();
   SPP_CHECK_HIP(a->d_pj.alloc(all.size()));
-  SPP_CHECK_HIP(a->d_vj.alloc(vall.size()));
   SPP_CHECK_HIP(hipMemcpy(a->d_pj.ptr, all.data(), sizeof(PackJob) * all.size(), hipMemcpyHostToDevice));
-  SPP_CHECK_HIP(hipMemcpy(a->d_vj.ptr, vall.data(), sizeof(VecJob) * vall.size(), hipMemcpyHostToDevice));
   return SPP_OK;
 }
 
-static void launch_pack(sppAgent* a, int off, int n, int voff, int vn, hipStream_t st) {
+static void launch_pack(sppAgent* a, int off, int n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(k_pack_matrix, dim3(64, n), dim3(256), 0, st, (const PackJob*)(a->d_pj.ptr + off));
-  if (vn > 0) hipLaunchKernelGGL(k_pack_vector, dim3(1, vn), dim3(256), 0, st, (const VecJob*)(a->d_vj.ptr + voff));
 }
 
 // (Re)build a weight-gradient job set for batch size B.
@@ -734,6 +715,8 @@ static SacArgs make_args(sppAgent* a, int B) {
   p.acm = a->acm;
   p.AH1 = a->AH1; p.AH2 = a->AH2; p.AD1 = a->AD1; p.AD2 = a->AD2; p.ADH = a->ADH;
   p.part = a->part;
+  p.nseg = (int)a->tab.size();
+  for (int i = 0; i < p.nseg; ++i) p.seg[i] = a->tab[i];
   return p;
 }
 
@@ -781,7 +764,7 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   a->nsize[SPP_NET_ACM] = acm_size(2 * ob, ac);
   a->Bmax = cfg->max_batch;
   const int64_t Bp = round_up(cfg->max_batch, 32);
-  SPP_REQUIRE(Bp * 256 < ((int64_t)1 << 31), SPP_E_SHAPE, "max_batch %d too large (32-bit scratch offsets)",
+  SPP_REQUIRE((int64_t)Bp * 256 * 4 < ((int64_t)1 << 31), SPP_E_SHAPE, "max_batch %d too large (31-bit buffer offsets)",
               cfg->max_batch);
   a->Bpmax = (int)Bp;
   const int64_t ntiles = Bp / 32;
@@ -829,7 +812,7 @@ sppStatus sppAgentDestroy(sppAgentHandle a) {
   if (!a) return SPP_OK;
   hipSetDevice(a->device);
   hipDeviceSynchronize();
-  a->limits.release(); a->pk.release(); a->pv.release(); a->d_pj.release(); a->d_vj.release();
+  a->limits.release(); a->pk.release(); a->d_pj.release();
   for (auto& v : a->tev)
     for (auto e : v) hipEventDestroy(e);
   a->scratch.release(); a->d_adam.release();
@@ -853,7 +836,7 @@ sppStatus sppAgentBindNet(sppAgentHandle a, int net, float* p, float* g, float* 
   if (changed) {  // pack tables and gradient jobs hold these pointers
     a->pk.release();
     a->pj_actor.clear(); a->pj_acm.clear(); a->pj_targ.clear(); a->pj_critic_fwd.clear(); a->pj_critic_all.clear();
-    a->vj_actor.clear(); a->vj_acm.clear(); a->vj_targ.clear(); a->vj_critic.clear();
+    a->tab.clear();
   }
   return SPP_OK;
 }
@@ -918,7 +901,7 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
   }
   // pack actor, ACM, targets, critics (current weights)
   launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size() + a->pj_targ.size() + a->pj_critic_fwd.size()),
-              a->vo_actor, (int)(a->vj_actor.size() + a->vj_acm.size() + a->vj_targ.size() + a->vj_critic.size()), st);
+              st);
   SacArgs p = make_args(a, B);
   const int grid = phase_grid(a, p.Bp);
   tmark(a, 0, st);
@@ -962,7 +945,7 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   const int B = a->cur_B;
   SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
   // repack the updated critics
-  launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), a->vo_critic, (int)a->vj_critic.size(), st);
+  launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), st);
   SacArgs p = make_args(a, B);
   AcmScratch z{a->Z1, a->Z2, a->T3};
   const int grid = phase_grid(a, p.Bp);
@@ -1092,7 +1075,7 @@ sppStatus sppAcmRegressGrads(sppAgentHandle a, const float* x, const float* y, i
   if (a->dws[1].B != B) {
     if ((s = build_dw(a, 1, B))) return s;
   }
-  launch_pack(a, a->o_acm, (int)a->pj_acm.size(), a->vo_acm, (int)a->vj_acm.size(), st);
+  launch_pack(a, a->o_acm, (int)a->pj_acm.size(), st);
   SacArgs p = make_args(a, B);
   p.acm.W1 = a->acm_W1n;
   AcmRegArgs g{};
@@ -1137,8 +1120,7 @@ sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* e
   hipStream_t st = S(stream);
   sppStatus s = check_ready(a);
   if (s) return s;
-  launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size()), a->vo_actor,
-              (int)(a->vj_actor.size() + a->vj_acm.size()), st);
+  launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size()), st);
   SacArgs p = make_args(a, 32);
   ActArgs g{E, mode, denorm_out, act_noise, obs, eps, noise, target_out, env_out};
   const int grid = std::max(1, std::min(cdiv(cdiv(E, 32), kWavesPerWG), a->num_cu));
@@ -1150,32 +1132,34 @@ sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* e
 sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,
                         void* stream) {
   SPP_REQUIRE(x && W && y && B > 0 && K > 0 && K <= 256 && N > 0 && N <= 256, SPP_E_INVALID_ARG, "debug dense: bad");
+  SPP_REQUIRE(K <= 224 || K == 256, SPP_E_INVALID_ARG, "debug dense: K in (224, 256) not supported");
   hipStream_t st = S(stream);
   const int NBI = blocks_of(K), NBO = blocks_of(N);
+  const int ibm = NBI == 8 ? 1 : 0;
   float4* wf;
-  float* bp;
   PackJob* dj;
-  VecJob* dv;
   SPP_CHECK_HIP(hipMalloc(&wf, sizeof(float4) * NBO * NBI * 256));
-  SPP_CHECK_HIP(hipMalloc(&bp, sizeof(float) * NBO * 32));
   SPP_CHECK_HIP(hipMalloc(&dj, sizeof(PackJob)));
-  SPP_CHECK_HIP(hipMalloc(&dv, sizeof(VecJob)));
-  PackJob pj{W, nullptr, 1 << 30, K, 0, 0, nat(N), nat(K), NBO, NBI, wf};
-  VecJob vj{b, nullptr, 1 << 30, nat(N), NBO, bp};
+  PackJob pj{W, nullptr, 1 << 30, K, 0, 0, nat(N), nat(K), NBO, NBI, ibm, wf};
   SPP_CHECK_HIP(hipMemcpy(dj, &pj, sizeof(pj), hipMemcpyHostToDevice));
-  SPP_CHECK_HIP(hipMemcpy(dv, &vj, sizeof(vj), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_pack_matrix, dim3(16, 1), dim3(256), 0, st, (const PackJob*)dj);
-  if (b) hipLaunchKernelGGL(k_pack_vector, dim3(1, 1), dim3(256), 0, st, (const VecJob*)dv);
   const dim3 grid(cdiv(B, 32));
-  const float* bpp = b ? bp : nullptr;
-  switch (NBI) {
-#define SPP_DD(n) case n: hipLaunchKernelGGL(k_debug_dense<n>, grid, dim3(64), 0, st, (const float4*)wf, bpp, x, y, B, K, N, act); break;
-    SPP_DD(1) SPP_DD(2) SPP_DD(3) SPP_DD(4) SPP_DD(5) SPP_DD(6) SPP_DD(7) SPP_DD(8)
+  if (NBI < 8) {
+    switch (NBI) {
+#define SPP_DD(n) case n: hipLaunchKernelGGL((k_debug_dense<n, 1>), grid, dim3(64), 0, st, (const float4*)wf, b, x, y, B, K, N, act); break;
+      SPP_DD(1) SPP_DD(2) SPP_DD(3) SPP_DD(4) SPP_DD(5) SPP_DD(6) SPP_DD(7)
 #undef SPP_DD
+    }
+  } else {
+    switch (NBO) {
+#define SPP_DD(n) case n: hipLaunchKernelGGL((k_debug_dense<8, n>), grid, dim3(64), 0, st, (const float4*)wf, b, x, y, B, K, N, act); break;
+      SPP_DD(1) SPP_DD(2) SPP_DD(3) SPP_DD(4) SPP_DD(5) SPP_DD(6) SPP_DD(7) SPP_DD(8)
+#undef SPP_DD
+    }
   }
   SPP_CHECK_HIP(hipGetLastError());
   SPP_CHECK_HIP(hipStreamSynchronize(st));
-  hipFree(wf); hipFree(bp); hipFree(dj); hipFree(dv);
+  hipFree(wf); hipFree(dj);
   return SPP_OK;
 }
 

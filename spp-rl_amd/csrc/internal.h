@@ -20,22 +20,15 @@ struct DwJob {
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)
 //   L[n][k] = trans ? S[k][coff + n] : S[n][coff + k]; source rows >= split come from W2
+// image order: ob-major ((ob*NBI + ib)*4 + rq)*64 + lane (dense), or
+//              ib-major ((ib*NBO + ob)*4 + rq)*64 + lane (dense_lds)
 struct PackJob {
   const float* W;
   const float* W2;
   int split, ld, trans, coff;
   MapDesc out, in;
-  int NBO, NBI;
+  int NBO, NBI, ibmajor;
   float4* dst;
-};
-// vector image: dst[(ob*16 + q)*2 + h] = v[map(ob, q, h)] (idx >= split -> v2[idx - split])
-struct VecJob {
-  const float* v;
-  const float* v2;
-  int split;
-  MapDesc map;
-  int NB;
-  float* dst;
 };
 
 struct AdamJob {

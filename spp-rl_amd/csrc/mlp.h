@@ -106,7 +106,10 @@ constexpr int chunk_of(int nq) { return nq <= 8 ? nq : (nq % 8 == 0 ? 8 : (nq % 
 
 // ---------------------------------------------------------------- dense layer
 template <int N>
-struct IC { static constexpr int value = N; };
+struct IC {
+  static constexpr int value = N;
+  __host__ __device__ constexpr operator int() const { return N; }
+};
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (B < E) {
@@ -132,13 +135,34 @@ constexpr int q_rq(uint64_t RV, int NBI, int q) {
   return 0;
 }
 
-// out blocks ob = 0..NBO-1 (runtime), acc initialised from the packed bias
-// image biasP[(ob*16 + q)*2 + h] (NULL -> 0), epi(ob, acc) consumes each block.
+// Unit of register r for lane half 0; unit_of(r, h) = ru(r) + 4h.
+__device__ __forceinline__ constexpr int ru(int r) { return (r & 3) + 8 * (r >> 2); }
+
+// Bias of output block ob from a natural-order LDS table biasL[32*NBO]:
+// register q of lane half h is unit 32*ob + ru(q) + 4h (4 consecutive units per
+// register quad -> one broadcast ds_read_b128 each).
+__device__ __forceinline__ f32x16 bias_tile(const float* biasL, int ob, int h) {
+  f32x16 acc;
+  const float4* b4 = reinterpret_cast<const float4*>(biasL + 32 * ob + 4 * h);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float4 v = b4[2 * k];  // units 8k + 4h .. 8k + 4h + 3
+    acc[4 * k + 0] = v.x;
+    acc[4 * k + 1] = v.y;
+    acc[4 * k + 2] = v.z;
+    acc[4 * k + 3] = v.w;
+  }
+  return acc;
+}
+
+// Register-input layer (small K): out blocks ob = 0..NBO-1 (runtime), acc
+// initialised from the LDS bias table (NULL -> 0), epi(ob, acc) consumes each
+// block.  Weight image ob-major: Wf[((ob*NBI + ib)*4 + rq)*64 + lane].
 // Weight fragments stream through a 2-deep register ring of CH float4 so the
 // next chunk's loads are in flight while the current chunk's MFMAs issue.
 template <int NBI, uint64_t RV, typename Epi>
 __device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
-                                      const float* __restrict__ biasP, Epi&& epi) {
+                                      const float* biasL, Epi&& epi) {
   constexpr int NQ = rv_total(RV, NBI);
   static_assert(NQ > 0, "empty layer");
   constexpr int CH = chunk_of(NQ);
@@ -155,13 +179,7 @@ __device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, co
   });
 #pragma unroll 1
   for (int ob = 0; ob < NBO; ++ob) {
-    f32x16 acc;
-    if (biasP) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = biasP[(ob * 16 + q) * 2 + h];
-    } else {
-      acc = zero16();
-    }
+    f32x16 acc = biasL ? bias_tile(biasL, ob, h) : zero16();
     const int obn = ob + 1 < NBO ? ob + 1 : ob;
     static_for<0, NC>([&](auto C) {
       constexpr int c = decltype(C)::value;
@@ -189,9 +207,79 @@ __device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, co
   }
 }
 
+constexpr int cgcd(int a, int b) { return b ? cgcd(b, a % b) : a; }
+
+// 256-input layer reading its input straight from the wave's LDS image
+// img[unit][32] (all 8 blocks), all NBO output blocks accumulated at once
+// (acc[NBO] lives in the accumulation registers), input blocks streamed in the
+// outer loop.  Weight image ib-major: Wf[((ib*NBO + ob)*4 + rq)*64 + lane], so
+// the whole layer is ONE linear stream of 1 KiB fragments, consumed in chunks
+// of CH float4 through a D-deep register ring: chunk g+D-1's loads are issued
+// (pinned by a scheduling barrier) before chunk g's MFMAs, i.e. (D-1)*CH*4
+// MFMAs of latency cover per load.  epi(ob, acc) runs once per block after the
+// last input block, so it may overwrite img.
+template <int NBO, typename Epi>
+__device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, const float* biasL,
+                                          Epi&& epi) {
+  constexpr int NQ = NBO * 4;               // float4 per input block
+  constexpr int CH = 4;                     // float4 per chunk
+  constexpr int NCI = NQ / CH;              // chunks per input block (= NBO)
+  constexpr int D = 4;                      // ring depth (chunks)
+  constexpr int U = NCI * D / cgcd(NCI, D);  // chunks per loop iteration
+  constexpr int IBU = U / NCI;              // input blocks per iteration
+  constexpr int G = 8 * NCI;                // chunks in the layer
+  static_assert(8 % IBU == 0, "input blocks per iteration");
+  constexpr int NIT = 8 / IBU;
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const float* l = img + 4 * h * 32 + (lane & 31);
+  const float4* wl = Wf + lane;
+  f32x16 acc[NBO];
+  static_for<0, NBO>([&](auto O) { acc[O] = biasL ? bias_tile(biasL, O, h) : zero16(); });
+  float4 ring[D][CH];
+  static_for<0, D - 1>([&](auto I) {
+    static_for<0, CH>([&](auto J) { ring[I][J] = wl[((int)I * CH + (int)J) * 64]; });
+  });
+  f32x16 xin[IBU];
+  static_for<0, IBU>([&](auto K) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xin[K][r] = l[(32 * (int)K + ru(r)) * 32];
+  });
+#pragma unroll 1
+  for (int it = 0; it < NIT; ++it) {
+    const int itn = it + 1 < NIT ? it + 1 : it;
+    f32x16 xnx[IBU];
+    static_for<0, IBU>([&](auto K) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xnx[K][r] = l[(32 * (itn * IBU + (int)K) + ru(r)) * 32];
+    });
+    static_for<0, U>([&](auto UC) {
+      constexpr int u = UC;
+      constexpr int sn = (u + D - 1) % D;
+      const int gn = it * U + u + D - 1;
+      if (gn < G) {
+        const float4* wn = wl + (size_t)gn * (CH * 64);
+        static_for<0, CH>([&](auto J) { ring[sn][J] = wn[(int)J * 64]; });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int s = u % D;
+      static_for<0, CH>([&](auto J) {
+        constexpr int f = u * CH + J;
+        constexpr int kb = f / NQ;
+        constexpr int ob = (f % NQ) / 4;
+        constexpr int rq = f % 4;
+        acc[ob] = mfma(ring[s][J].x, xin[kb][4 * rq + 0], acc[ob]);
+        acc[ob] = mfma(ring[s][J].y, xin[kb][4 * rq + 1], acc[ob]);
+        acc[ob] = mfma(ring[s][J].z, xin[kb][4 * rq + 2], acc[ob]);
+        acc[ob] = mfma(ring[s][J].w, xin[kb][4 * rq + 3], acc[ob]);
+      });
+    });
+    static_for<0, IBU>([&](auto K) { xin[K] = xnx[K]; });
+  }
+  static_for<0, NBO>([&](auto O) { epi(O, acc[O]); });
+}
+
 // ---------------------------------------------------------------- loaders / stores
-// Unit of register r for lane half 0; unit_of(r, h) = ru(r) + 4h.
-__device__ __forceinline__ constexpr int ru(int r) { return (r & 3) + 8 * (r >> 2); }
 
 // Feature-major arrays X[f][ld] are addressed as X[urow*ld + loff] with the
 // wave-uniform row urow = 32*ib + ru(r) and ONE 32-bit per-lane offset
@@ -208,16 +296,53 @@ __device__ __forceinline__ void lds_load(f32x16 (&t)[NB], const float* lds) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[ib][r] = l[(32 * ib + ru(r)) * 32];
 }
-// Feature-major global array X[f][ld] at this lane's column, units < F.
+// 2-D fp32 arrays in HBM through buffer resources: element (row, column) at
+// byte offset row*ld4 + the lane's column offset vo.  row*ld4 is wave-uniform
+// and pinned in an SGPR at each access (no CSE'd / hoisted per-row offsets).
+// Unbounded accesses put it in soffset (no VALU); bounded ones (rsrc_n with the
+// array's byte size) put it in voffset so the hardware range check returns 0 /
+// drops the access for rows past the array (raw-buffer checks exclude soffset).
+// Byte offsets stay below 2^31 (asserted on the host).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t rsrc_n(const void* p, int nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nbytes, 0x00020000);
+}
+__device__ __forceinline__ rsrc_t rsrc(const void* p) { return rsrc_n(p, 0x7fffffff); }
+__device__ __forceinline__ int soff(int row, int ld4) {
+  int so = row * ld4;
+  asm volatile("" : "+s"(so));
+  return so;
+}
+__device__ __forceinline__ float fm_ld(rsrc_t r, int row, int ld4, uint32_t vo) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, soff(row, ld4), 0));
+}
+__device__ __forceinline__ void fm_st(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, soff(row, ld4), 0);
+}
+__device__ __forceinline__ float fm_ldb(rsrc_t r, int row, int ld4, uint32_t vo) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + (uint32_t)soff(row, ld4), 0, 0));
+}
+__device__ __forceinline__ void fm_stb(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo + (uint32_t)soff(row, ld4), 0, 0);
+}
+// Global array X (nbytes long) with F logical rows at this lane's column;
+// units >= F read 0 (feature-major X[f][ld]: nbytes = F*ld4; row-major [E][F]
+// with ld4 = 4: nbytes = E*F*4, the select masks the neighbouring env's values).
 template <int NB>
-__device__ __forceinline__ void gm_load(f32x16 (&t)[NB], const float* __restrict__ X, int F, int ld, int loff) {
+__device__ __forceinline__ void gm_load(f32x16 (&t)[NB], const float* X, int nbytes, int F, int ld4, uint32_t vo) {
+  const rsrc_t xr = rsrc_n(X, nbytes);
   const int h4 = 4 * (lane_id() >> 5);
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int u0 = 32 * ib + ru(r);
-      t[ib][r] = (u0 + h4 < F) ? X[u0 * ld + loff] : 0.f;
+      if (u0 < F) {
+        const float v = fm_ldb(xr, u0, ld4, vo);
+        t[ib][r] = (u0 + h4 < F) ? v : 0.f;
+      } else {
+        t[ib][r] = 0.f;
+      }
     }
 }
 
@@ -227,11 +352,6 @@ template <class T>
 __device__ __forceinline__ T* opaque(T* p) {
   asm volatile("" : "+s"(p));
   return p;
-}
-
-// Packed-vector image vP[(ob*16 + q)*2 + h] (bias / last-layer weight vectors).
-__device__ __forceinline__ float vec_at(const float* __restrict__ vP, int ob, int q) {
-  return vP[(ob * 16 + q) * 2 + (lane_id() >> 5)];
 }
 
 }  // namespace spp

@@ -15,8 +15,8 @@ __global__ void k_pack_matrix(const PackJob* __restrict__ jobs) {
     int64_t rest = i >> 6;
     const int rq = (int)(rest & 3);
     rest >>= 2;
-    const int ib = (int)(rest % J.NBI);
-    const int ob = (int)(rest / J.NBI);
+    const int ib = J.ibmajor ? (int)(rest / J.NBO) : (int)(rest % J.NBI);
+    const int ob = J.ibmajor ? (int)(rest % J.NBO) : (int)(rest / J.NBI);
     int q, hh;
     row_to_pos(lane & 31, q, hh);
     const int n = map_index(J.out, ob, q, hh);
@@ -34,18 +34,6 @@ __global__ void k_pack_matrix(const PackJob* __restrict__ jobs) {
       v[j] = x;
     }
     J.dst[i] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-
-__global__ void k_pack_vector(const VecJob* __restrict__ jobs) {
-  const VecJob J = jobs[blockIdx.y];
-  const int total = J.NB * 32;
-  for (int i = threadIdx.x; i < total; i += blockDim.x) {
-    const int hh = i & 1, q = (i >> 1) & 15, ob = i >> 5;
-    const int idx = map_index(J.map, ob, q, hh);
-    float x = 0.f;
-    if (idx >= 0) x = idx < J.split ? J.v[idx] : J.v2[idx - J.split];
-    J.dst[i] = x;
   }
 }
 

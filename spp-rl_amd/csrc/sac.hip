@@ -1,5 +1,7 @@
 // SAC_AcM per-sample kernels (gfx950).  One wave = 32 samples; one workgroup
-// = 4 waves (one per SIMD) with a private 40 KiB LDS image each.
+// = 4 waves (one per SIMD), each with a private 32 KiB LDS image [256][32]
+// (rows 192..255 double as the SMALL image of the 64-wide ACM layers), plus a
+// 16 KiB per-workgroup table of bias / fc3 vectors shared by the 4 waves.
 //
 //  k_sac_critic_phase   rltoolkit/acm/off_policy/sac_acm.py:30-58 (targets) and
 //                       :114-131 (both critics' forward + backward) -> per-sample
@@ -41,11 +43,24 @@ struct Cfg {
 };
 
 constexpr int kWavesPerWG = 4;
-constexpr int kLdsPerWave = 256 * 32 + 64 * 32;  // BIG [256][32] + SMALL [64][32] floats
+constexpr int kLdsPerWave = 256 * 32;  // BIG [256][32] floats
+constexpr int kSmallRow = 192;         // SMALL [64][32] = BIG rows 192..255
+
+// Fill the per-workgroup LDS constant table (all threads), then barrier.
+__device__ __forceinline__ void load_table(const SacArgs& p, float* tbl) {
+  for (int s = 0; s < p.nseg; ++s) {
+    const TabSeg g = p.seg[s];
+    for (int i = threadIdx.x; i < g.npad; i += blockDim.x) tbl[g.off + i] = i < g.n ? g.src[i] : 0.f;
+  }
+  __syncthreads();
+}
+// Natural-order table vector at (block ob, register q) of this lane half.
+__device__ __forceinline__ float tval(const float* t, int ob, int q, int h4) { return t[32 * ob + ru(q) + h4]; }
 
 __device__ __forceinline__ void setbits(uint64_t& lo, uint64_t& hi, int ob, uint32_t bits) {
   if (ob < 4) lo |= (uint64_t)bits << (16 * ob);
   else hi |= (uint64_t)bits << (16 * (ob - 4));
+  asm volatile("" : "+v"(lo), "+v"(hi));  // materialise now: no sinking of 16 live floats per block
 }
 __device__ __forceinline__ bool getbit(uint64_t lo, uint64_t hi, int ob, int q) {
   const uint64_t w = ob < 4 ? (lo >> (16 * ob)) : (hi >> (16 * (ob - 4)));
@@ -95,17 +110,14 @@ __device__ __forceinline__ void load_pair(f32x16 (&t)[C::NB_PAIR], const float* 
 // Concatenated input tile: blocks [0, NB0) natural from global X (F0 units),
 // blocks [NB0, NB0+NB1) natural from the LDS image rows [0, F1).
 template <int NB0, int NB1>
-__device__ __forceinline__ void load_cat_gl(f32x16 (&t)[NB0 + NB1], const float* __restrict__ X, int F0, int ld,
-                                            int loff, const float* lds, int F1) {
+__device__ __forceinline__ void load_cat_gl(f32x16 (&t)[NB0 + NB1], const float* X, int nbytes, int F0, int ld4,
+                                            uint32_t vo, const float* lds, int F1) {
   const int lane = lane_id(), h4 = 4 * (lane >> 5);
   const float* l = lds + h4 * 32 + (lane & 31);
+  f32x16 g[NB0];
+  gm_load<NB0>(g, X, nbytes, F0, ld4, vo);
 #pragma unroll
-  for (int ib = 0; ib < NB0; ++ib)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int u0 = 32 * ib + ru(r);
-      t[ib][r] = (u0 + h4 < F0) ? X[u0 * ld + loff] : 0.f;
-    }
+  for (int ib = 0; ib < NB0; ++ib) t[ib] = g[ib];
 #pragma unroll
   for (int ib = 0; ib < NB1; ++ib)
 #pragma unroll
@@ -116,43 +128,44 @@ __device__ __forceinline__ void load_cat_gl(f32x16 (&t)[NB0 + NB1], const float*
 }
 // Concatenated input tile from two global feature-major arrays.
 template <int NB0, int NB1>
-__device__ __forceinline__ void load_cat_gg(f32x16 (&t)[NB0 + NB1], const float* __restrict__ X0, int F0,
-                                            const float* __restrict__ X1, int F1, int ld, int loff) {
-  const int h4 = 4 * (lane_id() >> 5);
+__device__ __forceinline__ void load_cat_gg(f32x16 (&t)[NB0 + NB1], const float* X0, int F0, const float* X1, int F1,
+                                            int ld4, uint32_t vo) {
+  f32x16 g0[NB0], g1[NB1];
+  gm_load<NB0>(g0, X0, F0 * ld4, F0, ld4, vo);
+  gm_load<NB1>(g1, X1, F1 * ld4, F1, ld4, vo);
 #pragma unroll
-  for (int ib = 0; ib < NB0; ++ib)
+  for (int ib = 0; ib < NB0; ++ib) t[ib] = g0[ib];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int u0 = 32 * ib + ru(r);
-      t[ib][r] = (u0 + h4 < F0) ? X0[u0 * ld + loff] : 0.f;
-    }
-#pragma unroll
-  for (int ib = 0; ib < NB1; ++ib)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int u0 = 32 * ib + ru(r);
-      t[NB0 + ib][r] = (u0 + h4 < F1) ? X1[u0 * ld + loff] : 0.f;
-    }
+  for (int ib = 0; ib < NB1; ++ib) t[NB0 + ib] = g1[ib];
 }
 
 // Per-tile lane context: LDS images, sample column offsets.
+// Global 2-D arrays X[row][ld] are addressed through buffer resources:
+// byte offset row*ld4 (wave-uniform soffset) + vo (this lane's column, voffset).
 struct Lane {
   int h, s, h4;
-  int ld, b, loff, poff;  // loff = 4h*ld + b (natural layout), poff = 8h*ld + b (pairing layout)
+  float* img;             // BIG image base of this wave
+  const float* tbl;       // per-workgroup LDS table
+  int b, ld4;             // sample index, row stride in bytes
+  uint32_t vo, vp;        // 4*(4h*ld + b) (natural layout), 4*(8h*ld + b) (pairing layout)
   float *bl, *sl;         // BIG / SMALL image at this lane: image[urow*32] = unit (urow + 4h), sample s
   float* pl;              // BIG at the pairing offset: pl[j0*32] = row j0 + 8h
 };
-__device__ __forceinline__ Lane make_lane(float* big, float* small, int ld, int b) {
+__device__ __forceinline__ Lane make_lane(float* big, float* small, const float* tbl, int ld, int b) {
   Lane L;
+  L.img = big;
+  L.tbl = tbl;
   int lane = lane_id();
   asm volatile("" : "+v"(lane));  // keep lane-derived values inside the tile loop (no LICM + spill)
+  int ld4 = 4 * ld;
+  asm volatile("" : "+s"(ld4));   // likewise the row strides (no hoisted per-row offsets)
   L.h = lane >> 5;
   L.s = lane & 31;
   L.h4 = 4 * L.h;
-  L.ld = ld;
+  L.ld4 = ld4;
   L.b = b;
-  L.loff = L.h4 * ld + b;
-  L.poff = 8 * L.h * ld + b;
+  L.vo = (uint32_t)(L.h4 * ld4 + 4 * b);
+  L.vp = (uint32_t)(8 * L.h * ld4 + 4 * b);
   L.bl = big + L.h4 * 32 + L.s;
   L.sl = small + L.h4 * 32 + L.s;
   L.pl = big + 8 * L.h * 32 + L.s;
@@ -160,47 +173,45 @@ __device__ __forceinline__ Lane make_lane(float* big, float* small, int ld, int 
 }
 
 // Actor trunk: x -> relu(L1) -> relu(L2) -> heads (mu | logsig) into LDS rows [0, 2*AOUT).
-// Optionally stores h1 / h2 feature-major and returns ReLU masks.
-template <class C>
-__device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* __restrict__ X, int xld, int xoff,
-                                            const Lane& L, float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
-                                            uint64_t& m2lo, uint64_t& m2hi) {
+// ST: store h1 / h2 feature-major (H1g, H2g).  Returns the ReLU masks.
+template <class C, bool ST>
+__device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, int xbytes, const Lane& L, float* H1g,
+                                            float* H2g,
+                                            uint64_t& m1lo, uint64_t& m1hi, uint64_t& m2lo, uint64_t& m2hi) {
   {
     f32x16 x[C::NB_OB];
-    gm_load<C::NB_OB>(x, X, C::OB, xld, xoff);
-    dense<C::NB_OB, C::RV_X>(A.W1, 8, x, A.b1P, [&](int ob, const f32x16& acc) {
+    gm_load<C::NB_OB>(x, X, xbytes, C::OB, L.ld4, L.vo);
+    const rsrc_t hr = rsrc(H1g);
+    dense<C::NB_OB, C::RV_X>(A.W1, 8, x, L.tbl + A.tb1, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
         const float v = fmaxf(acc[q], 0.f);
         L.bl[ur * 32] = v;
-        if (H1g) H1g[ur * L.ld + L.loff] = v;
+        if constexpr (ST) fm_st(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
       setbits(m1lo, m1hi, ob, bits);
     });
   }
   {
-    f32x16 hin[8];
-    lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
-    dense<8, C::RV_H>(A.W2, 8, hin, A.b2P, [&](int ob, const f32x16& acc) {
+    const rsrc_t hr = rsrc(H2g);
+    dense_lds<8>(A.W2, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
         const float v = fmaxf(acc[q], 0.f);
         L.bl[ur * 32] = v;
-        if (H2g) H2g[ur * L.ld + L.loff] = v;
+        if constexpr (ST) fm_st(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
       setbits(m2lo, m2hi, ob, bits);
     });
   }
   {
-    f32x16 hin[8];
-    lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
-    dense<8, C::RV_H>(A.Wh, C::NB_H2, hin, A.bhP, [&](int ob, const f32x16& acc) {
+    dense_lds<C::NB_H2>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
@@ -211,72 +222,74 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* __re
 }
 
 // ACM forward (basic_model.py:118-126): in [s | a_d] -> tanh 64 -> tanh 32 -> tanh(ac)*lim.
-// Writes z1 / z2 / t3 feature-major if given; output c into SMALL rows [0, AC).
-template <class C>
+// ST: store z1 / z2 / t3 feature-major; output c into SMALL rows [0, AC).
+template <class C, bool ST>
 __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin)[C::NB_ACMIN], const Lane& L,
                                             float* Z1g, float* Z2g, float* T3g) {
   float* small = L.sl - L.h4 * 32 - L.s;
-  dense<C::NB_ACMIN, C::RV_ACMIN>(p.acm.W1, 2, xin, p.acm.b1P, [&](int ob, const f32x16& acc) {
+  const rsrc_t z1r = rsrc(Z1g), z2r = rsrc(Z2g), t3r = rsrc(T3g);
+  dense<C::NB_ACMIN, C::RV_ACMIN>(p.acm.W1, 2, xin, L.tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ur = 32 * ob + ru(q);
       const float v = tanhf(acc[q]);
       L.sl[ur * 32] = v;
-      if (Z1g) Z1g[ur * L.ld + L.loff] = v;
+      if constexpr (ST) fm_st(z1r, ur, L.ld4, L.vo, v);
     }
   });
   f32x16 z1[2];
   lds_load<2>(z1, small);
-  dense<2, C::RV_Z1>(p.acm.W2, 1, z1, p.acm.b2P, [&](int ob, const f32x16& acc) {
+  dense<2, C::RV_Z1>(p.acm.W2, 1, z1, L.tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = tanhf(acc[q]);
       L.sl[ru(q) * 32] = v;
-      if (Z2g) Z2g[ru(q) * L.ld + L.loff] = v;
+      if constexpr (ST) fm_st(z2r, ru(q), L.ld4, L.vo, v);
     }
   });
   f32x16 z2[1];
   lds_load<1>(z2, small);
-  dense<1, C::RV_Z2>(p.acm.W3, 1, z2, p.acm.b3P, [&](int ob, const f32x16& acc) {
+  dense<1, C::RV_Z2>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int u = ru(q) + L.h4;
       if (u < C::AC) {
         const float t = tanhf(acc[q]);
         L.sl[ru(q) * 32] = t * p.acm_lim[u];
-        if (T3g) T3g[ru(q) * L.ld + L.loff] = t;
+        if constexpr (ST) fm_st(t3r, ru(q), L.ld4, L.vo, t);
       }
     }
   });
 }
 
 // Critic forward through L2 with q = w3 . relu(h2) + b3 reduced per sample.
-template <class C>
+// ST: store h1 / h2 feature-major.
+template <class C, bool ST>
 __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN], const Lane& L,
                                                 float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
                                                 uint64_t& m2lo, uint64_t& m2hi) {
-  dense<C::NB_CIN, C::RV_CIN>(Q.W1, 8, xin, Q.b1P, [&](int ob, const f32x16& acc) {
+  const rsrc_t h1r = rsrc(H1g), h2r = rsrc(H2g);
+  dense<C::NB_CIN, C::RV_CIN>(Q.W1, 8, xin, L.tbl + Q.tb1, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ur = 32 * ob + ru(q);
       const float v = fmaxf(acc[q], 0.f);
       L.bl[ur * 32] = v;
-      if (H1g) H1g[ur * L.ld + L.loff] = v;
+      if constexpr (ST) fm_st(h1r, ur, L.ld4, L.vo, v);
       bits |= (uint32_t)(v > 0.f) << q;
     }
     setbits(m1lo, m1hi, ob, bits);
   });
-  f32x16 hin[8];
-  lds_load<8>(hin, L.bl - L.h4 * 32 - L.s);
   float qp = 0.f;
-  dense<8, C::RV_H>(Q.W2, 8, hin, Q.b2P, [&](int ob, const f32x16& acc) {
+  const float* w3 = L.tbl + Q.tw3;
+  dense_lds<8>(Q.W2, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = fmaxf(acc[q], 0.f);
-      if (H2g) H2g[(32 * ob + ru(q)) * L.ld + L.loff] = v;
-      qp = fmaf(v, vec_at(Q.w3P, ob, q), qp);
+      if constexpr (ST) fm_st(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
+      qp = fmaf(v, tval(w3, ob, q, L.h4), qp);
       bits |= (uint32_t)(v > 0.f) << q;
     }
     setbits(m2lo, m2hi, ob, bits);
@@ -291,6 +304,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
                                               const float* __restrict__ EPS, const Lane& L) {
   float lp = 0.f, corr = 0.f;
   const int h8 = 8 * L.h;
+  const rsrc_t er = rsrc(EPS);
 #pragma unroll
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
@@ -301,7 +315,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         const float mu = hd[ib][r];
         const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
         const float sc = expf(ls);
-        const float e = EPS[j0 * L.ld + L.poff];
+        const float e = fm_ld(er, j0, L.ld4, L.vp);
         const float u = fadd_rn(mu, fmul_rn(e, sc));
         const float d = fsub_rn(u, mu);
         const float var = fmul_rn(sc, sc);
@@ -320,19 +334,21 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
 template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
-  float* small = big + 256 * 32;
+  float* small = big + kSmallRow * 32;
   const int ntiles = p.Bp / 32;
   const int ld = p.Bp;
   const float alpha = *p.alpha;
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
-    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
     uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
     // ---- target action: a' ~ pi(s'), a'_d, logpi'   (sac_acm.py:44-45)
-    actor_trunk<C>(p.actor, p.S2, ld, L.loff, L, nullptr, nullptr, d0, d1, d2, d3);
+    actor_trunk<C, false>(p.actor, p.S2, C::OB * L.ld4, L, nullptr, nullptr, d0, d1, d2, d3);
 #ifdef SPP_CUT
     if (SPP_CUT == 1) { p.part[tile] = L.bl[0]; continue; }
 #endif
@@ -346,18 +362,18 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     f32x16 tin[C::NB_CIN];
     if constexpr (C::ACMC) {
       f32x16 xin[C::NB_ACMIN];
-      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S2, C::OB, ld, L.loff, big, C::AOUT);
-      acm_forward<C>(p, xin, L, nullptr, nullptr, nullptr);
-      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB, ld, L.loff, small, C::AC);
+      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
+      acm_forward<C, false>(p, xin, L, nullptr, nullptr, nullptr);
+      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, small, C::AC);
     } else {
-      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB, ld, L.loff, big, C::AOUT);
+      load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
     }
 #ifdef SPP_CUT
     if (SPP_CUT == 2) { p.part[tile] = L.bl[0] + tin[0][3] + lp2; continue; }
 #endif
     // ---- soft-min twin target (:50-56)
-    const float q1t = critic_forward<C>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
-    const float q2t = critic_forward<C>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    const float q1t = critic_forward<C, false>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    const float q2t = critic_forward<C, false>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
     const float notdone = 1.f - p.DN[b];
     const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
 #ifdef SPP_CUT
@@ -369,9 +385,9 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     for (int i = 0; i < 2; ++i) {
       uint64_t m1lo = 0, m1hi = 0, m2lo = 0, m2hi = 0;
       f32x16 xin[C::NB_CIN];
-      load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, ld, L.loff);
+      load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
-      const float q = critic_forward<C>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
+      const float q = critic_forward<C, true>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;  // d mse / dq
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
@@ -381,29 +397,24 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       if (SPP_CUT == 4) continue;
 #endif
       // delta2 = dq * w3 * relu'(h2): staged through the LDS image, stored feature-major
-      float* D2 = p.D2[i];
-      const float* w3 = opaque(Q.w3P);
+      const rsrc_t d2r = rsrc(p.D2[i]);
+      const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
       for (int ob = 0; ob < 8; ++ob) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2) {
           const int ur = 32 * ob + ru(q2);
-          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * vec_at(w3, ob, q2) : 0.f;
+          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tval(w3, ob, q2, L.h4) : 0.f;
           L.bl[ur * 32] = v;
-          D2[ur * ld + L.loff] = v;
+          fm_st(d2r, ur, L.ld4, L.vo, v);
         }
       }
-      f32x16 din[8];
-      lds_load<8>(din, big);
-#ifdef SPP_CUT
-      if (SPP_CUT == 5) { p.part[tile] = din[3][5]; continue; }
-#endif
       // delta1 = (W2^T delta2) * relu'(h1)
-      float* D1 = p.D1[i];
-      dense<8, C::RV_H>(Q.W2T, 8, din, nullptr, [&](int ob, const f32x16& acc) {
+      const rsrc_t d1r = rsrc(p.D1[i]);
+      dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2)
-          D1[(32 * ob + ru(q2)) * ld + L.loff] = getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f;
+          fm_st(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
       });
     }
     const float s0 = wave_sum(lq0), s1 = wave_sum(lq1);
@@ -423,20 +434,22 @@ struct AcmScratch {
 template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratch z) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
-  float* small = big + 256 * 32;
+  float* small = big + kSmallRow * 32;
   const int ntiles = p.Bp / 32;
   const int ld = p.Bp;
   const float alpha = *p.alpha;
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
-    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
     const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
     // ---- a, logpi = actor(s)  (sac_acm.py:137)
     uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
-    actor_trunk<C>(p.actor, p.S, ld, L.loff, L, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
+    actor_trunk<C, true>(p.actor, p.S, C::OB * L.ld4, L, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
     f32x16 hd[C::NB_PAIR];
     load_pair<C>(hd, big);
     const float lp = squash_write<C>(p, hd, p.EPS2, L);  // a_d -> big rows [0, AOUT)
@@ -444,16 +457,16 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     f32x16 cin[C::NB_CIN];
     if constexpr (C::ACMC) {
       f32x16 xin[C::NB_ACMIN];
-      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S, C::OB, ld, L.loff, big, C::AOUT);
-      acm_forward<C>(p, xin, L, z.Z1, z.Z2, z.T3);
-      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB, ld, L.loff, small, C::AC);
+      load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
+      acm_forward<C, true>(p, xin, L, z.Z1, z.Z2, z.T3);
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, small, C::AC);
     } else {
-      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB, ld, L.loff, big, C::AOUT);
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
     }
     // ---- q = min(Q1, Q2)(s, c)  (:73-75), masks kept for the backward
     uint64_t ma0 = 0, ma1 = 0, ma2 = 0, ma3 = 0, mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0;
-    const float q1 = critic_forward<C>(p.critic[0], cin, L, nullptr, nullptr, ma0, ma1, ma2, ma3);
-    const float q2 = critic_forward<C>(p.critic[1], cin, L, nullptr, nullptr, mb0, mb1, mb2, mb3);
+    const float q1 = critic_forward<C, false>(p.critic[0], cin, L, nullptr, nullptr, ma0, ma1, ma2, ma3);
+    const float q2 = critic_forward<C, false>(p.critic[1], cin, L, nullptr, nullptr, mb0, mb1, mb2, mb3);
     const float qmin = fminf(q1, q2);
     // torch.minimum backward: ties split the gradient in half
     const float gq = valid ? -p.inv_B : 0.f;
@@ -468,22 +481,18 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       const CriticDev& Q = p.critic[i];
       const uint64_t k0 = i ? mb0 : ma0, k1 = i ? mb1 : ma1, k2 = i ? mb2 : ma2, k3 = i ? mb3 : ma3;
       const float dqi = i ? dqb : dqa;
-      const float* w3 = opaque(Q.w3P);
+      const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
       for (int ob = 0; ob < 8; ++ob) {
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * vec_at(w3, ob, q) : 0.f;
+          L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tval(w3, ob, q, L.h4) : 0.f;
       }
-      f32x16 din[8];
-      lds_load<8>(din, big);
-      dense<8, C::RV_H>(Q.W2T, 8, din, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
       });
-      f32x16 d1[8];
-      lds_load<8>(d1, big);
-      dense<8, C::RV_H>(Q.W1Ta, C::NB_CA, d1, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<C::NB_CA>(Q.W1Ta, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int ib = 0; ib < C::NB_CA; ++ib)
           if (ib == ob) dca[ib] += acc;
@@ -497,7 +506,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         const int u = ru(q) + L.h4;
         float v = 0.f;
         if (u < C::AC) {
-          const float t = z.T3[ru(q) * ld + L.loff];
+          const float t = fm_ld(rsrc(z.T3), ru(q), L.ld4, L.vo);
           v = dca[0][q] * p.acm_lim[u] * (1.f - t * t);
         }
         dp3[0][q] = v;
@@ -505,7 +514,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       dense<1, C::RV_AC>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const float zz = z.Z2[ru(q) * ld + L.loff];
+          const float zz = fm_ld(rsrc(z.Z2), ru(q), L.ld4, L.vo);
           L.sl[ru(q) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
@@ -515,7 +524,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int ur = 32 * ob + ru(q);
-          const float zz = z.Z1[ur * ld + L.loff];
+          const float zz = fm_ld(rsrc(z.Z1), ur, L.ld4, L.vo);
           L.sl[ur * 32] = acc[q] * (1.f - zz * zz);
         }
       });
@@ -554,7 +563,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           const float lsr = hd[ib][r + 8];
           const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
           const float sc = expf(ls);
-          const float e = p.EPS2[j0 * ld + L.poff];
+          const float e = fm_ld(rsrc(p.EPS2), j0, L.ld4, L.vp);
           const float u = fadd_rn(mu, fmul_rn(e, sc));
           const float d = fsub_rn(u, mu);
           const float t = tanhf(u);
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           float g_ad = L.pl[j0 * 32];  // from the critics through the ACM
           float g_a = 0.f;
           if (p.custom_loss != 0.f) {
-            const float s2 = p.S2[j0 * ld + L.poff];
+            const float s2 = fm_ld(rsrc(p.S2), j0, L.ld4, L.vp);
             if (p.norm_closs) {
               const float df = fsub_rn(a, normalize(p, j, s2));
               g_a += cl_scale * df;
@@ -581,8 +590,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           gmu = gu + g_lp * d / var;
           const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
           gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
-          p.ADH[j0 * ld + L.poff] = gmu;
-          p.ADH[(C::AOUT + j0) * ld + L.poff] = gls;
+          fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, gmu);
+          fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, gls);
         }
         hd[ib][r] = gmu;
         hd[ib][r + 8] = gls;
@@ -594,16 +603,14 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         const int ur = 32 * ob + ru(q);
         const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
         L.bl[ur * 32] = v;
-        p.AD2[ur * ld + L.loff] = v;
+        fm_st(rsrc(p.AD2), ur, L.ld4, L.vo, v);
       }
     });
     {
-      f32x16 d2[8];
-      lds_load<8>(d2, big);
-      dense<8, C::RV_H>(p.actor.W2T, 8, d2, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<8>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          p.AD1[(32 * ob + ru(q)) * ld + L.loff] = getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f;
+          fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
       });
     }
     const float ps = wave_sum(sac_part);
@@ -628,19 +635,21 @@ struct ActArgs {
 template <class C>
 __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
-  float* small = big + 256 * 32;
+  float* small = big + kSmallRow * 32;
   const int ntiles = (a.E + 31) / 32;
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
     const int e = tile * 32 + (lane & 31);
     const bool valid = e < a.E;
     const int er = valid ? e : 0;
     // row-major obs: element (unit u, env e) = obs[e*OB + u] -> ld = 1, offset 4h + e*OB
-    Lane L = make_lane(big, small, 1, er * C::OB);
+    Lane L = make_lane(big, small, tbl, 1, er * C::OB);
     if (a.mode != 0) {
       uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-      actor_trunk<C>(p.actor, a.obs, 1, L.loff, L, nullptr, nullptr, d0, d1, d2, d3);
+      actor_trunk<C, false>(p.actor, a.obs, a.E * C::OB * 4, L, nullptr, nullptr, d0, d1, d2, d3);
     }
     f32x16 hd[C::NB_PAIR];
     if (a.mode != 0) load_pair<C>(hd, big);
@@ -674,8 +683,8 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
       }
     // env action = ACM(cat(obs, a))  (off_policy.py:89-106)
     f32x16 xin[C::NB_ACMIN];
-    load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, a.obs, C::OB, 1, L.loff, big, C::AOUT);
-    acm_forward<C>(p, xin, L, nullptr, nullptr, nullptr);
+    load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, a.obs, a.E * C::OB * 4, C::OB, L.ld4, L.vo, big, C::AOUT);
+    acm_forward<C, false>(p, xin, L, nullptr, nullptr, nullptr);
     if (L.h == 0 && valid)
       for (int u = 0; u < C::AC; ++u) a.env_out[er * C::AC + u] = small[u * 32 + L.s];
   }
@@ -693,16 +702,18 @@ struct AcmRegArgs {
 template <class C>
 __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
-  float* small = big + 256 * 32;
+  float* small = big + kSmallRow * 32;
   const int ntiles = g.Bp / 32;
   const int ld = g.Bp;
   constexpr int IN = 2 * C::OB;
   constexpr int NB_IN = blocks_of(IN);
   constexpr uint64_t RV_IN = rv_nat(IN, NB_IN);
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
-    const Lane L = make_lane(big, small, ld, tile * 32 + (lane & 31));
+    const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < g.B;
     const int br = valid ? b : 0;
@@ -715,25 +726,25 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
         const int u = ur + L.h4;
         const float v = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
         xin[ib][r] = v;
-        if (u < IN) g.XT[ur * ld + L.loff] = v;
+        if (u < IN) fm_st(rsrc(g.XT), ur, L.ld4, L.vo, v);
       }
-    dense<NB_IN, RV_IN>(p.acm.W1, 2, xin, p.acm.b1P, [&](int ob, const f32x16& acc) {
+    dense<NB_IN, RV_IN>(p.acm.W1, 2, xin, tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
         const float v = tanhf(acc[q]);
         L.sl[ur * 32] = v;
-        g.Z1[ur * ld + L.loff] = v;
+        fm_st(rsrc(g.Z1), ur, L.ld4, L.vo, v);
       }
     });
     f32x16 z1[2];
     lds_load<2>(z1, small);
-    dense<2, C::RV_Z1>(p.acm.W2, 1, z1, p.acm.b2P, [&](int ob, const f32x16& acc) {
+    dense<2, C::RV_Z1>(p.acm.W2, 1, z1, tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float v = tanhf(acc[q]);
         L.sl[ru(q) * 32] = v;
-        g.Z2[ru(q) * ld + L.loff] = v;
+        fm_st(rsrc(g.Z2), ru(q), L.ld4, L.vo, v);
       }
     });
     f32x16 z2[1];
@@ -741,7 +752,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     float lsum = 0.f;
     f32x16 p3[1];
     const float sc = 2.f / ((float)g.B * (float)C::AC);
-    dense<1, C::RV_Z2>(p.acm.W3, 1, z2, p.acm.b3P, [&](int ob, const f32x16& acc) {
+    dense<1, C::RV_Z2>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int u = ru(q) + L.h4;
@@ -754,7 +765,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
           v = sc * df * lim * (1.f - t * t);
         }
         p3[0][q] = v;
-        if (u < C::AC) g.P3[ru(q) * ld + L.loff] = v;
+        if (u < C::AC) fm_st(rsrc(g.P3), ru(q), L.ld4, L.vo, v);
       }
     });
     dense<1, C::RV_AC>(p.acm.W3T, 1, p3, nullptr, [&](int ob, const f32x16& acc) {
@@ -763,7 +774,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
         const float zz = z2[0][q];
         const float v = acc[q] * (1.f - zz * zz);
         L.sl[ru(q) * 32] = v;
-        g.P2[ru(q) * ld + L.loff] = v;
+        fm_st(rsrc(g.P2), ru(q), L.ld4, L.vo, v);
       }
     });
     f32x16 p2[1];
@@ -773,7 +784,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
         const float zz = ob == 0 ? z1[0][q] : z1[1][q];
-        g.P1[ur * ld + L.loff] = acc[q] * (1.f - zz * zz);
+        fm_st(rsrc(g.P1), ur, L.ld4, L.vo, acc[q] * (1.f - zz * zz));
       }
     });
     const float ls = wave_sum(lsum);
@@ -832,10 +843,16 @@ __global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint6
 }
 
 // ============================================================================ debug dense
-template <int NBI>
-__global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const float* bP, const float* x, float* y, int B,
-                                                    int K, int N, int act) {
+// One layer on a [B][K] row-major batch with a natural bias b (NULL -> 0).
+// K <= 224: register-input dense (ob-major image); K == 256: dense_lds from the
+// LDS image (ib-major image), NBO compile-time.
+template <int NBI, int NBO>
+__global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const float* bias, const float* x, float* y,
+                                                    int B, int K, int N, int act) {
+  __shared__ float img[256 * 32];
+  __shared__ __attribute__((aligned(16))) float tb[256];
   const int lane = threadIdx.x & 63, h = lane >> 5, s = lane & 31;
+  for (int i = lane; i < 256; i += 64) tb[i] = (bias && i < N) ? bias[i] : 0.f;
   const int64_t b = (int64_t)blockIdx.x * 32 + s;
   f32x16 in[NBI];
 #pragma unroll
@@ -844,8 +861,10 @@ __global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const floa
     for (int r = 0; r < 16; ++r) {
       const int u = 32 * ib + unit_of(r, h);
       in[ib][r] = (u < K && b < B) ? x[b * K + u] : 0.f;
+      img[(32 * ib + ru(r) + 4 * h) * 32 + s] = in[ib][r];
     }
-  dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, bP, [&](int ob, const f32x16& acc) {
+  __syncthreads();
+  auto epi = [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int u = 32 * ob + unit_of(q, h);
@@ -854,7 +873,11 @@ __global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const floa
       if (act == 2) v = tanhf(v);
       if (u < N && b < B) y[b * N + u] = v;
     }
-  });
+  };
+  if constexpr (NBI == 8)
+    dense_lds<NBO>(Wf, img, bias ? tb : nullptr, epi);
+  else
+    dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, bias ? tb : nullptr, epi);
 }
 
 }  // namespace spp

@@ -5,19 +5,30 @@
 namespace spp {
 
 // Packed (fragment-image) views of one network, produced by the pack kernels.
+// W2 / Wh / W2T / W1Ta (256-input layers) are ib-major images for dense_lds;
+// the others are ob-major images for dense.  t* are offsets of the network's
+// bias (and critic fc3 weight) vectors in the per-workgroup LDS table.
 struct ActorDev {
   const float4 *W1, *W2, *Wh, *W2T, *WhT;
-  const float *b1P, *b2P, *bhP;  // packed bias images
+  int tb1, tb2, tbh;
 };
 struct CriticDev {
   const float4 *W1, *W2, *W2T, *W1Ta;
-  const float *b1P, *b2P, *w3P;
+  int tb1, tb2, tw3;
   const float* b3;  // canonical scalar
 };
 struct AcmDev {
   const float4 *W1, *W2, *W3, *W3T, *W2T, *W1Ta;
-  const float *b1P, *b2P, *b3P;
+  int tb1, tb2, tb3;
 };
+
+// LDS table segment: tbl[off + i] = i < n ? src[i] : 0 for i < npad.
+struct TabSeg {
+  const float* src;
+  int n, npad, off, pad_;
+};
+constexpr int kTabSegs = 20;
+constexpr int kTabMax = 4096;  // floats (16 KiB)
 
 // Feature-major ("unit-major") scratch: X[f][Bp], zero padded beyond B.
 struct SacArgs {
@@ -41,6 +52,9 @@ struct SacArgs {
   // actor-phase outputs
   float *AH1, *AH2, *AD1, *AD2, *ADH;
   float *part;  // per-tile partial sums [ntiles][8]
+  // per-workgroup LDS constant table (biases, critic fc3 weights)
+  TabSeg seg[kTabSegs];
+  int nseg;
 };
 
 constexpr int kParts = 8;

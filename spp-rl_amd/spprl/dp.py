@@ -1,0 +1,41 @@
+"""Data-parallel plumbing for the SPP-SAC hot path.
+
+One process per GPU.  Each rank steps its own E envs into a local replay shard,
+samples rho*E transitions from it and computes gradients locally; the flat
+gradient buckets of ``SAC_AcM`` ([critic_1|critic_2], [actor|alpha operand],
+[acm]) are averaged across ranks between the ``*Grads`` and ``*Apply`` halves
+of the update, so every rank applies the identical Adam step and the replicas
+stay bit-identical.  With equal shard batches the average of per-rank mean-loss
+gradients equals the full-batch mean-loss gradient (all losses of the path are
+batch means: sac_acm.py:97-131, :60-87, sac.py:201-216, acm.py:356-372).
+"""
+import torch.distributed as dist
+
+
+def make_allreduce(group=None):
+    """Returns ``allreduce(bucket)`` (in-place average over the group) or None
+    when the group has a single rank.  On ROCm the "nccl" backend is RCCL."""
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    world = dist.get_world_size(group)
+    if world == 1:
+        return None
+    inv = 1.0 / world
+
+    def allreduce(bucket):
+        dist.all_reduce(bucket, group=group)
+        bucket.mul_(inv)
+
+    return allreduce
+
+
+def shard_seed(base, rank):
+    """Per-rank seed of the env / sampling / eps streams (ranks must differ)."""
+    return int(base) + 1000 * int(rank)
+
+
+def shard_batch(B, world):
+    """Per-rank minibatch of a global batch B (equal shards keep the mean exact)."""
+    if B % world:
+        raise ValueError("global batch %d not divisible by world size %d" % (B, world))
+    return B // world

@@ -1,0 +1,139 @@
+"""Data-parallel exchange of the SAC_AcM update, world size 2 over gloo on CPU.
+
+Each rank runs the grads half of the update on its shard of the golden batch
+(the oracle stands in for the device kernels, which need a GPU), averages the
+flat buckets with ``spprl.dp.make_allreduce`` (the same callable bench.py hands
+to ``SAC_AcM.update_from_replay_dp``), then applies.  Checks: the averaged
+buckets equal the full-batch gradients, both replicas end bit-identical, and
+the post-step parameters match a single-process full-batch update.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from golden_cases import sac_case
+
+CASE = "sac_hopper_paper"
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _make_oracle(cfg, params, norm, ob, aout, ac):
+    from oracle.sac_acm import OracleSacAcm
+    return OracleSacAcm(ob, aout, ac, acm_critic=cfg["acm_critic"], custom_loss=cfg["custom_loss"],
+                        norm_closs=cfg["norm_closs"], norm=norm, acm_lim=np.ones(ac, np.float32), params=params)
+
+
+def _flat(gs):
+    return torch.cat([g.reshape(-1) for g in gs])
+
+
+def _unflat(flat, like):
+    out, o = [], 0
+    for g in like:
+        out.append(flat[o:o + g.numel()].view_as(g).clone())
+        o += g.numel()
+    return out
+
+
+def _step(o, batch, e1, e2, allreduce):
+    """update_from_replay_dp's exchange points, on the oracle."""
+    obs, nobs, act, rew, done, acm = batch
+    cg, _, _ = o.critic_grads(obs, nobs, act, rew, done, acm, e1)
+    bucket = torch.cat([_flat(cg["critic_1"]), _flat(cg["critic_2"])])  # [critic_1 | critic_2]
+    if allreduce is not None:
+        allreduce(bucket)
+    n1 = sum(g.numel() for g in cg["critic_1"])
+    avg_c = {"critic_1": _unflat(bucket[:n1], cg["critic_1"]), "critic_2": _unflat(bucket[n1:], cg["critic_2"])}
+    o.critic_apply(avg_c)
+    g, ga, _, _ = o.actor_grads(obs, nobs, e2)
+    bucket_a = torch.cat([_flat(g), ga.reshape(1).to(torch.float32)])  # [actor | alpha operand]
+    if allreduce is not None:
+        allreduce(bucket_a)
+    o.actor_apply(_unflat(bucket_a[:-1], g), bucket_a[-1].to(torch.float64))
+    return bucket, bucket_a
+
+
+def _state(o):
+    return {k: o.flat(k) for k in o.p} | {"log_alpha": np.array([o.log_alpha.item()])}
+
+
+def _worker(rank, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from spprl.dp import make_allreduce, shard_batch
+        cfg, fx, params, layouts, norm, steps = sac_case(CASE)
+        ob, aout, ac, B = (int(v) for v in fx["dims"])
+        b = shard_batch(B, WORLD)
+        sl = slice(rank * b, (rank + 1) * b)
+        o = _make_oracle(cfg, params, norm, ob, aout, ac)
+        allreduce = make_allreduce()
+        assert allreduce is not None
+        buckets = []
+        for batch, e1, e2 in steps:
+            bc, ba = _step(o, tuple(x[sl] for x in batch), e1[sl], e2[sl], allreduce)
+            buckets.append((bc.numpy(), ba.numpy()))
+        st = _state(o)
+        np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **st,
+                 **{"bc%d" % i: x[0] for i, x in enumerate(buckets)}, **{"ba%d" % i: x[1] for i, x in enumerate(buckets)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_world2_gloo_matches_full_batch(tmp_path):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, "rank exited with %s" % p.exitcode
+    r0 = dict(np.load(tmp_path / "rank0.npz"))
+    r1 = dict(np.load(tmp_path / "rank1.npz"))
+    # replicas bit-identical after the exchange
+    for k in r0:
+        assert np.array_equal(r0[k], r1[k]), k
+
+    # single-process full-batch reference
+    cfg, fx, params, layouts, norm, steps = sac_case(CASE)
+    ob, aout, ac, B = (int(v) for v in fx["dims"])
+    o = _make_oracle(cfg, params, norm, ob, aout, ac)
+    for i, (batch, e1, e2) in enumerate(steps):
+        bc, ba = _step(o, batch, e1, e2, None)
+        for got, want in ((r0["bc%d" % i], bc.numpy()), (r0["ba%d" % i], ba.numpy())):
+            scale = np.abs(want).max()
+            assert np.abs(got - want).max() <= 1e-5 * scale
+    full = _state(o)
+    for k, want in full.items():
+        d = np.abs(r0[k] - want)
+        # Adam normalises the step: agreement to ~1e-6 except where a gradient
+        # element sits at rounding level (sign may differ -> at most 2*lr*steps)
+        assert np.mean(d > 1e-5) < 1e-3, (k, np.mean(d > 1e-5))
+        assert d.max() <= 2 * 1e-3 * len(steps) + 1e-6, k
+
+
+def test_make_allreduce_single_process_is_none():
+    from spprl.dp import make_allreduce, shard_batch
+    assert make_allreduce() is None
+    assert shard_batch(409600, 8) == 51200
+    with pytest.raises(ValueError):
+        shard_batch(100, 3)

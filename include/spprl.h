@@ -218,6 +218,30 @@ sppStatus sppPolicyAct(sppAgentHandle h, const float* obs /*[E][ob]*/, int E, co
 sppStatus sppSynthEnvStep(const float* A /*[ob][ob]*/, const float* obs /*[E][ob]*/, const float* action /*[E][ac]*/,
                           int E, int ob, int ac, float* next_obs, float* reward, void* stream);
 
+/* ------------------------------------------------------------------ PPO path
+ * PPO.calculate_q_val + calculate_gae (rltoolkit/algorithms/a2c/a2c.py:247-265,
+ * algorithms/ppo/ppo.py:117-150) over E independent streams of T steps, time-major
+ * [T][E] (E = 1 is the reference's single rollout buffer).  Inputs are the critic's
+ * V(s), V(s') and the buffer's rewards / done / end (truncation) flags.
+ *   q_out[t][e] = r + gamma (1 - d) V(s')          (optional, may be NULL)
+ *   adv[t][e]   = reverse GAE with done reset and end bootstrap V(s') (quirk Q10)
+ * mode 0: one lane per stream, the reference's float32 operation order (bit-exact);
+ * mode 1: reverse affine scan with wavefront shuffles, one workgroup per stream
+ *         (for few long streams; fp32 reassociation, not bit-exact);
+ * mode -1: 0 when E >= 64, else 1. */
+sppStatus sppGaeScan(const float* rew, const float* v, const float* v_next, const uint8_t* done,
+                     const uint8_t* end, int64_t T, int64_t E, double gamma, double lam, int mode, float* q_out,
+                     float* adv, void* stream);
+/* PPO._clip_loss (ppo.py:194-204) and utils.kl_divergence (utils.py:48-59) on a
+ * minibatch of B: out2[0] = -mean(min(r A, clip(r, 1-eps, 1+eps) A)), r = exp(lp_new - lp_old);
+ * out2[1] = mean(lp_old - lp_new).  grad (optional) = d out2[0] / d lp_new with torch's
+ * minimum (ties split) and clamp (inclusive bounds) backward rules. */
+sppStatus sppPpoClipLoss(const float* lp_old, const float* lp_new, const float* adv, int B, float eps, float* grad,
+                         float* out2, void* stream);
+/* AdvantageDataset normalisation (algorithms/ppo/advantage_dataset.py:8-12):
+ * out = (adv - mean) / (std(ddof=1) + 1.2e-7).  out may alias adv. */
+sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream);
+
 /* Debug / layout check: y = act(x W^T + b) through the MFMA register-tile path.
  * x [B][K], W [N][K], b [N], y [B][N]; act 0 none, 1 relu, 2 tanh. */
 sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,

@@ -15,6 +15,7 @@
 
 #include "dw.hip"
 #include "optim.hip"
+#include "ppo.hip"
 #include "replay.hip"
 #include "sac.hip"
 
@@ -316,6 +317,50 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   return SPP_OK;
 }
 
+sppStatus sppGaeScan(const float* rew, const float* v, const float* v_next, const uint8_t* done,
+                     const uint8_t* end, int64_t T, int64_t E, double gamma, double lam, int mode, float* q_out,
+                     float* adv, void* stream) {
+  SPP_REQUIRE(T >= 0 && E > 0 && mode >= -1 && mode <= 1, SPP_E_INVALID_ARG, "gae: T=%lld E=%lld mode=%d",
+              (long long)T, (long long)E, mode);
+  if (T == 0) return SPP_OK;
+  SPP_REQUIRE(rew && v && v_next && done && end && adv, SPP_E_INVALID_ARG, "gae: null input");
+  if (mode < 0) mode = E >= 64 ? 0 : 1;
+  const double disc = lam * gamma;  // python floats: discount = gae_lambda * gamma (ppo.py:136)
+  if (mode == 0)
+    hipLaunchKernelGGL(k_gae_seq, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), rew, v, v_next, done, end, T, E,
+                       (float)gamma, disc, q_out, adv);
+  else
+    hipLaunchKernelGGL(k_gae_scan, dim3(E), dim3(kScanThreads), 0, S(stream), rew, v, v_next, done, end, T, E,
+                       (float)gamma, (float)disc, q_out, adv);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppPpoClipLoss(const float* lp_old, const float* lp_new, const float* adv, int B, float eps, float* grad,
+                         float* out2, void* stream) {
+  SPP_REQUIRE(lp_old && lp_new && adv && out2 && B > 0, SPP_E_INVALID_ARG, "clip loss: bad args");
+  const int nblk = cdiv(B, 256);
+  double* part = nullptr;
+  SPP_CHECK_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * nblk, S(stream)));
+  hipLaunchKernelGGL(k_ppo_clip, dim3(nblk), dim3(256), 0, S(stream), lp_old, lp_new, adv, B, eps, grad, part);
+  hipLaunchKernelGGL(k_ppo_clip_finish, dim3(1), dim3(256), 0, S(stream), (const double*)part, nblk, B, out2);
+  SPP_CHECK_HIP(hipFreeAsync(part, S(stream)));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream) {
+  SPP_REQUIRE(adv && out && n > 0, SPP_E_INVALID_ARG, "adv normalize: bad args");
+  const int nblk = (int)std::min<int64_t>(cdiv(n, 256), 1024);
+  double* part = nullptr;
+  SPP_CHECK_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * nblk, S(stream)));
+  hipLaunchKernelGGL(k_adv_moments, dim3(nblk), dim3(256), 0, S(stream), adv, n, part);
+  hipLaunchKernelGGL(k_adv_norm, dim3(nblk), dim3(256), 0, S(stream), adv, n, (const double*)part, nblk, out);
+  SPP_CHECK_HIP(hipFreeAsync(part, S(stream)));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
 sppStatus sppSynthEnvStep(const float* A, const float* obs, const float* action, int E, int ob, int ac,
                           float* next_obs, float* reward, void* stream) {
   SPP_REQUIRE(A && obs && action && next_obs && reward && E > 0, SPP_E_INVALID_ARG, "synth env: bad args");
@@ -418,6 +463,7 @@ struct sppAgent {
     DevArray<int> items;
     int B = -1;
     int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
+    int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
   } dws[2];
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
@@ -569,16 +615,34 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
   const int ca = a->cfg.acm_critic ? ac : aout, cin = ob + ca;
   std::vector<DwJob> jobs;
-  auto J = [&](const float* A, int N, const float* X0, int K0, const float* X1, int K1, float* dW, float* db) {
+  // rows >= nrow2 of a job go to (dW2, db2)
+  auto J = [&](const float* A, int N, const float* X0, int K0, const float* X1, int K1, float* dW, float* db,
+               int nrow2 = -1, float* dW2 = nullptr, float* db2 = nullptr) {
     DwJob j{};
     j.A = A; j.N = N; j.X0 = X0; j.K0 = K0; j.X1 = X1; j.K1 = K1; j.dW = dW; j.db = db; j.Bp = Bp;
-    // every work item covers <= 2048 samples so no job's items serialise the launch
-    int ns = cdiv(Bp, 2048);
-    ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
-    j.split_len = (int)round_up(cdiv(Bp, ns), 32);
-    j.nsplit = cdiv(Bp, j.split_len);
-    j.slab_stride = (int64_t)N * (K0 + K1) + N;
+    j.nrow2 = nrow2 < 0 ? N : nrow2;
+    j.dW2 = dW2; j.db2 = db2;
+    j.slab_stride = round_up((int64_t)N * (K0 + K1) + N, 4);
     jobs.push_back(j);
+  };
+  // Sample splits: the large (>= 128x128 padded) GEMMs of a phase share ~one
+  // workgroup per CU in proportion to their MACs; the small, HBM-bound ones
+  // take 2048-sample items.
+  auto is_big = [](const DwJob& j) {
+    return (int64_t)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32) >= 128 * 128;
+  };
+  auto assign_splits = [&](int first, int count) {
+    double big = 0.0;
+    for (int i = first; i < first + count; ++i)
+      if (is_big(jobs[i])) big += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
+    for (int i = first; i < first + count; ++i) {
+      DwJob& j = jobs[i];
+      const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
+      int ns = is_big(j) ? (int)std::lround(a->num_cu * pm / big) : cdiv(Bp, 2048);
+      ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
+      j.split_len = (int)round_up(cdiv(Bp, ns), 32);
+      j.nsplit = cdiv(Bp, j.split_len);
+    }
   };
   sppAgent::DwSet& D = a->dws[set];
   int nph = 0;
@@ -598,8 +662,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
           *gbp = gWp + aout * 256, *gWs = gbp + aout, *gbs = gWs + aout * 256;
     J(a->AD1, 256, a->S, ob, nullptr, 0, gW1, gb1);
     J(a->AD2, 256, a->AH1, 256, nullptr, 0, gW2, gb2);
-    J(a->ADH, aout, a->AH2, 256, nullptr, 0, gWp, gbp);
-    J(a->ADH + (int64_t)aout * Bp, aout, a->AH2, 256, nullptr, 0, gWs, gbs);
+    J(a->ADH, 2 * aout, a->AH2, 256, nullptr, 0, gWp, gbp, aout, gWs, gbs);  // [mu | log-std] heads
     D.j0[1] = D.nj[0];
     D.nj[1] = (int)jobs.size() - D.nj[0];
     nph = 2;
@@ -614,6 +677,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     D.nj[0] = (int)jobs.size();
     nph = 1;
   }
+  for (int ph = 0; ph < nph; ++ph) assign_splits(D.j0[ph], D.nj[ph]);
   // slabs: phases run back to back on one stream -> they share one arena
   size_t need = 0;
   for (int ph = 0; ph < nph; ++ph) {
@@ -639,11 +703,19 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
         jobs[j].slab = D.slab.ptr + off;
         off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
       }
-      for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
-        jj.push_back(j - D.j0[ph]);
-        ss.push_back(sp);
-      }
     }
+    // large-GEMM items first (they set the launch's critical path)
+    for (int pass = 0; pass < 2; ++pass)
+      for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+        if (is_big(jobs[j]) != (pass == 0)) continue;
+        for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
+          jj.push_back(j - D.j0[ph]);
+          ss.push_back(sp);
+        }
+      }
+    D.max_elems[ph] = 1;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j)
+      D.max_elems[ph] = std::max<int64_t>(D.max_elems[ph], (int64_t)jobs[j].N * (jobs[j].K0 + jobs[j].K1) + jobs[j].N);
     D.ioff[ph] = (int)items.size();
     D.nitems[ph] = (int)jj.size();
     items.insert(items.end(), jj.begin(), jj.end());
@@ -665,7 +737,7 @@ static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) {
   const int* is = ij + D.nitems[ph];
   const DwJob* jobs = D.jobs.ptr + D.j0[ph];
   hipLaunchKernelGGL(k_dw, dim3(D.nitems[ph]), dim3(kDwThreads), 0, st, jobs, ij, is);
-  hipLaunchKernelGGL(k_dw_reduce, dim3(64, D.nj[ph]), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_dw_reduce, dim3(cdiv(D.max_elems[ph], 4 * 256), D.nj[ph]), dim3(256), 0, st, jobs);
 }
 
 // Adam job table [critic1, critic2 (+polyak targets) | actor | acm]; pointers only.

@@ -64,9 +64,21 @@ constexpr int regs_valid(int K, int ib) {
 constexpr int blocks_of(int n) { return (n + 31) / 32; }
 
 // float-exact (no contraction) helpers where the reference rounds twice
-__device__ __forceinline__ float fmul_rn(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float fadd_rn(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float fsub_rn(float a, float b) { return __fsub_rn(a, b); }
+// Separately rounded fp32 ops: hipcc contracts a*b+c into an FMA by default
+// (-ffp-contract=fast, and __fmul_rn/__fadd_rn are plain operators), which
+// changes rounding against the reference's torch/numpy evaluation order.
+__device__ __forceinline__ float fmul_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float fadd_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float fsub_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
 __device__ __forceinline__ float fdiv_rn(float a, float b) { return __fdiv_rn(a, b); }
 
 __device__ __forceinline__ float wave_sum(float v) {

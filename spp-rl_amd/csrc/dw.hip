@@ -1,131 +1,199 @@
 // Weight gradients as split-K MFMA GEMMs over the batch:
 //   dW[n][k] = sum_b A[n][b] * X[k][b],   db[n] = sum_b A[n][b]
 // A = per-sample layer-output gradients (delta) and X = layer inputs, both
-// feature-major [rows][Bp] as written by the per-sample kernels.  One
-// workgroup (8 waves) owns the whole <=256x256 output of one job for one
-// sample range; partial slabs are summed in a fixed order (deterministic).
+// feature-major [rows][Bp] as written by the per-sample kernels.
+//
+// One work item = (job, sample range).  A workgroup of 4 waves owns the whole
+// <=256x256 output of its item: wave w holds the 128x128 quadrant
+// (n blocks 4*(w>>1).., k blocks 4*(w&1)..) as 16 accumulator tiles.  The
+// operands need no LDS: the sum over samples is order-free, so lane half h
+// takes samples [b+8h, b+8h+8) of its row as two float4 and feeds them to 8
+// consecutive MFMA k-steps for both A and X (same sample<->k map on both
+// sides).  Each lane streams its 4 A rows and 4 X rows straight from HBM
+// through an R-deep register ring (loads for step t+R-1 issued before step
+// t's MFMAs).  Partial slabs are summed in a fixed order by k_dw_reduce
+// (deterministic, no atomics).
 #include "common.h"
 #include "internal.h"
 
 namespace spp {
 
-constexpr int kDwThreads = 512;
-constexpr int kDwChunk = 32;       // samples per LDS stage
-constexpr int kDwPad = kDwChunk + 1;
+constexpr int kDwThreads = 256;
+constexpr int kDwRing = 2;  // steps (16 samples each) in flight
+
+// One step = 16 samples: lane half h takes samples [16t + 8h, +8) of each of
+// its rows as two adjacent float4 (a full 64 B run per row and half), i.e. 8
+// MFMA k-steps per row pair.
+template <int NI, int NJ, bool DB>
+__device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
+                                        f32x16 (&acc)[4][4], float (&bs)[4]) {
+  float4 ra[kDwRing][NI][2], rx[kDwRing][NJ][2];
+  const float* a0[NI];
+  const float* x0[NJ];
+  static_for<0, NI>([&](auto I) { a0[I] = ap[I]; });
+  static_for<0, NJ>([&](auto J) { x0[J] = xp[J]; });
+  auto load = [&](auto SL, int t) {
+    constexpr int sl = decltype(SL)::value;
+    static_for<0, NI>([&](auto I) {
+      ra[sl][I][0] = *reinterpret_cast<const float4*>(a0[I] + 16 * t);
+      ra[sl][I][1] = *reinterpret_cast<const float4*>(a0[I] + 16 * t + 4);
+    });
+    static_for<0, NJ>([&](auto J) {
+      rx[sl][J][0] = *reinterpret_cast<const float4*>(x0[J] + 16 * t);
+      rx[sl][J][1] = *reinterpret_cast<const float4*>(x0[J] + 16 * t + 4);
+    });
+  };
+  static_for<0, kDwRing - 1>([&](auto S) { load(S, (int)S); });
+#pragma unroll 1
+  for (int t0 = 0; t0 < nsteps; t0 += kDwRing) {
+    static_for<0, kDwRing>([&](auto U) {
+      constexpr int u = U;
+      constexpr int sn = (u + kDwRing - 1) % kDwRing;
+      const int tn = t0 + u + kDwRing - 1;
+      if (tn < nsteps) load(IC<sn>{}, tn);
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, NI>([&](auto I) {
+        static_for<0, 2>([&](auto P) {
+          const float4 av = ra[u][I][P];
+          if constexpr (DB) bs[I] += (av.x + av.y) + (av.z + av.w);
+          static_for<0, NJ>([&](auto J) {
+            const float4 xv = rx[u][J][P];
+            acc[I][J] = mfma(av.x, xv.x, acc[I][J]);
+            acc[I][J] = mfma(av.y, xv.y, acc[I][J]);
+            acc[I][J] = mfma(av.z, xv.z, acc[I][J]);
+            acc[I][J] = mfma(av.w, xv.w, acc[I][J]);
+          });
+        });
+      });
+    });
+  }
+}
 
 __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ jobs, const int* __restrict__ item_job,
                                                       const int* __restrict__ item_split) {
-  __shared__ float sA[256 * kDwPad];
-  __shared__ float sX[256 * kDwPad];
   const int item = blockIdx.x;
   const DwJob J = jobs[item_job[item]];
   const int split = item_split[item];
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
   const int64_t ld = J.Bp;
-  const int64_t b_begin = (int64_t)split * J.split_len;
-  const int64_t b_end = min<int64_t>(b_begin + J.split_len, (int64_t)J.Bp);
+  const int b_begin = split * J.split_len;
+  const int b_end = min(b_begin + J.split_len, J.Bp);
+  const int nsteps = (b_end - b_begin) / 16;  // split_len and Bp are multiples of 32
   const int N = J.N, K = J.K0 + J.K1;
-  const int Nr = (N + 31) & ~31, Kr = (K + 31) & ~31;
-  // wave tile: n blocks [4*(w>>2), +4), k blocks [2*(w&3), +2)
-  const int nb0 = 4 * (w >> 2), kb0 = 2 * (w & 3);
-  f32x16 acc[4][2];
+  const int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1);
+  const int ni = min(4, max(0, (N + 31) / 32 - nb0));
+  const int nj = min(4, max(0, (K + 31) / 32 - kb0));
+  if (ni == 0 || nj == 0) return;
+  const bool db = J.db != nullptr && (w & 1) == 0;
+  // per-lane row pointers at this item's first sample; rows past N / K are
+  // clamped to row 0 (their outputs are never stored)
+  const float* ap[4];
+  const float* xp[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
-  float dbsum = 0.f;
-  // staging: each thread moves 4 float4 of A and 4 of X per stage
-  float4 ra[4], rx[4];
-  auto gload = [&](int64_t b0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (t >> 3) + 64 * i, c4 = t & 7;
-      const int64_t off = b0 + 4 * c4;
-      ra[i] = row < N ? *reinterpret_cast<const float4*>(J.A + (int64_t)row * ld + off) : make_float4(0, 0, 0, 0);
-      const float* xr = row < J.K0 ? J.X0 + (int64_t)row * ld : (row < K ? J.X1 + (int64_t)(row - J.K0) * ld : nullptr);
-      rx[i] = xr ? *reinterpret_cast<const float4*>(xr + off) : make_float4(0, 0, 0, 0);
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (t >> 3) + 64 * i, c = 4 * (t & 7);
-      if (row < Nr) {
-        float* d = sA + row * kDwPad + c;
-        d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
-      }
-      if (row < Kr) {
-        float* d = sX + row * kDwPad + c;
-        d[0] = rx[i].x; d[1] = rx[i].y; d[2] = rx[i].z; d[3] = rx[i].w;
-      }
-    }
-  };
-  const bool nact[4] = {32 * (nb0 + 0) < N, 32 * (nb0 + 1) < N, 32 * (nb0 + 2) < N, 32 * (nb0 + 3) < N};
-  const bool kact[2] = {32 * (kb0 + 0) < K, 32 * (kb0 + 1) < K};
-  if (b_begin < b_end) gload(b_begin);
-  for (int64_t b0 = b_begin; b0 < b_end; b0 += kDwChunk) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (b0 + kDwChunk < b_end) gload(b0 + kDwChunk);
-    if (J.db && t < 2 * Nr && (t >> 1) < N) {
-      const float* rowp = sA + (t >> 1) * kDwPad + 16 * (t & 1);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) dbsum += rowp[c];
-    }
-#pragma unroll
-    for (int kk = 0; kk < kDwChunk / 2; ++kk) {
-      const int col = 2 * kk + h;
-      float bf[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = kact[j] ? sX[(32 * (kb0 + j) + (lane & 31)) * kDwPad + col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (!nact[i]) continue;
-        const float af = sA[(32 * (nb0 + i) + (lane & 31)) * kDwPad + col];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          if (kact[j]) acc[i][j] = mfma(af, bf[j], acc[i][j]);
-      }
-    }
+  for (int i = 0; i < 4; ++i) {
+    int n = 32 * (nb0 + i) + c;
+    n = n < N ? n : 0;
+    ap[i] = J.A + (int64_t)n * ld + b_begin + 8 * h;
+    int k = 32 * (kb0 + i) + c;
+    k = k < K ? k : 0;
+    xp[i] = (k < J.K0 ? J.X0 + (int64_t)k * ld : J.X1 + (int64_t)(k - J.K0) * ld) + b_begin + 8 * h;
   }
-  // write the partial (or final) result
-  float* out = J.nsplit == 1 ? nullptr : J.slab + (int64_t)split * J.slab_stride;
+  f32x16 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (!nact[i] || !kact[j]) continue;
-      const int k = 32 * (kb0 + j) + (lane & 31);
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+#define SPP_DW_CASE(I, J_)                                             \
+  case (I) * 8 + (J_):                                                 \
+    if (db) dw_tile<I, J_, true>(ap, xp, nsteps, acc, bs);             \
+    else dw_tile<I, J_, false>(ap, xp, nsteps, acc, bs);               \
+    break;
+  switch (ni * 8 + nj) {
+    SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)
+    SPP_DW_CASE(2, 1) SPP_DW_CASE(2, 2) SPP_DW_CASE(2, 3) SPP_DW_CASE(2, 4)
+    SPP_DW_CASE(3, 1) SPP_DW_CASE(3, 2) SPP_DW_CASE(3, 3) SPP_DW_CASE(3, 4)
+    SPP_DW_CASE(4, 1) SPP_DW_CASE(4, 2) SPP_DW_CASE(4, 3) SPP_DW_CASE(4, 4)
+  }
+#undef SPP_DW_CASE
+  // partial (or final) result; rows >= nrow2 go to the second output (dW2/db2)
+  const bool direct = J.nsplit == 1;
+  float* slab = direct ? nullptr : J.slab + (int64_t)split * J.slab_stride;
+  auto out_w = [&](int n, int k, float v) {
+    if (!direct) slab[(int64_t)n * K + k] = v;
+    else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;
+    else J.dW2[(int64_t)(n - J.nrow2) * K + k] = v;
+  };
+  auto out_b = [&](int n, float v) {
+    if (!direct) slab[(int64_t)N * K + n] = v;
+    else if (n < J.nrow2) J.db[n] = v;
+    else J.db2[n - J.nrow2] = v;
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= ni) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= nj) break;
+      const int k = 32 * (kb0 + j) + c;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int n = 32 * (nb0 + i) + unit_of(q, h);
-        if (n < N && k < K) {
-          if (out) out[(int64_t)n * K + k] = acc[i][j][q];
-          else J.dW[(int64_t)n * K + k] = acc[i][j][q];
-        }
+        if (n < N && k < K) out_w(n, k, acc[i][j][q]);
       }
     }
-  if (J.db) {
-    const float tot = dbsum + __shfl_xor(dbsum, 1, 64);
-    if ((t & 1) == 0 && (t >> 1) < N) {
-      if (out) out[(int64_t)N * K + (t >> 1)] = tot;
-      else J.db[t >> 1] = tot;
+    if (db) {
+      const float tot = bs[i] + __shfl_xor(bs[i], 32, 64);
+      const int n = 32 * (nb0 + i) + c;
+      if (h == 0 && n < N) out_b(n, tot);
     }
   }
 }
 
-// Fixed-order reduction of the split slabs.
+// Fixed-order reduction of the split slabs: one thread per 4 consecutive
+// elements of a job's [N*K | N] image, slabs summed in split order.
 __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const DwJob J = jobs[blockIdx.y];
   if (J.nsplit == 1) return;
   const int N = J.N, K = J.K0 + J.K1;
-  const int64_t total = (int64_t)N * K + (J.db ? N : 0);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int sp = 0; sp < J.nsplit; ++sp) s += J.slab[(int64_t)sp * J.slab_stride + e];
-    if (e < (int64_t)N * K) J.dW[e] = s;
-    else J.db[e - (int64_t)N * K] = s;
+  const int64_t nw = (int64_t)N * K;
+  const int64_t total = nw + (J.db ? N : 0);
+  const int64_t e0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (e0 >= total) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* p = J.slab + e0;
+  if (e0 + 4 <= total) {
+    int sp = 0;
+    for (; sp + 4 <= J.nsplit; sp += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(sp + u) * J.slab_stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[0] += v[u].x; s[1] += v[u].y; s[2] += v[u].z; s[3] += v[u].w;
+      }
+    }
+    for (; sp < J.nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)sp * J.slab_stride);
+      s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+    }
+  } else {
+    for (int sp = 0; sp < J.nsplit; ++sp)
+      for (int u = 0; e0 + u < total; ++u) s[u] += p[(int64_t)sp * J.slab_stride + u];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t e = e0 + u;
+    if (e >= total) break;
+    if (e < nw) {
+      const int n = (int)(e / K), k = (int)(e % K);
+      if (n < J.nrow2) J.dW[(int64_t)n * K + k] = s[u];
+      else J.dW2[(int64_t)(n - J.nrow2) * K + k] = s[u];
+    } else {
+      const int n = (int)(e - nw);
+      if (n < J.nrow2) J.db[n] = s[u];
+      else J.db2[n - J.nrow2] = s[u];
+    }
   }
 }
 

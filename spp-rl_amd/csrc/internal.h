@@ -10,12 +10,14 @@ struct DwJob {
   const float* A;   // delta [N][Bp]
   const float* X0;  // input segment 0 [K0][Bp]
   const float* X1;  // input segment 1 [K1][Bp] (may be null)
-  float* dW;        // [N][K0+K1] canonical
-  float* db;        // [N] or null
-  float* slab;      // split partials
+  float* dW;        // rows [0, nrow2) of [N][K0+K1], canonical
+  float* db;        // [nrow2] or null
+  float* dW2;       // rows [nrow2, N) (second output, e.g. the log-std head), or null
+  float* db2;
+  float* slab;      // split partials [nsplit][slab_stride]
   int64_t slab_stride;
   int N, K0, K1, Bp;
-  int split_len, nsplit;
+  int split_len, nsplit, nrow2;
 };
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)

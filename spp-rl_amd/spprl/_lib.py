@@ -90,6 +90,11 @@ _SIGS = {
     "sppAgentSetTiming": (c_int, [c_void_p, c_int]),
     "sppAgentGetTiming": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppSynthEnvStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sppGaeScan": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, ctypes.c_double,
+                           ctypes.c_double,
+                            c_int, c_void_p, c_void_p, c_void_p]),
+    "sppPpoClipLoss": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    "sppAdvNormalize": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }
 EXPORTED = tuple(_SIGS)

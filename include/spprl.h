@@ -99,14 +99,16 @@ typedef struct {
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);
 
 /* ------------------------------------------------------------------ agent */
-enum { SPP_ALGO_SAC_ACM = 1 };
+enum { SPP_ALGO_SAC_ACM = 1, SPP_ALGO_DDPG_ACM = 2 };
 enum { /* network ids for parameter binding (SAC_AcM) */
   SPP_NET_ACTOR = 0, SPP_NET_CRITIC1 = 1, SPP_NET_CRITIC2 = 2,
-  SPP_NET_CRITIC1_TARG = 3, SPP_NET_CRITIC2_TARG = 4, SPP_NET_ACM = 5, SPP_NET_COUNT = 6
+  SPP_NET_CRITIC1_TARG = 3, SPP_NET_CRITIC2_TARG = 4, SPP_NET_ACM = 5,
+  SPP_NET_ACTOR_TARG = 6, /* DDPG_AcM only; DDPG's single critic / target use CRITIC1 / CRITIC1_TARG */
+  SPP_NET_COUNT = 7
 };
 
 typedef struct {
-  int algo;                 /* SPP_ALGO_SAC_ACM */
+  int algo;                 /* SPP_ALGO_SAC_ACM (ACM = AcM 64-32) | SPP_ALGO_DDPG_ACM (ACM = BasicAcM) */
   int ob, aout, ac;         /* obs dim, actor output dim (= len(acm_ob_idx) = ob), env action dim */
   int acm_critic;           /* critics see ACM(s, denorm a) (ac) instead of denorm a (aout) */
   int min_max_denormalize;  /* memory.py:107-121 min-max vs z-score */
@@ -182,6 +184,18 @@ sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int
  * device from (seed, counter). */
 sppStatus sppSacAcmUpdateStaged(sppAgentHandle h, uint64_t seed, uint64_t counter, float* losses_dev,
                                 void* stream);
+
+/* DDPG_AcM.update (rltoolkit/acm/off_policy/ddpg_acm.py:147-201): critic step on
+ * y = r + gamma (1-d) Q_targ(s', BasicAcM(s', denorm mu_targ(s'))), actor step on
+ * -Q(s, BasicAcM(s, denorm mu(s))).mean() + custom_loss * MSE, then polyak of the critic
+ * AND actor targets (ddpg.py:273-284).  Losses (device float[8]): {critic, actor, ddpg, dist}.
+ * Split at the same exchange points as SAC_AcM for data-parallel use; batch == NULL
+ * uses the staged batch (sppAgentStageFromReplay). */
+sppStatus sppDdpgAcmUpdate(sppAgentHandle h, const sppBatch* batch, float* losses_dev, void* stream);
+sppStatus sppDdpgAcmCriticGrads(sppAgentHandle h, const sppBatch* batch, float* losses_dev, void* stream);
+sppStatus sppDdpgAcmCriticApply(sppAgentHandle h, void* stream);
+sppStatus sppDdpgAcmActorGrads(sppAgentHandle h, float* losses_dev, void* stream);
+sppStatus sppDdpgAcmActorApply(sppAgentHandle h, void* stream);
 
 /* AcMTrainer.batch_update (rltoolkit/acm/acm.py:246-258): x [B][2ob], y [B][ac]
  * -> MSE loss (device float) and one Adam step on the bound ACM net. */

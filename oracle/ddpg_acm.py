@@ -1,9 +1,9 @@
 """ORACLE (test infrastructure only): one DDPG_AcM grad step, restated.
 
 Follows rltoolkit/acm/off_policy/ddpg_acm.py (reference @ v0):
-  compute_qfunc_targ :295-318  y = r + g(1-d) Qt(s', ACM(s', denorm mu_t(s')))
-  compute_pi_loss    :320-340  -Q(s, ACM(s, denorm mu(s))).mean() + c*MSE
-  update             :342-396  critic step, actor step, polyak on critic AND actor targets
+  compute_qfunc_targ :100-123  y = r + g(1-d) Qt(s', ACM(s', denorm mu_t(s')))
+  compute_pi_loss    :125-145  -Q(s, ACM(s, denorm mu(s))).mean() + c*MSE
+  update             :147-201  critic step, actor step, polyak on critic AND actor targets
 polyak: rltoolkit/algorithms/ddpg/ddpg.py:273-284.  The SPP-DDPG scripts inject
 BasicAcM (train/spp_ddpg_hcheetah.py:124) — ``acm_kind`` selects it.
 """
@@ -53,7 +53,8 @@ class OracleDdpgAcm:
             action = acm_action
         lq = F.mse_loss(nets.ddpg_critic(P["critic"], obs, action), y)
         losses["critic"] = lq.item()
-        self.opt["critic"].step(torch.autograd.grad(lq, list(P["critic"].values())))
+        gq = torch.autograd.grad(lq, list(P["critic"].values()))
+        self.opt["critic"].step(gq)
         a = nets.ddpg_actor(P["actor"], obs, self.actor_lim)
         ad = self.norm.denormalize(a)
         ca = self._acm(torch.cat([obs, ad], axis=1)) if self.acm_critic else ad
@@ -66,7 +67,10 @@ class OracleDdpgAcm:
             losses["dist"] = dist.item()
             loss = loss + self.custom_loss * dist
         losses["actor"] = loss.item()
-        self.opt["actor"].step(torch.autograd.grad(loss, list(P["actor"].values())))
+        ga = torch.autograd.grad(loss, list(P["actor"].values()))
+        self.opt["actor"].step(ga)
+        flat = lambda gs: torch.cat([x.reshape(-1) for x in gs]).numpy()  # noqa: E731
+        self.last = {"y": y, "grads": {"critic": flat(gq), "actor": flat(ga)}}
         with torch.no_grad():
             for c, tg in (("critic", "critic_targ"), ("actor", "actor_targ")):
                 for n in P[c]:

@@ -18,6 +18,7 @@
 #include "ppo.hip"
 #include "replay.hip"
 #include "sac.hip"
+#include "ddpg.hip"
 
 namespace spp {
 
@@ -400,23 +401,46 @@ struct KernelSet {
   void (*actor)(SacArgs, AcmScratch);
   void (*act)(SacArgs, ActArgs);
   void (*acmreg)(SacArgs, AcmRegArgs);
+  // DDPG_AcM
+  void (*dcritic)(SacArgs, BAcmScratch);
+  void (*dactor)(SacArgs, BAcmScratch);
+  void (*dact)(SacArgs, ActArgs, BAcmScratch);
+  void (*dreg)(SacArgs, BAcmRegArgs);
 };
 template <int OB, int AOUT, int AC, bool ACMC>
 KernelSet make_kset() {
   using C = Cfg<OB, AOUT, AC, ACMC>;
-  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>};
+  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>,
+          nullptr, nullptr, nullptr, nullptr};
 }
-static bool find_kset(int ob, int aout, int ac, bool acmc, KernelSet* ks) {
+template <int OB, int AOUT, int AC, bool ACMC>
+KernelSet make_dkset() {
+  using D = DCfg<OB, AOUT, AC, ACMC>;
+  return {nullptr, nullptr, nullptr, nullptr,
+          k_ddpg_critic_phase<D>, k_ddpg_actor_phase<D>, k_ddpg_policy_act<D>, k_bacm_regress<D>};
+}
+static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, KernelSet* ks) {
 #define SPP_KS(o, a, c)                                                    \
   if (ob == o && aout == a && ac == c) {                                   \
     *ks = acmc ? make_kset<o, a, c, true>() : make_kset<o, a, c, false>(); \
     return true;                                                           \
   }
-  SPP_KS(11, 11, 3)   // Hopper-v2
-  SPP_KS(17, 17, 6)   // HalfCheetah-v2
-  SPP_KS(111, 111, 8) // Ant
-  SPP_KS(3, 3, 1)     // Pendulum-v0 (tests)
+#define SPP_DKS(o, a, c)                                                     \
+  if (ob == o && aout == a && ac == c) {                                     \
+    *ks = acmc ? make_dkset<o, a, c, true>() : make_dkset<o, a, c, false>(); \
+    return true;                                                             \
+  }
+  if (algo == SPP_ALGO_SAC_ACM) {
+    SPP_KS(11, 11, 3)   // Hopper-v2
+    SPP_KS(17, 17, 6)   // HalfCheetah-v2
+    SPP_KS(111, 111, 8) // Ant
+    SPP_KS(3, 3, 1)     // Pendulum-v0 (tests)
+  } else if (algo == SPP_ALGO_DDPG_ACM) {
+    SPP_DKS(17, 17, 6)  // HalfCheetah-v2 (SPP-DDPG, train/spp_ddpg_hcheetah.py)
+    SPP_DKS(11, 11, 3)  // Hopper-v2
+  }
 #undef SPP_KS
+#undef SPP_DKS
   return false;
 }
 
@@ -437,6 +461,7 @@ struct sppAgent {
   // packed images
   DevArray<float4> pk;     // all matrix images
   std::vector<PackJob> pj_actor, pj_acm, pj_targ, pj_critic_fwd, pj_critic_all, pj_acmreg;
+  bool ddpg = false;
   DevArray<PackJob> d_pj;
   // job-table offsets inside d_pj
   int o_actor = 0, o_acm = 0, o_targ = 0, o_cfwd = 0, o_call = 0, o_acmreg = 0;
@@ -446,6 +471,12 @@ struct sppAgent {
   CriticDev critic[2]{}, targ[2]{};
   AcmDev acm{};
   const float4* acm_W1n = nullptr;  // ACM W1 natural input packing (regression)
+  // DDPG_AcM
+  BAcmDev bacm{};
+  ActorDev actor_targ{};
+  const float4 *bacm_W1n = nullptr, *bacm_W21n = nullptr;  // natural-input packings (regression)
+  BAcmScratch bz{};  // agent-phase BasicAcM activations
+  float *RBH = nullptr, *RBH1 = nullptr, *RS21 = nullptr, *RBP1 = nullptr, *RPZ = nullptr, *RPZ21 = nullptr;
   // scratch
   DevArray<float> scratch;
   float *S = nullptr, *S2 = nullptr, *ACT = nullptr, *AENV = nullptr, *R = nullptr, *DN = nullptr, *EPS1 = nullptr,
@@ -490,6 +521,11 @@ namespace spp {
 static int64_t sac_actor_size(int ob, int aout) { return 256LL * ob + 256 + 65536 + 256 + 2LL * (aout * 256 + aout); }
 static int64_t critic_size(int cin) { return 256LL * cin + 256 + 65536 + 256 + 256 + 1; }
 static int64_t acm_size(int in, int ac) { return 64LL * in + 64 + 32 * 64 + 32 + (int64_t)ac * 32 + ac; }
+static int64_t ddpg_actor_size(int ob, int aout) { return 256LL * ob + 256 + 65536 + 256 + (int64_t)aout * 256 + aout; }
+// BasicAcM state_dict: t, t1, fc1, fc2, fc21, fc3 (basic_acm.py:11-21)
+static int64_t bacm_size(int in, int ac) {
+  return 1 + ac + 100LL * in + 100 + 50 * 100 + 50 + 50LL * in + 50 + (int64_t)ac * 50 + ac;
+}
 
 static MapDesc nat(int n) { return MapDesc{MAP_NAT, n, 0, 0, 0}; }
 static MapDesc cat(int n0, int n1) { return MapDesc{MAP_CAT, n0, blocks_of(n0), n1, n0}; }
@@ -502,8 +538,12 @@ static sppStatus build_packs(sppAgent* a) {
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
   const int ca = a->cfg.acm_critic ? ac : aout;
   const int cin = ob + ca;
-  for (int k = 0; k < SPP_NET_COUNT; ++k)
-    SPP_REQUIRE(a->net[k].p, SPP_E_STATE, "network %d parameters not bound", k);
+  for (int k = 0; k < SPP_NET_COUNT; ++k) {
+    const bool used = a->ddpg ? (k == SPP_NET_ACTOR || k == SPP_NET_CRITIC1 || k == SPP_NET_CRITIC1_TARG ||
+                                 k == SPP_NET_ACM || k == SPP_NET_ACTOR_TARG)
+                              : k != SPP_NET_ACTOR_TARG;
+    SPP_REQUIRE(!used || a->net[k].p, SPP_E_STATE, "network %d parameters not bound", k);
+  }
   // sizes: count float4 and vector slots first
   struct MatSpec {
     std::vector<PackJob>* list;
@@ -527,39 +567,87 @@ static sppStatus build_packs(sppAgent* a) {
     toff += tot;
     return off;
   };
-  // ---- actor (sac/models.py:12-22): fc1 [256][ob], fc2, fc_prob [aout][256], fc_scale
-  {
-    const float* P = a->net[SPP_NET_ACTOR].p;
-    const float *W1 = P, *b1 = W1 + 256 * ob, *W2 = b1 + 256, *b2 = W2 + 65536, *Wp = b2 + 256, *bp = Wp + aout * 256,
-                *Ws = bp + aout, *bs = Ws + aout * 256;
-    M(&a->pj_actor, W1, nullptr, 1 << 30, ob, 0, 0, nat(256), nat(ob), 8, blocks_of(ob), &a->actor.W1);
-    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &a->actor.W2, 1);
-    M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh, 1);
-    M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T, 1);
-    M(&a->pj_actor, Wp, Ws, aout, 256, 1, 0, nat(256), pair(aout), 8, (aout + 15) / 16, &a->actor.WhT);
-    a->actor.tb1 = T(b1, 256);
-    a->actor.tb2 = T(b2, 256);
-    a->actor.tbh = T(bp, aout, bs, aout);
+  if (!a->ddpg) {
+    // ---- actor (sac/models.py:12-22): fc1 [256][ob], fc2, fc_prob [aout][256], fc_scale
+    {
+      const float* P = a->net[SPP_NET_ACTOR].p;
+      const float *W1 = P, *b1 = W1 + 256 * ob, *W2 = b1 + 256, *b2 = W2 + 65536, *Wp = b2 + 256, *bp = Wp + aout * 256,
+                  *Ws = bp + aout, *bs = Ws + aout * 256;
+      M(&a->pj_actor, W1, nullptr, 1 << 30, ob, 0, 0, nat(256), nat(ob), 8, blocks_of(ob), &a->actor.W1);
+      M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &a->actor.W2, 1);
+      M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh, 1);
+      M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T, 1);
+      M(&a->pj_actor, Wp, Ws, aout, 256, 1, 0, nat(256), pair(aout), 8, (aout + 15) / 16, &a->actor.WhT);
+      a->actor.tb1 = T(b1, 256);
+      a->actor.tb2 = T(b2, 256);
+      a->actor.tbh = T(bp, aout, bs, aout);
+    }
+  } else {
+    // ---- DDPG actor and its target (ddpg/models.py:5-22): fc1 [256][ob], fc2, fc3 [aout][256]
+    for (int t = 0; t < 2; ++t) {
+      const float* P = a->net[t == 0 ? SPP_NET_ACTOR : SPP_NET_ACTOR_TARG].p;
+      ActorDev& ad = t == 0 ? a->actor : a->actor_targ;
+      std::vector<PackJob>* l = t == 0 ? &a->pj_actor : &a->pj_targ;
+      const float *W1 = P, *b1 = W1 + 256 * ob, *W2 = b1 + 256, *b2 = W2 + 65536, *W3 = b2 + 256, *b3 = W3 + aout * 256;
+      M(l, W1, nullptr, 1 << 30, ob, 0, 0, nat(256), nat(ob), 8, blocks_of(ob), &ad.W1);
+      M(l, W2, nullptr, 1 << 30, 256, 0, 0, nat(256), nat(256), 8, 8, &ad.W2, 1);
+      M(l, W3, nullptr, 1 << 30, 256, 0, 0, nat(aout), nat(256), blocks_of(aout), 8, &ad.Wh, 1);
+      if (t == 0) {
+        M(l, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &ad.W2T, 1);
+        M(l, W3, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(aout), 8, blocks_of(aout), &ad.WhT);
+      }
+      ad.tb1 = T(b1, 256);
+      ad.tb2 = T(b2, 256);
+      ad.tbh = T(b3, aout);
+    }
   }
-  // ---- ACM (basic_model.py:108-117): fc1 [64][2ob], fc2 [32][64], fc3 [ac][32]
-  {
+  if (!a->ddpg) {
+    // ---- ACM (basic_model.py:108-117): fc1 [64][2ob], fc2 [32][64], fc3 [ac][32]
+    {
+      const float* P = a->net[SPP_NET_ACM].p;
+      const int in = 2 * ob;
+      const float *W1 = P, *b1 = W1 + 64 * in, *W2 = b1 + 64, *b2 = W2 + 32 * 64, *W3 = b2 + 32, *b3 = W3 + ac * 32;
+      M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), cat(ob, aout), 2, blocks_of(ob) + blocks_of(aout),
+        &a->acm.W1);
+      M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 0, 0, nat(32), nat(64), 1, 2, &a->acm.W2);
+      M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 0, 0, nat(ac), nat(32), 1, 1, &a->acm.W3);
+      M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 1, 0, nat(32), nat(ac), 1, 1, &a->acm.W3T);
+      M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 1, 0, nat(64), nat(32), 2, 1, &a->acm.W2T);
+      M(&a->pj_acm, W1, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(64), blocks_of(aout), 2, &a->acm.W1Ta);
+      M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), nat(in), 2, blocks_of(in), &a->acm_W1n);
+      a->acm.tb1 = T(b1, 64);
+      a->acm.tb2 = T(b2, 32);
+      a->acm.tb3 = T(b3, ac);
+    }
+  } else {
+    // ---- BasicAcM (acm/models/basic_acm.py:11-21): t, t1, fc1 [100][2ob], fc2 [50][100],
+    //      fc21 [50][2ob], fc3 [ac][50]
     const float* P = a->net[SPP_NET_ACM].p;
     const int in = 2 * ob;
-    const float *W1 = P, *b1 = W1 + 64 * in, *W2 = b1 + 64, *b2 = W2 + 32 * 64, *W3 = b2 + 32, *b3 = W3 + ac * 32;
-    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), cat(ob, aout), 2, blocks_of(ob) + blocks_of(aout),
-      &a->acm.W1);
-    M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 0, 0, nat(32), nat(64), 1, 2, &a->acm.W2);
-    M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 0, 0, nat(ac), nat(32), 1, 1, &a->acm.W3);
-    M(&a->pj_acm, W3, nullptr, 1 << 30, 32, 1, 0, nat(32), nat(ac), 1, 1, &a->acm.W3T);
-    M(&a->pj_acm, W2, nullptr, 1 << 30, 64, 1, 0, nat(64), nat(32), 2, 1, &a->acm.W2T);
-    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(64), blocks_of(aout), 2, &a->acm.W1Ta);
-    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(64), nat(in), 2, blocks_of(in), &a->acm_W1n);
-    a->acm.tb1 = T(b1, 64);
-    a->acm.tb2 = T(b2, 32);
-    a->acm.tb3 = T(b3, ac);
+    const float *t = P, *t1 = P + 1, *W1 = t1 + ac, *b1 = W1 + 100 * in, *W2 = b1 + 100, *b2 = W2 + 50 * 100,
+                *W21 = b2 + 50, *b21 = W21 + 50 * in, *W3 = b21 + 50, *b3 = W3 + ac * 50;
+    BAcmDev& B = a->bacm;
+    const int nbi = blocks_of(ob) + blocks_of(aout);
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(100), cat(ob, aout), 4, nbi, &B.W1);
+    M(&a->pj_acm, W21, nullptr, 1 << 30, in, 0, 0, nat(50), cat(ob, aout), 2, nbi, &B.W21);
+    M(&a->pj_acm, W2, nullptr, 1 << 30, 100, 0, 0, nat(50), nat(100), 2, 4, &B.W2);
+    M(&a->pj_acm, W3, nullptr, 1 << 30, 50, 0, 0, nat(ac), nat(50), 1, 2, &B.W3);
+    M(&a->pj_acm, W3, nullptr, 1 << 30, 50, 1, 0, nat(50), nat(ac), 2, 1, &B.W3T);
+    M(&a->pj_acm, W2, nullptr, 1 << 30, 100, 1, 0, nat(100), nat(50), 4, 2, &B.W2T);
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(100), blocks_of(aout), 4, &B.W1Ta);
+    M(&a->pj_acm, W21, nullptr, 1 << 30, in, 1, ob, nat(aout), nat(50), blocks_of(aout), 2, &B.W21Ta);
+    M(&a->pj_acm, W1, nullptr, 1 << 30, in, 0, 0, nat(100), nat(in), 4, blocks_of(in), &a->bacm_W1n);
+    M(&a->pj_acm, W21, nullptr, 1 << 30, in, 0, 0, nat(50), nat(in), 2, blocks_of(in), &a->bacm_W21n);
+    B.tb1 = T(b1, 100);
+    B.tb21 = T(b21, 50);
+    B.tb2 = T(b2, 50);
+    B.tb3 = T(b3, ac);
+    B.t = t;
+    B.t1 = t1;
   }
   // ---- critics and targets (sac/models.py:75-91): fc1 [256][cin], fc2, fc3 [1][256]
   for (int t = 0; t < 4; ++t) {
+    if (a->ddpg && (t == 1 || t == 3)) continue;  // DDPG: one critic and its target
     const int netid = t < 2 ? SPP_NET_CRITIC1 + t : SPP_NET_CRITIC1_TARG + (t - 2);
     CriticDev& cd = t < 2 ? a->critic[t] : a->targ[t - 2];
     const float* P = a->net[netid].p;
@@ -646,7 +734,42 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
   };
   sppAgent::DwSet& D = a->dws[set];
   int nph = 0;
-  if (set == 0) {
+  if (a->ddpg) {
+    if (set == 0) {
+      // critic phase (ddpg_acm.py:174-185): fc1 (delta1 x [s|a]), fc2 (delta2 x h1), fc3 (dq x h2)
+      float* G = a->net[SPP_NET_CRITIC1].g;
+      float *gW1 = G, *gb1 = gW1 + 256 * cin, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gw3 = gb2 + 256, *gb3 = gw3 + 256;
+      J(a->D1[0], 256, a->S, ob, a->cfg.acm_critic ? a->AENV : a->ACT, ca, gW1, gb1);
+      J(a->D2[0], 256, a->H1[0], 256, nullptr, 0, gW2, gb2);
+      J(a->DQ[0], 1, a->H2[0], 256, nullptr, 0, gw3, gb3);
+      D.j0[0] = 0;
+      D.nj[0] = (int)jobs.size();
+      // actor phase (:187-196): fc1 (delta1 x s), fc2 (delta2 x h1), fc3 (dhead x h2)
+      float* A = a->net[SPP_NET_ACTOR].g;
+      float *aW1 = A, *ab1 = aW1 + 256 * ob, *aW2 = ab1 + 256, *ab2 = aW2 + 65536, *aW3 = ab2 + 256,
+            *ab3 = aW3 + aout * 256;
+      J(a->AD1, 256, a->S, ob, nullptr, 0, aW1, ab1);
+      J(a->AD2, 256, a->AH1, 256, nullptr, 0, aW2, ab2);
+      J(a->ADH, aout, a->AH2, 256, nullptr, 0, aW3, ab3);
+      D.j0[1] = D.nj[0];
+      D.nj[1] = (int)jobs.size() - D.nj[0];
+      nph = 2;
+    } else {
+      // BasicAcM regression (acm.py:246-258): fc1, fc2, fc21 (grad of its output = t * dz), fc3;
+      // t / t1 come from the per-tile partials (k_finalize_bacm)
+      float* G = a->net[SPP_NET_ACM].g;
+      const int in = 2 * ob;
+      float *gW1 = G + 1 + ac, *gb1 = gW1 + 100 * in, *gW2 = gb1 + 100, *gb2 = gW2 + 50 * 100, *gW21 = gb2 + 50,
+            *gb21 = gW21 + 50 * in, *gW3 = gb21 + 50, *gb3 = gW3 + ac * 50;
+      J(a->RBP1, 100, a->RX, in, nullptr, 0, gW1, gb1);
+      J(a->RPZ, 50, a->RBH, 100, nullptr, 0, gW2, gb2);
+      J(a->RPZ21, 50, a->RX, in, nullptr, 0, gW21, gb21);
+      J(a->RP3, ac, a->RBH1, 50, nullptr, 0, gW3, gb3);
+      D.j0[0] = 0;
+      D.nj[0] = (int)jobs.size();
+      nph = 1;
+    }
+  } else if (set == 0) {
     // critic phase: fc1 (delta1 x [s|a]), fc2 (delta2 x h1), fc3 (dq x h2)  per critic
     for (int i = 0; i < 2; ++i) {
       float* G = a->net[SPP_NET_CRITIC1 + i].g;
@@ -741,14 +864,15 @@ static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) {
 }
 
 // Adam job table [critic1, critic2 (+polyak targets) | actor | acm]; pointers only.
+// DDPG_AcM: [critic (+polyak) | - | actor (+polyak of the target actor, ddpg.py:273-284) | acm].
 static sppStatus build_adam(sppAgent* a) {
-  AdamJob jobs[4];
-  for (int i = 0; i < 2; ++i) {
+  AdamJob jobs[4] = {};
+  for (int i = 0; i < (a->ddpg ? 1 : 2); ++i) {
     NetBufs& n = a->net[SPP_NET_CRITIC1 + i];
     jobs[i] = AdamJob{n.p, n.g, n.m, n.v, a->net[SPP_NET_CRITIC1_TARG + i].p, n.n};
   }
   NetBufs& na = a->net[SPP_NET_ACTOR];
-  jobs[2] = AdamJob{na.p, na.g, na.m, na.v, nullptr, na.n};
+  jobs[2] = AdamJob{na.p, na.g, na.m, na.v, a->ddpg ? a->net[SPP_NET_ACTOR_TARG].p : nullptr, na.n};
   NetBufs& nm = a->net[SPP_NET_ACM];
   jobs[3] = AdamJob{nm.p, nm.g, nm.m, nm.v, nullptr, nm.n};
   if (!a->d_adam.ptr) SPP_CHECK_HIP(a->d_adam.alloc(4));
@@ -785,6 +909,8 @@ static SacArgs make_args(sppAgent* a, int B) {
     p.H1[i] = a->H1[i]; p.H2[i] = a->H2[i]; p.D1[i] = a->D1[i]; p.D2[i] = a->D2[i]; p.DQ[i] = a->DQ[i];
   }
   p.acm = a->acm;
+  p.bacm = a->bacm;
+  p.actor_targ = a->actor_targ;
   p.AH1 = a->AH1; p.AH2 = a->AH2; p.AD1 = a->AD1; p.AD2 = a->AD2; p.ADH = a->ADH;
   p.part = a->part;
   p.nseg = (int)a->tab.size();
@@ -798,7 +924,7 @@ static int phase_grid(sppAgent* a, int Bp) {
 }
 
 static sppStatus check_ready(sppAgent* a) {
-  SPP_REQUIRE(a->alpha_state && a->alpha_f32, SPP_E_STATE, "alpha not bound");
+  SPP_REQUIRE(a->ddpg || (a->alpha_state && a->alpha_f32), SPP_E_STATE, "alpha not bound");
   SPP_REQUIRE(a->cfg.min_max_denormalize ? (a->lo && a->hi) : (a->mean && a->std), SPP_E_STATE,
               "normalizer not bound");
   SPP_REQUIRE(a->limits.ptr, SPP_E_STATE, "limits not set");
@@ -815,11 +941,12 @@ extern "C" {
 
 sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int device) {
   SPP_REQUIRE(out && cfg, SPP_E_INVALID_ARG, "null arg");
-  SPP_REQUIRE(cfg->algo == SPP_ALGO_SAC_ACM, SPP_E_INVALID_ARG, "unsupported algo %d", cfg->algo);
+  SPP_REQUIRE(cfg->algo == SPP_ALGO_SAC_ACM || cfg->algo == SPP_ALGO_DDPG_ACM, SPP_E_INVALID_ARG,
+              "unsupported algo %d", cfg->algo);
   SPP_REQUIRE(cfg->max_batch > 0, SPP_E_INVALID_ARG, "max_batch must be > 0");
   KernelSet ks;
-  SPP_REQUIRE(find_kset(cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, &ks), SPP_E_SHAPE,
-              "no kernel instantiation for (ob=%d, aout=%d, ac=%d)", cfg->ob, cfg->aout, cfg->ac);
+  SPP_REQUIRE(find_kset(cfg->algo, cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, &ks), SPP_E_SHAPE,
+              "no kernel instantiation for algo %d (ob=%d, aout=%d, ac=%d)", cfg->algo, cfg->ob, cfg->aout, cfg->ac);
   SPP_CHECK_HIP(hipSetDevice(device));
   auto a = std::make_unique<sppAgent>();
   a->cfg = *cfg;
@@ -830,10 +957,13 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   a->num_cu = prop.multiProcessorCount;
   const int ob = cfg->ob, aout = cfg->aout, ac = cfg->ac;
   a->cin = ob + (cfg->acm_critic ? ac : aout);
-  a->nsize[SPP_NET_ACTOR] = sac_actor_size(ob, aout);
-  a->nsize[SPP_NET_CRITIC1] = a->nsize[SPP_NET_CRITIC2] = critic_size(a->cin);
-  a->nsize[SPP_NET_CRITIC1_TARG] = a->nsize[SPP_NET_CRITIC2_TARG] = critic_size(a->cin);
-  a->nsize[SPP_NET_ACM] = acm_size(2 * ob, ac);
+  a->ddpg = cfg->algo == SPP_ALGO_DDPG_ACM;
+  const bool dd = a->ddpg;
+  a->nsize[SPP_NET_ACTOR] = dd ? ddpg_actor_size(ob, aout) : sac_actor_size(ob, aout);
+  a->nsize[SPP_NET_ACTOR_TARG] = dd ? ddpg_actor_size(ob, aout) : 0;
+  a->nsize[SPP_NET_CRITIC1] = a->nsize[SPP_NET_CRITIC1_TARG] = critic_size(a->cin);
+  a->nsize[SPP_NET_CRITIC2] = a->nsize[SPP_NET_CRITIC2_TARG] = dd ? 0 : critic_size(a->cin);
+  a->nsize[SPP_NET_ACM] = dd ? bacm_size(2 * ob, ac) : acm_size(2 * ob, ac);
   a->Bmax = cfg->max_batch;
   const int64_t Bp = round_up(cfg->max_batch, 32);
   SPP_REQUIRE((int64_t)Bp * 256 * 4 < ((int64_t)1 << 31), SPP_E_SHAPE, "max_batch %d too large (31-bit buffer offsets)",
@@ -846,16 +976,18 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   auto take = [&](int64_t rows) { int64_t o = total; total += rows * per; return o; };
   const int64_t oS = take(ob), oS2 = take(ob), oACT = take(aout), oAENV = take(ac), oR = take(1), oDN = take(1),
                 oE1 = take(aout), oE2 = take(aout);
-  int64_t oH1[2], oH2[2], oD1[2], oD2[2], oDQ[2];
-  for (int i = 0; i < 2; ++i) {
+  int64_t oH1[2] = {}, oH2[2] = {}, oD1[2] = {}, oD2[2] = {}, oDQ[2] = {};
+  for (int i = 0; i < (dd ? 1 : 2); ++i) {
     oH1[i] = take(256); oH2[i] = take(256); oD1[i] = take(256); oD2[i] = take(256); oDQ[i] = take(1);
   }
-  const int64_t oAH1 = take(256), oAH2 = take(256), oAD1 = take(256), oAD2 = take(256), oADH = take(2 * aout),
-                oZ1 = take(64), oZ2 = take(32), oT3 = take(ac);
-  const int64_t oRX = take(2 * ob), oRZ1 = take(64), oRZ2 = take(32), oRP1 = take(64), oRP2 = take(32),
-                oRP3 = take(ac);
+  const int64_t oAH1 = take(256), oAH2 = take(256), oAD1 = take(256), oAD2 = take(256), oADH = take(2 * aout);
+  // ACM activations kept for its backward: AcM z1 [64], z2 [32], t3 [ac]; BasicAcM h [128], h1 [64], r3 [ac]
+  const int64_t oZ1 = take(dd ? 128 : 64), oZ2 = take(dd ? 64 : 32), oT3 = take(ac);
+  const int64_t oRX = take(2 * ob), oRZ1 = take(dd ? 128 : 64), oRZ2 = take(dd ? 64 : 32), oRP1 = take(dd ? 128 : 64),
+                oRP2 = take(dd ? 64 : 32), oRP3 = take(ac);
+  const int64_t oRS21 = dd ? take(64) : 0, oRPZ21 = dd ? take(64) : 0;
   const int64_t oPart = total;
-  total += ntiles * kParts + 64;
+  total += ntiles * kBParts + 64;
   const int64_t oAux = total;
   total += 16;
   hipError_t e = a->scratch.alloc(total);
@@ -873,6 +1005,11 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   a->AH1 = b + oAH1; a->AH2 = b + oAH2; a->AD1 = b + oAD1; a->AD2 = b + oAD2; a->ADH = b + oADH;
   a->Z1 = b + oZ1; a->Z2 = b + oZ2; a->T3 = b + oT3;
   a->RX = b + oRX; a->RZ1 = b + oRZ1; a->RZ2 = b + oRZ2; a->RP1 = b + oRP1; a->RP2 = b + oRP2; a->RP3 = b + oRP3;
+  if (dd) {
+    a->bz = BAcmScratch{a->Z1, a->Z2, a->T3};
+    a->RBH = a->RZ1; a->RBH1 = a->RZ2; a->RBP1 = a->RP1; a->RPZ = a->RP2;
+    a->RS21 = b + oRS21; a->RPZ21 = b + oRPZ21;
+  }
   a->part = b + oPart;
   a->aux = b + oAux;
   SPP_CHECK_HIP(a->limits.alloc(aout + ac));
@@ -963,6 +1100,7 @@ static sppStatus stage(sppAgentHandle a, const sppBatch* bt, const float* e1, co
 }
 
 static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_t st) {
+  SPP_REQUIRE(!a->ddpg, SPP_E_STATE, "not a SAC_AcM agent");
   const int B = a->cur_B;
   SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
   sppStatus s = check_ready(a);
@@ -1014,6 +1152,7 @@ sppStatus sppSacAcmCriticApply(sppAgentHandle a, void* stream) {
 }
 
 static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
+  SPP_REQUIRE(!a->ddpg, SPP_E_STATE, "not a SAC_AcM agent");
   const int B = a->cur_B;
   SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
   // repack the updated critics
@@ -1106,6 +1245,7 @@ sppStatus sppSacAcmActorApply(sppAgentHandle a, float* losses, void* stream) {
 
 sppStatus sppSacAcmUpdate(sppAgentHandle a, const sppBatch* bt, const float* eps_next, const float* eps_cur,
                           float* losses, void* stream) {
+  SPP_REQUIRE(a && !a->ddpg, SPP_E_STATE, "not a SAC_AcM agent");
   SPP_REQUIRE(a && eps_next && eps_cur, SPP_E_INVALID_ARG, "eps required (use sppSacAcmUpdateStaged for device draws)");
   hipStream_t st = S(stream);
   sppStatus s = stage(a, bt, eps_next, eps_cur, st);
@@ -1114,6 +1254,80 @@ sppStatus sppSacAcmUpdate(sppAgentHandle a, const sppBatch* bt, const float* eps
   if ((s = sppSacAcmCriticApply(a, stream))) return s;
   if ((s = actor_grads(a, losses, st))) return s;
   return actor_apply(a, losses, st);
+}
+
+// ------------------------------------------------------------------ DDPG_AcM (ddpg_acm.py:147-201)
+sppStatus sppDdpgAcmCriticGrads(sppAgentHandle a, const sppBatch* bt, float* losses, void* stream) {
+  SPP_REQUIRE(a && a->ddpg, SPP_E_STATE, "not a DDPG_AcM agent");
+  hipStream_t st = S(stream);
+  sppStatus s;
+  if (bt && (s = stage(a, bt, nullptr, nullptr, st))) return s;
+  const int B = a->cur_B;
+  SPP_REQUIRE(B > 0, SPP_E_STATE, "no staged batch");
+  if ((s = check_ready(a))) return s;
+  if (a->dws[0].B != B && (s = build_dw(a, 0, B))) return s;
+  launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size() + a->pj_targ.size() + a->pj_critic_fwd.size()),
+              st);
+  SacArgs p = make_args(a, B);
+  tmark(a, 0, st);
+  hipLaunchKernelGGL(a->ks.dcritic, dim3(phase_grid(a, p.Bp)), dim3(256), 0, st, p, a->bz);
+  tmark(a, 0, st);
+  SPP_CHECK_HIP(hipGetLastError());
+  tmark(a, 2, st);
+  launch_dw(a, 0, 0, st);
+  tmark(a, 2, st);
+  hipLaunchKernelGGL(k_finalize_ddpg_critic, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppDdpgAcmCriticApply(sppAgentHandle a, void* stream) {
+  SPP_REQUIRE(a && a->ddpg && a->d_adam.ptr, SPP_E_STATE, "DDPG_AcM agent not ready");
+  a->steps[1] += 1;
+  tmark(a, 3, S(stream));
+  launch_adam(a, 0, 1, a->net[SPP_NET_CRITIC1].n, a->steps[1], a->cfg.critic_lr, a->cfg.tau, S(stream));
+  tmark(a, 3, S(stream));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppDdpgAcmActorGrads(sppAgentHandle a, float* losses, void* stream) {
+  SPP_REQUIRE(a && a->ddpg && a->cur_B > 0, SPP_E_STATE, "DDPG_AcM agent: no staged batch");
+  hipStream_t st = S(stream);
+  const int B = a->cur_B;
+  launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), st);  // the updated critic
+  SacArgs p = make_args(a, B);
+  tmark(a, 1, st);
+  hipLaunchKernelGGL(a->ks.dactor, dim3(phase_grid(a, p.Bp)), dim3(256), 0, st, p, a->bz);
+  tmark(a, 1, st);
+  SPP_CHECK_HIP(hipGetLastError());
+  tmark(a, 2, st);
+  launch_dw(a, 0, 1, st);
+  tmark(a, 2, st);
+  hipLaunchKernelGGL(k_finalize_ddpg_actor, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B,
+                     a->cfg.aout, a->cfg.custom_loss, losses);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// actor Adam step, then polyak of the critic target (already fused into the critic
+// step: the critic does not change afterwards) and of the actor target (ddpg.py:273-284)
+sppStatus sppDdpgAcmActorApply(sppAgentHandle a, void* stream) {
+  SPP_REQUIRE(a && a->ddpg && a->d_adam.ptr, SPP_E_STATE, "DDPG_AcM agent not ready");
+  a->steps[0] += 1;
+  tmark(a, 3, S(stream));
+  launch_adam(a, 2, 1, a->net[SPP_NET_ACTOR].n, a->steps[0], a->cfg.actor_lr, a->cfg.tau, S(stream));
+  tmark(a, 3, S(stream));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppDdpgAcmUpdate(sppAgentHandle a, const sppBatch* bt, float* losses, void* stream) {
+  sppStatus s;
+  if ((s = sppDdpgAcmCriticGrads(a, bt, losses, stream))) return s;
+  if ((s = sppDdpgAcmCriticApply(a, stream))) return s;
+  if ((s = sppDdpgAcmActorGrads(a, losses, stream))) return s;
+  return sppDdpgAcmActorApply(a, stream);
 }
 
 sppStatus sppAgentStageFromReplay(sppAgentHandle a, sppReplayHandle r, const int64_t* idx, int B, void* stream) {
@@ -1149,6 +1363,23 @@ sppStatus sppAcmRegressGrads(sppAgentHandle a, const float* x, const float* y, i
   }
   launch_pack(a, a->o_acm, (int)a->pj_acm.size(), st);
   SacArgs p = make_args(a, B);
+  if (a->ddpg) {  // BasicAcM: natural-input fc1 / fc21 packings
+    p.bacm.W1 = a->bacm_W1n;
+    p.bacm.W21 = a->bacm_W21n;
+    BAcmRegArgs g{};
+    g.B = B; g.Bp = (int)round_up(B, 32); g.x = x; g.y = y;
+    g.XT = a->RX; g.H = a->RBH; g.H1 = a->RBH1; g.S21 = a->RS21; g.P1 = a->RBP1; g.PZ = a->RPZ; g.PZ21 = a->RPZ21;
+    g.P3 = a->RP3; g.part = a->part;
+    tmark(a, 4, st);
+    hipLaunchKernelGGL(a->ks.dreg, dim3(phase_grid(a, g.Bp)), dim3(256), 0, st, p, g);
+    SPP_CHECK_HIP(hipGetLastError());
+    launch_dw(a, 1, 0, st);
+    tmark(a, 4, st);
+    hipLaunchKernelGGL(k_finalize_bacm, dim3(1), dim3(256), 0, st, (const float*)a->part, g.Bp / 32, kBParts, B,
+                       a->cfg.ac, a->net[SPP_NET_ACM].g, loss);
+    SPP_CHECK_HIP(hipGetLastError());
+    return SPP_OK;
+  }
   p.acm.W1 = a->acm_W1n;
   AcmRegArgs g{};
   g.B = B; g.Bp = (int)round_up(B, 32); g.x = x; g.y = y;
@@ -1196,7 +1427,10 @@ sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* e
   SacArgs p = make_args(a, 32);
   ActArgs g{E, mode, denorm_out, act_noise, obs, eps, noise, target_out, env_out};
   const int grid = std::max(1, std::min(cdiv(cdiv(E, 32), kWavesPerWG), a->num_cu));
-  hipLaunchKernelGGL(a->ks.act, dim3(grid), dim3(256), 0, st, p, g);
+  if (a->ddpg)
+    hipLaunchKernelGGL(a->ks.dact, dim3(grid), dim3(256), 0, st, p, g, a->bz);
+  else
+    hipLaunchKernelGGL(a->ks.act, dim3(grid), dim3(256), 0, st, p, g);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

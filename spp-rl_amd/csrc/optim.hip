@@ -133,4 +133,35 @@ __global__ void k_finalize_acm(const float* part, int ntiles, int B, int ac, flo
   if (threadIdx.x == 0 && loss) *loss = (float)(s / ((double)B * ac));
 }
 
+// DDPG_AcM losses {critic, actor, ddpg, dist} (ddpg_acm.py:133-143, :181)
+__global__ void k_finalize_ddpg_critic(const float* part, int ntiles, int B, float* losses) {
+  const double l0 = block_sum(part, ntiles, 8, 0);
+  if (threadIdx.x == 0 && losses) losses[0] = (float)(l0 / B);
+}
+__global__ void k_finalize_ddpg_actor(const float* part, int ntiles, int B, int aout, float custom_loss,
+                                      float* losses) {
+  const double sq = block_sum(part, ntiles, 8, 2);
+  const double sd = block_sum(part, ntiles, 8, 3);
+  if (threadIdx.x != 0 || !losses) return;
+  const double ddpg = sq / B, dist = sd / ((double)B * aout);
+  losses[1] = (float)(custom_loss != 0.f ? ddpg + (double)custom_loss * dist : ddpg);
+  losses[2] = custom_loss != 0.f ? (float)ddpg : 0.f;
+  losses[3] = custom_loss != 0.f ? (float)dist : 0.f;
+}
+
+// BasicAcM regression: loss, and the gradients of its scale parameters t, t1
+// (grad buffer slots 0 and 1..ac, state_dict order) from the per-tile partials.
+__global__ void k_finalize_bacm(const float* part, int ntiles, int stride, int B, int ac, float* grad, float* loss) {
+  const double s = block_sum(part, ntiles, stride, 0);
+  const double dt = block_sum(part, ntiles, stride, 1);
+  if (threadIdx.x == 0) {
+    if (loss) *loss = (float)(s / ((double)B * ac));
+    grad[0] = (float)dt;
+  }
+  for (int k = 0; k < ac; ++k) {
+    const double v = block_sum(part, ntiles, stride, 2 + k);
+    if (threadIdx.x == 0) grad[1 + k] = (float)v;
+  }
+}
+
 }  // namespace spp

@@ -172,9 +172,10 @@ __device__ __forceinline__ Lane make_lane(float* big, float* small, const float*
   return L;
 }
 
-// Actor trunk: x -> relu(L1) -> relu(L2) -> heads (mu | logsig) into LDS rows [0, 2*AOUT).
+// Actor trunk: x -> relu(L1) -> relu(L2) -> heads into LDS rows [0, NHR): SAC
+// (mu | logsig), NHR = 2*AOUT; DDPG fc3 pre-activation, NHR = AOUT (NBH blocks).
 // ST: store h1 / h2 feature-major (H1g, H2g).  Returns the ReLU masks.
-template <class C, bool ST>
+template <class C, bool ST, int NBH = C::NB_H2, int NHR = 2 * C::AOUT>
 __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, int xbytes, const Lane& L, float* H1g,
                                             float* H2g,
                                             uint64_t& m1lo, uint64_t& m1hi, uint64_t& m2lo, uint64_t& m2hi) {
@@ -211,11 +212,11 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
     });
   }
   {
-    dense_lds<C::NB_H2>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
+    dense_lds<NBH>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
-        if (ur + L.h4 < 2 * C::AOUT) L.bl[ur * 32] = acc[q];
+        if (ur + L.h4 < NHR) L.bl[ur * 32] = acc[q];
       }
     });
   }

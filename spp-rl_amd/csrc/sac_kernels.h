@@ -22,6 +22,14 @@ struct AcmDev {
   int tb1, tb2, tb3;
 };
 
+// BasicAcM (rltoolkit/acm/models/basic_acm.py:11-27): fc1 in->100, fc2 100->50,
+// fc21 in->50 (skip), fc3 50->ac; h1 = tanh(fc2(h) + t*fc21(x)); out = tanh(fc3(h1))*t1.
+struct BAcmDev {
+  const float4 *W1, *W21, *W2, *W3, *W3T, *W2T, *W1Ta, *W21Ta;
+  int tb1, tb21, tb2, tb3;
+  const float *t, *t1;  // canonical scalar / [ac] (frozen during the agent update)
+};
+
 // LDS table segment: tbl[off + i] = i < n ? src[i] : 0 for i < npad.
 struct TabSeg {
   const float* src;
@@ -47,6 +55,8 @@ struct SacArgs {
   ActorDev actor;
   CriticDev critic[2], targ[2];
   AcmDev acm;
+  BAcmDev bacm;       // DDPG_AcM's ACM
+  ActorDev actor_targ;  // DDPG target actor
   // critic-phase outputs (weight-gradient operands)
   float *H1[2], *H2[2], *D1[2], *D2[2], *DQ[2];
   // actor-phase outputs

@@ -8,5 +8,6 @@ from . import _lib, config, dp, nets, ppo  # noqa: F401
 from ._lib import SppError, load  # noqa: F401
 from .replay import BufferAcMOffPolicy  # noqa: F401
 from .sac_acm import SAC_AcM  # noqa: F401
+from .ddpg_acm import DDPG_AcM  # noqa: F401
 
-__all__ = ["SAC_AcM", "BufferAcMOffPolicy", "SppError", "load"]
+__all__ = ["SAC_AcM", "DDPG_AcM", "BufferAcMOffPolicy", "SppError", "load"]

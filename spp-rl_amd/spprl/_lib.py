@@ -13,8 +13,9 @@ import torch  # noqa: F401  (must precede the HIP library: shared runtime)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libspprl.so")
 
-SPP_NET_ACTOR, SPP_NET_CRITIC1, SPP_NET_CRITIC2, SPP_NET_CRITIC1_TARG, SPP_NET_CRITIC2_TARG, SPP_NET_ACM = range(6)
-SPP_ALGO_SAC_ACM = 1
+(SPP_NET_ACTOR, SPP_NET_CRITIC1, SPP_NET_CRITIC2, SPP_NET_CRITIC1_TARG, SPP_NET_CRITIC2_TARG, SPP_NET_ACM,
+ SPP_NET_ACTOR_TARG) = range(7)
+SPP_ALGO_SAC_ACM, SPP_ALGO_DDPG_ACM = 1, 2
 NUM_LOSSES = 8
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
@@ -90,6 +91,11 @@ _SIGS = {
     "sppAgentSetTiming": (c_int, [c_void_p, c_int]),
     "sppAgentGetTiming": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppSynthEnvStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sppDdpgAcmUpdate": (c_int, [c_void_p, P(Batch), c_void_p, c_void_p]),
+    "sppDdpgAcmCriticGrads": (c_int, [c_void_p, P(Batch), c_void_p, c_void_p]),
+    "sppDdpgAcmCriticApply": (c_int, [c_void_p, c_void_p]),
+    "sppDdpgAcmActorGrads": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "sppDdpgAcmActorApply": (c_int, [c_void_p, c_void_p]),
     "sppGaeScan": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, ctypes.c_double,
                            ctypes.c_double,
                             c_int, c_void_p, c_void_p, c_void_p]),

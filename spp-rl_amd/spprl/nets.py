@@ -6,6 +6,8 @@ addresses layers by these offsets.  Layouts follow the reference modules:
   SAC_Actor   rltoolkit/algorithms/sac/models.py:8-22   fc1, fc2, fc_prob, fc_scale
   SAC_Critic  rltoolkit/algorithms/sac/models.py:72-80  fc1, fc2, fc3
   AcM         rltoolkit/basic_model.py:108-117          fc1 (->64), fc2 (->32), fc3 (->ac)
+  DDPG Actor  rltoolkit/algorithms/ddpg/models.py:5-22  fc1, fc2, fc3 (->aout, tanh*lim)
+  BasicAcM    rltoolkit/acm/models/basic_acm.py:11-21   t, t1, fc1 (->100), fc2 (->50), fc21 (->50), fc3
 """
 import math
 
@@ -30,6 +32,18 @@ def acm_layout(inp, ac):
             ("fc3.weight", (ac, 32)), ("fc3.bias", (ac,))]
 
 
+def ddpg_actor_layout(ob, aout):
+    return [("fc1.weight", (H, ob)), ("fc1.bias", (H,)), ("fc2.weight", (H, H)), ("fc2.bias", (H,)),
+            ("fc3.weight", (aout, H)), ("fc3.bias", (aout,))]
+
+
+def basic_acm_layout(inp, ac):
+    # module parameters t, t1 precede the submodules' in named_parameters / state_dict
+    return [("t", (1,)), ("t1", (ac,)), ("fc1.weight", (100, inp)), ("fc1.bias", (100,)),
+            ("fc2.weight", (50, 100)), ("fc2.bias", (50,)), ("fc21.weight", (50, inp)), ("fc21.bias", (50,)),
+            ("fc3.weight", (ac, 50)), ("fc3.bias", (ac,))]
+
+
 def numel(layout):
     return sum(math.prod(s) for _, s in layout)
 
@@ -50,6 +64,9 @@ def linear_init_(flat, layout, generator=None):
     fan_in = None
     with torch.no_grad():
         for name, shape in layout:
+            if name in ("t", "t1"):  # BasicAcM output scales start at 1 (basic_acm.py:20-21)
+                v[name].fill_(1.0)
+                continue
             if name.endswith("weight"):
                 fan_in = shape[1]
             bound = 1.0 / math.sqrt(fan_in)

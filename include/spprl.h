@@ -256,6 +256,43 @@ sppStatus sppPpoClipLoss(const float* lp_old, const float* lp_new, const float* 
  * out = (adv - mean) / (std(ddof=1) + 1.2e-7).  out may alias adv. */
 sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream);
 
+/* ------------------------------------------------------------------ on-policy nets (A2C / PPO)
+ * The 64-wide tanh MLPs of rltoolkit/basic_model.py:7-76 used by A2C / PPO(_AcM):
+ *   net 0 = Actor (continuous): log_scale [aout], fc1 ob->64, fc2 64->64, fc3 64->aout,
+ *           mu = tanh(fc3) * lim, policy Independent(Normal(mu, exp(log_scale)))
+ *   net 1 = Critic: fc1 ob->64, fc2 64->64, fc3 64->1
+ * Flat buffers in state_dict order; inputs are the buffer's normalised obs, row-major. */
+typedef struct sppOnPolicy* sppOnPolicyHandle;
+typedef struct {
+  int ob, aout;
+  float actor_lr, critic_lr;   /* config.A_LR / C_LR */
+  float ppo_epsilon;           /* PPO clip */
+  float entropy_coef;          /* PPO_ENTROPY */
+  int max_batch;               /* largest N of any call */
+} sppOnPolicyConfig;
+sppStatus sppOnpCreate(sppOnPolicyHandle* out, const sppOnPolicyConfig* cfg, int device);
+sppStatus sppOnpDestroy(sppOnPolicyHandle h);
+sppStatus sppOnpNetSize(sppOnPolicyHandle h, int net, int64_t* n);
+sppStatus sppOnpBindNet(sppOnPolicyHandle h, int net, float* params, float* grads, float* exp_avg, float* exp_avg_sq);
+sppStatus sppOnpSetLimits(sppOnPolicyHandle h, const float* actor_lim_host /*[aout]*/);
+/* critic(x) -> v [N] (calculate_q_val / calculate_gae inputs, a2c.py:257-265, ppo.py:131). */
+sppStatus sppOnpValue(sppOnPolicyHandle h, const float* x, int N, float* v, void* stream);
+/* One critic step of A2C.update_critic (a2c.py:209-219): loss = 0.5 * mean((q - V(x))^2)
+ * (device float[1]); grads into the critic buffer; Apply = Adam(critic_lr). */
+sppStatus sppOnpCriticGrads(sppOnPolicyHandle h, const float* x, const float* q, int N, float* loss, void* stream);
+sppStatus sppOnpCriticApply(sppOnPolicyHandle h, void* stream);
+/* One PPO actor minibatch step (ppo.py:174-190 / on_policy.py:189-205): logp of the stored
+ * actions under the current policy, loss = clip_loss - entropy_coef * entropy; grads into the
+ * actor buffer (log_scale included).  out4 = {actor (clip) loss, KL = mean(lp_old - lp_new),
+ * dist = MSE(actions, next_obs) (no gradient, as in the reference; next_obs may be NULL), entropy}. */
+sppStatus sppOnpActorGrads(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
+                           const float* adv, const float* next_obs, int N, float* out4, void* stream);
+sppStatus sppOnpActorApply(sppOnPolicyHandle h, void* stream);
+/* Actor.act (basic_model.py:32-51) continuous: a = mu + exp(log_scale) * eps (eps NULL:
+ * deterministic mu), logp = Independent(Normal).log_prob(a). */
+sppStatus sppOnpAct(sppOnPolicyHandle h, const float* x, int N, const float* eps, float* act_out, float* logp_out,
+                    void* stream);
+
 /* Debug / layout check: y = act(x W^T + b) through the MFMA register-tile path.
  * x [B][K], W [N][K], b [N], y [B][N]; act 0 none, 1 relu, 2 tanh. */
 sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,

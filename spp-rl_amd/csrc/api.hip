@@ -19,6 +19,7 @@
 #include "replay.hip"
 #include "sac.hip"
 #include "ddpg.hip"
+#include "onp.hip"
 
 namespace spp {
 
@@ -395,6 +396,17 @@ struct DevArray {
   }
 };
 
+// A weight-gradient job set (dw.hip): up to two phases launched separately.
+struct DwSet {
+  DevArray<float> slab;
+  DevArray<DwJob> jobs;
+  DevArray<int> items;
+  int B = -1;
+  int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
+  int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
+  void release() { slab.release(); jobs.release(); items.release(); }
+};
+
 // dims -> kernel instantiation
 struct KernelSet {
   void (*critic)(SacArgs);
@@ -488,14 +500,7 @@ struct sppAgent {
   // ACM regression scratch
   float *RX = nullptr, *RZ1 = nullptr, *RZ2 = nullptr, *RP1 = nullptr, *RP2 = nullptr, *RP3 = nullptr;
   // weight-gradient job sets: [0] SAC (critic phase, actor phase), [1] ACM regression
-  struct DwSet {
-    DevArray<float> slab;
-    DevArray<DwJob> jobs;
-    DevArray<int> items;
-    int B = -1;
-    int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
-    int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
-  } dws[2];
+  DwSet dws[2];
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
   float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
@@ -696,6 +701,81 @@ static void launch_pack(sppAgent* a, int off, int n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(k_pack_matrix, dim3(64, n), dim3(256), 0, st, (const PackJob*)(a->d_pj.ptr + off));
 }
 
+// Split assignment, slab arena, item table and upload of a job set.
+static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp, int B, int num_cu) {
+  // Sample splits: the large (>= 128x128 padded) GEMMs of a phase share ~one
+  // workgroup per CU in proportion to their MACs; the small, HBM-bound ones
+  // take 2048-sample items.
+  auto is_big = [](const DwJob& j) {
+    return (int64_t)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32) >= 128 * 128;
+  };
+  auto assign_splits = [&](int first, int count) {
+    double big = 0.0;
+    for (int i = first; i < first + count; ++i)
+      if (is_big(jobs[i])) big += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
+    for (int i = first; i < first + count; ++i) {
+      DwJob& j = jobs[i];
+      const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
+      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : cdiv(Bp, 2048);
+      ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
+      j.split_len = (int)round_up(cdiv(Bp, ns), 32);
+      j.nsplit = cdiv(Bp, j.split_len);
+    }
+  };
+  for (int ph = 0; ph < nph; ++ph) assign_splits(D.j0[ph], D.nj[ph]);
+  // slabs: phases run back to back on one stream -> they share one arena
+  size_t need = 0;
+  for (int ph = 0; ph < nph; ++ph) {
+    size_t off = 0;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+      if (jobs[j].nsplit > 1) {
+        jobs[j].slab = nullptr;
+        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+      }
+    }
+    need = std::max(need, off);
+  }
+  if (need > D.slab.n) {
+    D.slab.release();
+    SPP_CHECK_HIP(D.slab.alloc(need));
+  }
+  std::vector<int> items;
+  for (int ph = 0; ph < nph; ++ph) {
+    size_t off = 0;
+    std::vector<int> jj, ss;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+      if (jobs[j].nsplit > 1) {
+        jobs[j].slab = D.slab.ptr + off;
+        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+      }
+    }
+    // large-GEMM items first (they set the launch's critical path)
+    for (int pass = 0; pass < 2; ++pass)
+      for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+        if (is_big(jobs[j]) != (pass == 0)) continue;
+        for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
+          jj.push_back(j - D.j0[ph]);
+          ss.push_back(sp);
+        }
+      }
+    D.max_elems[ph] = 1;
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j)
+      D.max_elems[ph] = std::max<int64_t>(D.max_elems[ph], (int64_t)jobs[j].N * (jobs[j].K0 + jobs[j].K1) + jobs[j].N);
+    D.ioff[ph] = (int)items.size();
+    D.nitems[ph] = (int)jj.size();
+    items.insert(items.end(), jj.begin(), jj.end());
+    items.insert(items.end(), ss.begin(), ss.end());
+  }
+  D.jobs.release();
+  D.items.release();
+  SPP_CHECK_HIP(D.jobs.alloc(jobs.size()));
+  SPP_CHECK_HIP(D.items.alloc(items.size()));
+  SPP_CHECK_HIP(hipMemcpy(D.jobs.ptr, jobs.data(), sizeof(DwJob) * jobs.size(), hipMemcpyHostToDevice));
+  SPP_CHECK_HIP(hipMemcpy(D.items.ptr, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
+  D.B = B;
+  return SPP_OK;
+}
+
 // (Re)build a weight-gradient job set for batch size B.
 //   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
 static sppStatus build_dw(sppAgent* a, int set, int B) {
@@ -713,26 +793,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     j.slab_stride = round_up((int64_t)N * (K0 + K1) + N, 4);
     jobs.push_back(j);
   };
-  // Sample splits: the large (>= 128x128 padded) GEMMs of a phase share ~one
-  // workgroup per CU in proportion to their MACs; the small, HBM-bound ones
-  // take 2048-sample items.
-  auto is_big = [](const DwJob& j) {
-    return (int64_t)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32) >= 128 * 128;
-  };
-  auto assign_splits = [&](int first, int count) {
-    double big = 0.0;
-    for (int i = first; i < first + count; ++i)
-      if (is_big(jobs[i])) big += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
-    for (int i = first; i < first + count; ++i) {
-      DwJob& j = jobs[i];
-      const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
-      int ns = is_big(j) ? (int)std::lround(a->num_cu * pm / big) : cdiv(Bp, 2048);
-      ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
-      j.split_len = (int)round_up(cdiv(Bp, ns), 32);
-      j.nsplit = cdiv(Bp, j.split_len);
-    }
-  };
-  sppAgent::DwSet& D = a->dws[set];
+  DwSet& D = a->dws[set];
   int nph = 0;
   if (a->ddpg) {
     if (set == 0) {
@@ -800,68 +861,18 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     D.nj[0] = (int)jobs.size();
     nph = 1;
   }
-  for (int ph = 0; ph < nph; ++ph) assign_splits(D.j0[ph], D.nj[ph]);
-  // slabs: phases run back to back on one stream -> they share one arena
-  size_t need = 0;
-  for (int ph = 0; ph < nph; ++ph) {
-    size_t off = 0;
-    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-      if (jobs[j].nsplit > 1) {
-        jobs[j].slab = nullptr;
-        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
-      }
-    }
-    need = std::max(need, off);
-  }
-  if (need > D.slab.n) {
-    D.slab.release();
-    SPP_CHECK_HIP(D.slab.alloc(need));
-  }
-  std::vector<int> items;
-  for (int ph = 0; ph < nph; ++ph) {
-    size_t off = 0;
-    std::vector<int> jj, ss;
-    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-      if (jobs[j].nsplit > 1) {
-        jobs[j].slab = D.slab.ptr + off;
-        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
-      }
-    }
-    // large-GEMM items first (they set the launch's critical path)
-    for (int pass = 0; pass < 2; ++pass)
-      for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-        if (is_big(jobs[j]) != (pass == 0)) continue;
-        for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
-          jj.push_back(j - D.j0[ph]);
-          ss.push_back(sp);
-        }
-      }
-    D.max_elems[ph] = 1;
-    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j)
-      D.max_elems[ph] = std::max<int64_t>(D.max_elems[ph], (int64_t)jobs[j].N * (jobs[j].K0 + jobs[j].K1) + jobs[j].N);
-    D.ioff[ph] = (int)items.size();
-    D.nitems[ph] = (int)jj.size();
-    items.insert(items.end(), jj.begin(), jj.end());
-    items.insert(items.end(), ss.begin(), ss.end());
-  }
-  D.jobs.release();
-  D.items.release();
-  SPP_CHECK_HIP(D.jobs.alloc(jobs.size()));
-  SPP_CHECK_HIP(D.items.alloc(items.size()));
-  SPP_CHECK_HIP(hipMemcpy(D.jobs.ptr, jobs.data(), sizeof(DwJob) * jobs.size(), hipMemcpyHostToDevice));
-  SPP_CHECK_HIP(hipMemcpy(D.items.ptr, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
-  D.B = B;
-  return SPP_OK;
+  return finalize_dw(D, jobs, nph, Bp, B, a->num_cu);
 }
 
-static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) {
-  sppAgent::DwSet& D = a->dws[set];
+
+static void launch_dw_set(DwSet& D, int ph, hipStream_t st) {
   const int* ij = D.items.ptr + D.ioff[ph];
   const int* is = ij + D.nitems[ph];
   const DwJob* jobs = D.jobs.ptr + D.j0[ph];
   hipLaunchKernelGGL(k_dw, dim3(D.nitems[ph]), dim3(kDwThreads), 0, st, jobs, ij, is);
   hipLaunchKernelGGL(k_dw_reduce, dim3(cdiv(D.max_elems[ph], 4 * 256), D.nj[ph]), dim3(256), 0, st, jobs);
 }
+static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) { launch_dw_set(a->dws[set], ph, st); }
 
 // Adam job table [critic1, critic2 (+polyak targets) | actor | acm]; pointers only.
 // DDPG_AcM: [critic (+polyak) | - | actor (+polyak of the target actor, ddpg.py:273-284) | acm].
@@ -1025,7 +1036,7 @@ sppStatus sppAgentDestroy(sppAgentHandle a) {
   for (auto& v : a->tev)
     for (auto e : v) hipEventDestroy(e);
   a->scratch.release(); a->d_adam.release();
-  for (auto& D : a->dws) { D.slab.release(); D.jobs.release(); D.items.release(); }
+  for (auto& D : a->dws) D.release();
   delete a;
   return SPP_OK;
 }
@@ -1466,6 +1477,331 @@ sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y
   SPP_CHECK_HIP(hipGetLastError());
   SPP_CHECK_HIP(hipStreamSynchronize(st));
   hipFree(wf); hipFree(dj);
+  return SPP_OK;
+}
+
+}  // extern "C"
+
+// ================================================================== on-policy (A2C / PPO) nets
+namespace spp {
+struct OnpKernels {
+  void (*value)(OnpArgs);
+  void (*critic)(OnpArgs);
+  void (*actor)(OnpArgs);
+  void (*act)(OnpArgs);
+};
+template <int OB, int AOUT>
+OnpKernels make_onp() {
+  using C = OCfg<OB, AOUT>;
+  return {k_onp_value<C>, k_onp_critic_grad<C>, k_onp_actor_grad<C>, k_onp_act<C>};
+}
+static bool find_onp(int ob, int aout, OnpKernels* k) {
+  if (ob == 17 && aout == 17) { *k = make_onp<17, 17>(); return true; }  // SPP-PPO HalfCheetah
+  if (ob == 11 && aout == 11) { *k = make_onp<11, 11>(); return true; }  // Hopper
+  if (ob == 17 && aout == 6) { *k = make_onp<17, 6>(); return true; }    // vanilla PPO HalfCheetah
+  if (ob == 3 && aout == 1) { *k = make_onp<3, 1>(); return true; }      // Pendulum (tests)
+  return false;
+}
+static int64_t onp_actor_size(int ob, int aout) { return aout + 64LL * ob + 64 + 64 * 64 + 64 + aout * 64LL + aout; }
+static int64_t onp_critic_size(int ob) { return 64LL * ob + 64 + 64 * 64 + 64 + 64 + 1; }
+}  // namespace spp
+
+struct sppOnPolicy {
+  sppOnPolicyConfig cfg{};
+  int device = 0, num_cu = 256;
+  OnpKernels ks{};
+  NetBufs net[2];  // 0 actor, 1 critic
+  int64_t nsize[2] = {};
+  int64_t steps[2] = {0, 0};
+  DevArray<float> lim;
+  DevArray<float4> pk;
+  DevArray<PackJob> d_pj;
+  int npj_actor = 0, npj_critic = 0;
+  OnpNet actor{}, critic{};
+  std::vector<TabSeg> tab;
+  DevArray<float> scratch;
+  float *XT = nullptr, *H1 = nullptr, *H2 = nullptr, *D1 = nullptr, *D2 = nullptr, *D3 = nullptr, *part = nullptr;
+  int Bpmax = 0, pstride = 0;
+  DwSet dw[2];  // 0 critic, 1 actor
+  DevArray<AdamJob> d_adam;
+};
+
+static sppStatus onp_packs(sppOnPolicy* o) {
+  const int ob = o->cfg.ob, aout = o->cfg.aout;
+  SPP_REQUIRE(o->net[0].p && o->net[1].p, SPP_E_STATE, "on-policy nets not bound");
+  std::vector<PackJob> jobs;
+  std::vector<const float4**> slots;
+  auto M = [&](const float* W, int ld, int trans, MapDesc out, MapDesc in, int NBO, int NBI, const float4** slot) {
+    jobs.push_back(PackJob{W, nullptr, 1 << 30, ld, trans, 0, out, in, NBO, NBI, 0, nullptr});
+    slots.push_back(slot);
+  };
+  o->tab.clear();
+  int toff = 0;
+  auto T = [&](const float* v, int n) {
+    const int off = toff, tot = (int)round_up(n, 32);
+    o->tab.push_back(TabSeg{v, n, tot, off, 0});
+    toff += tot;
+    return off;
+  };
+  {  // actor: log_scale, fc1, fc2, fc3 (basic_model.py:14-21)
+    const float* P = o->net[0].p;
+    const float *W1 = P + aout, *b1 = W1 + 64 * ob, *W2 = b1 + 64, *b2 = W2 + 64 * 64, *W3 = b2 + 64,
+                *b3 = W3 + aout * 64;
+    M(W1, ob, 0, nat(64), nat(ob), 2, blocks_of(ob), &o->actor.W1);
+    M(W2, 64, 0, nat(64), nat(64), 2, 2, &o->actor.W2);
+    M(W3, 64, 0, nat(aout), nat(64), blocks_of(aout), 2, &o->actor.W3);
+    M(W3, 64, 1, nat(64), nat(aout), 2, blocks_of(aout), &o->actor.W3T);
+    M(W2, 64, 1, nat(64), nat(64), 2, 2, &o->actor.W2T);
+    o->actor.tb1 = T(b1, 64);
+    o->actor.tb2 = T(b2, 64);
+    o->actor.tb3 = T(b3, aout);
+  }
+  o->npj_actor = (int)jobs.size();
+  {  // critic: fc1, fc2, fc3 (basic_model.py:62-70)
+    const float* P = o->net[1].p;
+    const float *W1 = P, *b1 = W1 + 64 * ob, *W2 = b1 + 64, *b2 = W2 + 64 * 64, *w3 = b2 + 64, *b3 = w3 + 64;
+    M(W1, ob, 0, nat(64), nat(ob), 2, blocks_of(ob), &o->critic.W1);
+    M(W2, 64, 0, nat(64), nat(64), 2, 2, &o->critic.W2);
+    M(W2, 64, 1, nat(64), nat(64), 2, 2, &o->critic.W2T);
+    o->critic.tb1 = T(b1, 64);
+    o->critic.tb2 = T(b2, 64);
+    o->critic.tb3 = T(w3, 64);
+    o->critic.b3 = b3;
+  }
+  o->npj_critic = (int)jobs.size() - o->npj_actor;
+  SPP_REQUIRE(toff <= 1024 && o->tab.size() <= 8, SPP_E_SHAPE, "on-policy LDS table too large");
+  size_t nf4 = 0;
+  for (auto& j : jobs) nf4 += (size_t)j.NBO * j.NBI * 256;
+  o->pk.release();
+  SPP_CHECK_HIP(o->pk.alloc(nf4));
+  size_t of = 0;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    jobs[i].dst = o->pk.ptr + of;
+    *slots[i] = jobs[i].dst;
+    of += (size_t)jobs[i].NBO * jobs[i].NBI * 256;
+  }
+  o->d_pj.release();
+  SPP_CHECK_HIP(o->d_pj.alloc(jobs.size()));
+  SPP_CHECK_HIP(hipMemcpy(o->d_pj.ptr, jobs.data(), sizeof(PackJob) * jobs.size(), hipMemcpyHostToDevice));
+  AdamJob aj[2] = {AdamJob{o->net[0].p, o->net[0].g, o->net[0].m, o->net[0].v, nullptr, o->net[0].n},
+                   AdamJob{o->net[1].p, o->net[1].g, o->net[1].m, o->net[1].v, nullptr, o->net[1].n}};
+  if (!o->d_adam.ptr) SPP_CHECK_HIP(o->d_adam.alloc(2));
+  SPP_CHECK_HIP(hipMemcpy(o->d_adam.ptr, aj, sizeof(aj), hipMemcpyHostToDevice));
+  o->dw[0].B = o->dw[1].B = -1;
+  return SPP_OK;
+}
+
+static sppStatus onp_dw(sppOnPolicy* o, int which, int N) {
+  const int Bp = (int)round_up(N, 32), ob = o->cfg.ob, aout = o->cfg.aout;
+  std::vector<DwJob> jobs;
+  auto J = [&](const float* A, int Nn, const float* X, int K, float* dW, float* db) {
+    DwJob j{};
+    j.A = A; j.N = Nn; j.X0 = X; j.K0 = K; j.dW = dW; j.db = db; j.Bp = Bp; j.nrow2 = Nn;
+    j.slab_stride = round_up((int64_t)Nn * K + Nn, 4);
+    jobs.push_back(j);
+  };
+  if (which == 0) {
+    float* G = o->net[1].g;
+    float *gW1 = G, *gb1 = gW1 + 64 * ob, *gW2 = gb1 + 64, *gb2 = gW2 + 64 * 64, *gw3 = gb2 + 64, *gb3 = gw3 + 64;
+    J(o->D1, 64, o->XT, ob, gW1, gb1);
+    J(o->D2, 64, o->H1, 64, gW2, gb2);
+    J(o->D3, 1, o->H2, 64, gw3, gb3);
+  } else {
+    float* G = o->net[0].g;
+    float *gW1 = G + aout, *gb1 = gW1 + 64 * ob, *gW2 = gb1 + 64, *gb2 = gW2 + 64 * 64, *gW3 = gb2 + 64,
+          *gb3 = gW3 + aout * 64;
+    J(o->D1, 64, o->XT, ob, gW1, gb1);
+    J(o->D2, 64, o->H1, 64, gW2, gb2);
+    J(o->D3, aout, o->H2, 64, gW3, gb3);
+  }
+  DwSet& D = o->dw[which];
+  D.j0[0] = 0;
+  D.nj[0] = (int)jobs.size();
+  return finalize_dw(D, jobs, 1, Bp, N, o->num_cu);
+}
+
+static OnpArgs onp_args(sppOnPolicy* o, int N) {
+  OnpArgs p{};
+  p.N = N;
+  p.Np = (int)round_up(N, 32);
+  p.actor = o->actor;
+  p.critic = o->critic;
+  p.log_scale = o->net[0].p;
+  p.lim = o->lim.ptr;
+  p.eps_clip = o->cfg.ppo_epsilon;
+  p.XT = o->XT; p.H1 = o->H1; p.H2 = o->H2; p.D1 = o->D1; p.D2 = o->D2; p.D3 = o->D3;
+  p.part = o->part;
+  p.pstride = o->pstride;
+  p.nseg = (int)o->tab.size();
+  for (int i = 0; i < p.nseg; ++i) p.seg[i] = o->tab[i];
+  return p;
+}
+
+static sppStatus onp_ready(sppOnPolicy* o, int N, hipStream_t st) {
+  SPP_REQUIRE(N > 0 && N <= o->cfg.max_batch, SPP_E_SHAPE, "batch %d outside (0, max_batch=%d]", N, o->cfg.max_batch);
+  SPP_REQUIRE(o->lim.ptr, SPP_E_STATE, "actor limits not set");
+  if (!o->pk.ptr) {
+    sppStatus s = onp_packs(o);
+    if (s) return s;
+  }
+  hipLaunchKernelGGL(k_pack_matrix, dim3(16, o->npj_actor + o->npj_critic), dim3(256), 0, st,
+                     (const PackJob*)o->d_pj.ptr);
+  return SPP_OK;
+}
+
+static int onp_grid(sppOnPolicy* o, int N) {
+  return std::max(1, std::min(cdiv(cdiv(N, 32), 4), o->num_cu * 2));
+}
+
+extern "C" {
+
+sppStatus sppOnpCreate(sppOnPolicyHandle* out, const sppOnPolicyConfig* cfg, int device) {
+  SPP_REQUIRE(out && cfg && cfg->max_batch > 0, SPP_E_INVALID_ARG, "on-policy create: bad args");
+  OnpKernels k;
+  SPP_REQUIRE(find_onp(cfg->ob, cfg->aout, &k), SPP_E_SHAPE, "no on-policy instantiation for (ob=%d, aout=%d)", cfg->ob,
+              cfg->aout);
+  SPP_CHECK_HIP(hipSetDevice(device));
+  auto o = std::make_unique<sppOnPolicy>();
+  o->cfg = *cfg;
+  o->device = device;
+  o->ks = k;
+  hipDeviceProp_t prop;
+  SPP_CHECK_HIP(hipGetDeviceProperties(&prop, device));
+  o->num_cu = prop.multiProcessorCount;
+  o->nsize[0] = onp_actor_size(cfg->ob, cfg->aout);
+  o->nsize[1] = onp_critic_size(cfg->ob);
+  const int64_t Bp = round_up(cfg->max_batch, 32);
+  o->Bpmax = (int)Bp;
+  o->pstride = (int)round_up(3 + cfg->aout, 4);
+  const int64_t rows = cfg->ob + 64 + 64 + 64 + 64 + std::max(cfg->aout, 1);
+  const int64_t total = rows * Bp + (Bp / 32) * o->pstride + 64;
+  hipError_t e = o->scratch.alloc(total);
+  if (e != hipSuccess) {
+    set_error("on-policy scratch alloc: %s", hipGetErrorString(e));
+    return SPP_E_OOM;
+  }
+  SPP_CHECK_HIP(hipMemset(o->scratch.ptr, 0, sizeof(float) * total));
+  float* b = o->scratch.ptr;
+  o->XT = b; b += cfg->ob * Bp;
+  o->H1 = b; b += 64 * Bp;
+  o->H2 = b; b += 64 * Bp;
+  o->D1 = b; b += 64 * Bp;
+  o->D2 = b; b += 64 * Bp;
+  o->D3 = b; b += std::max(cfg->aout, 1) * Bp;
+  o->part = b;
+  *out = o.release();
+  return SPP_OK;
+}
+
+sppStatus sppOnpDestroy(sppOnPolicyHandle o) {
+  if (!o) return SPP_OK;
+  hipSetDevice(o->device);
+  hipDeviceSynchronize();
+  o->lim.release(); o->pk.release(); o->d_pj.release(); o->scratch.release(); o->d_adam.release();
+  for (auto& D : o->dw) D.release();
+  delete o;
+  return SPP_OK;
+}
+
+sppStatus sppOnpNetSize(sppOnPolicyHandle o, int net, int64_t* n) {
+  SPP_REQUIRE(o && n && (net == 0 || net == 1), SPP_E_INVALID_ARG, "bad net id");
+  *n = o->nsize[net];
+  return SPP_OK;
+}
+
+sppStatus sppOnpBindNet(sppOnPolicyHandle o, int net, float* p, float* g, float* m, float* v) {
+  SPP_REQUIRE(o && (net == 0 || net == 1) && p && g && m && v, SPP_E_INVALID_ARG, "on-policy bind: bad args");
+  o->net[net] = NetBufs{p, g, m, v, o->nsize[net]};
+  o->pk.release();
+  return SPP_OK;
+}
+
+sppStatus sppOnpSetLimits(sppOnPolicyHandle o, const float* lim_host) {
+  SPP_REQUIRE(o && lim_host, SPP_E_INVALID_ARG, "null");
+  if (!o->lim.ptr) SPP_CHECK_HIP(o->lim.alloc(o->cfg.aout));
+  SPP_CHECK_HIP(hipMemcpy(o->lim.ptr, lim_host, sizeof(float) * o->cfg.aout, hipMemcpyHostToDevice));
+  return SPP_OK;
+}
+
+sppStatus sppOnpValue(sppOnPolicyHandle o, const float* x, int N, float* v, void* stream) {
+  SPP_REQUIRE(o && x && v, SPP_E_INVALID_ARG, "value: null");
+  hipStream_t st = S(stream);
+  sppStatus s = onp_ready(o, N, st);
+  if (s) return s;
+  OnpArgs p = onp_args(o, N);
+  p.X = x;
+  p.V = v;
+  hipLaunchKernelGGL(o->ks.value, dim3(onp_grid(o, N)), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpCriticGrads(sppOnPolicyHandle o, const float* x, const float* q, int N, float* loss, void* stream) {
+  SPP_REQUIRE(o && x && q, SPP_E_INVALID_ARG, "critic grads: null");
+  hipStream_t st = S(stream);
+  sppStatus s = onp_ready(o, N, st);
+  if (s) return s;
+  if (o->dw[0].B != N && (s = onp_dw(o, 0, N))) return s;
+  OnpArgs p = onp_args(o, N);
+  p.X = x;
+  p.Q = q;
+  hipLaunchKernelGGL(o->ks.critic, dim3(onp_grid(o, N)), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
+  launch_dw_set(o->dw[0], 0, st);
+  hipLaunchKernelGGL(k_onp_finish_critic, dim3(1), dim3(256), 0, st, (const float*)o->part, p.Np / 32, o->pstride, N,
+                     loss);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpCriticApply(sppOnPolicyHandle o, void* stream) {
+  SPP_REQUIRE(o && o->d_adam.ptr, SPP_E_STATE, "on-policy handle not ready");
+  o->steps[1] += 1;
+  const double bc1 = 1.0 - std::pow(0.9, (double)o->steps[1]), bc2s = std::sqrt(1.0 - std::pow(0.999, (double)o->steps[1]));
+  hipLaunchKernelGGL(k_adam, dim3(std::max(1, std::min(cdiv(o->net[1].n, 1024), 1024)), 1), dim3(256), 0, S(stream),
+                     (const AdamJob*)(o->d_adam.ptr + 1), (float)(-(o->cfg.critic_lr / bc1)), (float)bc2s, 0.f);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpActorGrads(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old,
+                           const float* adv, const float* next_obs, int N, float* out4, void* stream) {
+  SPP_REQUIRE(o && x && act && lp_old && adv && out4, SPP_E_INVALID_ARG, "actor grads: null");
+  hipStream_t st = S(stream);
+  sppStatus s = onp_ready(o, N, st);
+  if (s) return s;
+  if (o->dw[1].B != N && (s = onp_dw(o, 1, N))) return s;
+  OnpArgs p = onp_args(o, N);
+  p.X = x; p.ACT = act; p.LP_OLD = lp_old; p.ADV = adv; p.NXT = next_obs;
+  hipLaunchKernelGGL(o->ks.actor, dim3(onp_grid(o, N)), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
+  launch_dw_set(o->dw[1], 0, st);
+  hipLaunchKernelGGL(k_onp_finish_actor, dim3(1), dim3(256), 0, st, (const float*)o->part, p.Np / 32, o->pstride, N,
+                     o->cfg.aout, o->cfg.entropy_coef, (const float*)o->net[0].p, o->net[0].g, out4);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpActorApply(sppOnPolicyHandle o, void* stream) {
+  SPP_REQUIRE(o && o->d_adam.ptr, SPP_E_STATE, "on-policy handle not ready");
+  o->steps[0] += 1;
+  const double bc1 = 1.0 - std::pow(0.9, (double)o->steps[0]), bc2s = std::sqrt(1.0 - std::pow(0.999, (double)o->steps[0]));
+  hipLaunchKernelGGL(k_adam, dim3(std::max(1, std::min(cdiv(o->net[0].n, 1024), 1024)), 1), dim3(256), 0, S(stream),
+                     (const AdamJob*)o->d_adam.ptr, (float)(-(o->cfg.actor_lr / bc1)), (float)bc2s, 0.f);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpAct(sppOnPolicyHandle o, const float* x, int N, const float* eps, float* act_out, float* logp_out,
+                    void* stream) {
+  SPP_REQUIRE(o && x && act_out, SPP_E_INVALID_ARG, "act: null");
+  hipStream_t st = S(stream);
+  sppStatus s = onp_ready(o, N, st);
+  if (s) return s;
+  OnpArgs p = onp_args(o, N);
+  p.X = x; p.EPS = eps; p.ACT_OUT = act_out; p.LP_OUT = logp_out;
+  hipLaunchKernelGGL(o->ks.act, dim3(onp_grid(o, N)), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
 

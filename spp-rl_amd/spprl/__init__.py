@@ -4,7 +4,7 @@ Host side keeps rltoolkit's agent / buffer API; all device work runs in
 libspprl.so (hand-written HIP kernels for gfx950) through the C-ABI in
 include/spprl.h.
 """
-from . import _lib, config, dp, nets, ppo  # noqa: F401
+from . import _lib, config, dp, nets, onpolicy, ppo  # noqa: F401
 from ._lib import SppError, load  # noqa: F401
 from .replay import BufferAcMOffPolicy  # noqa: F401
 from .sac_acm import SAC_AcM  # noqa: F401

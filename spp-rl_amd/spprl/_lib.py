@@ -33,6 +33,11 @@ class AgentConfig(ctypes.Structure):
                 ("alpha_lr", c_float), ("acm_lr", c_float), ("target_entropy", c_float), ("max_batch", c_int)]
 
 
+class OnPolicyConfig(ctypes.Structure):
+    _fields_ = [("ob", c_int), ("aout", c_int), ("actor_lr", c_float), ("critic_lr", c_float),
+                ("ppo_epsilon", c_float), ("entropy_coef", c_float), ("max_batch", c_int)]
+
+
 class Batch(ctypes.Structure):
     _fields_ = [("B", c_int), ("obs", c_void_p), ("next_obs", c_void_p), ("action", c_void_p),
                 ("reward", c_void_p), ("done", c_void_p), ("acm_action", c_void_p)]
@@ -96,6 +101,18 @@ _SIGS = {
     "sppDdpgAcmCriticApply": (c_int, [c_void_p, c_void_p]),
     "sppDdpgAcmActorGrads": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppDdpgAcmActorApply": (c_int, [c_void_p, c_void_p]),
+    "sppOnpCreate": (c_int, [P(c_void_p), P(OnPolicyConfig), c_int]),
+    "sppOnpDestroy": (c_int, [c_void_p]),
+    "sppOnpNetSize": (c_int, [c_void_p, c_int, P(c_int64)]),
+    "sppOnpBindNet": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sppOnpSetLimits": (c_int, [c_void_p, c_void_p]),
+    "sppOnpValue": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "sppOnpCriticGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "sppOnpCriticApply": (c_int, [c_void_p, c_void_p]),
+    "sppOnpActorGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                 c_void_p]),
+    "sppOnpActorApply": (c_int, [c_void_p, c_void_p]),
+    "sppOnpAct": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sppGaeScan": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, ctypes.c_double,
                            ctypes.c_double,
                             c_int, c_void_p, c_void_p, c_void_p]),

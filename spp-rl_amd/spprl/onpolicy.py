@@ -1,0 +1,161 @@
+"""On-policy (A2C / PPO / PPO_AcM) networks on the MI355X library.
+
+``OnPolicyNets`` holds the reference's 64-wide tanh Actor / Critic
+(rltoolkit/basic_model.py:7-76) as flat device buffers and mirrors the
+pieces of A2C / PPO that touch them:
+  value(x)                       critic(x)                          a2c.py:257-265
+  update_critic(obs, next_obs, rew, done)
+                                 A2C.update_critic: critic_num_target_updates x
+                                 num_critic_updates_per_target full-batch steps   a2c.py:186-225
+  update_actor(adv, obs, act, lp_old, next_obs)
+                                 PPO.update_actor(_acm): minibatch epochs with KL early stop
+                                                                    ppo.py:152-192, on_policy.py:164-216
+  act(obs, eps)                  Actor.act (continuous)             basic_model.py:32-51
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, nets, ppo
+from ._lib import call, ptr, stream_handle
+
+H = 64
+
+
+def actor_layout(ob, aout):
+    return [("log_scale", (aout,)), ("fc1.weight", (H, ob)), ("fc1.bias", (H,)), ("fc2.weight", (H, H)),
+            ("fc2.bias", (H,)), ("fc3.weight", (aout, H)), ("fc3.bias", (aout,))]
+
+
+def critic_layout(ob):
+    return [("fc1.weight", (H, ob)), ("fc1.bias", (H,)), ("fc2.weight", (H, H)), ("fc2.bias", (H,)),
+            ("fc3.weight", (1, H)), ("fc3.bias", (1,))]
+
+
+class OnPolicyNets:
+    def __init__(self, ob, aout, ac_lim=1.0, actor_lr=3e-3, critic_lr=3e-4, ppo_epsilon=0.2, entropy_coef=0.0,
+                 gamma=0.99, gae_lambda=0.95, critic_num_target_updates=10, num_critic_updates_per_target=10,
+                 max_ppo_epochs=50, ppo_batch_size=1000, kl_div_threshold=0.15, normalize_adv=True,
+                 max_batch=4096, device="cuda", seed=None):
+        _lib.load()
+        self.ob, self.aout, self.device = ob, aout, torch.device(device)
+        self.gamma, self.gae_lambda = gamma, gae_lambda
+        self.critic_num_target_updates, self.num_critic_updates_per_target = (critic_num_target_updates,
+                                                                              num_critic_updates_per_target)
+        self.max_ppo_epochs, self.ppo_batch_size, self.kl_div_threshold = max_ppo_epochs, ppo_batch_size, kl_div_threshold
+        self.normalize_adv = normalize_adv
+        self.max_batch = int(max_batch)
+        cfg = _lib.OnPolicyConfig(ob, aout, actor_lr, critic_lr, ppo_epsilon, entropy_coef, self.max_batch)
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        call("sppOnpCreate", ctypes.byref(h), ctypes.byref(cfg), dev)
+        self._h = h
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.layouts = [actor_layout(ob, aout), critic_layout(ob)]
+        self.params, self.grads, self.m, self.v = [], [], [], []
+        for net, lay in enumerate(self.layouts):
+            n = ctypes.c_int64()
+            call("sppOnpNetSize", self._h, net, ctypes.byref(n))
+            assert n.value == nets.numel(lay)
+            p = torch.empty(n.value, device=self.device)
+            if net == 0:
+                nets.linear_init_(p[aout:], lay[1:], gen)
+                p[:aout].fill_(-1.34)  # log_scale init, basic_model.py:18-20
+            else:
+                nets.linear_init_(p, lay, gen)
+            self.params.append(p)
+            for lst in (self.grads, self.m, self.v):
+                lst.append(torch.zeros(n.value, device=self.device))
+            call("sppOnpBindNet", self._h, net, ptr(p), ptr(self.grads[net]), ptr(self.m[net]), ptr(self.v[net]))
+        lim = np.full(aout, float(ac_lim), np.float32) if np.ndim(ac_lim) == 0 else np.asarray(ac_lim, np.float32)
+        call("sppOnpSetLimits", self._h, lim.ctypes.data_as(ctypes.c_void_p))
+        self.loss = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib.load().sppOnpDestroy(h)
+            self._h = None
+
+    def _dev(self, x):
+        return torch.as_tensor(x, dtype=torch.float32).to(self.device).contiguous()
+
+    def load_net(self, net, flat):
+        self.params[net].copy_(self._dev(flat).reshape(-1))
+
+    # ------------------------------------------------------------------ critic
+    def value(self, x):
+        x = self._dev(x)
+        v = torch.empty(x.shape[0], device=self.device)
+        call("sppOnpValue", self._h, ptr(x), x.shape[0], ptr(v), stream_handle())
+        self._keep = x
+        return v
+
+    def critic_step(self, x, q):
+        x, q = self._dev(x), self._dev(q).reshape(-1)
+        loss = torch.zeros(1, device=self.device)
+        call("sppOnpCriticGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
+        call("sppOnpCriticApply", self._h, stream_handle())
+        self._keep = (x, q)
+        return loss
+
+    def update_critic(self, obs, next_obs, rew, done):
+        """A2C.update_critic (a2c.py:186-225); returns the advantages of calculate_advantage."""
+        obs, next_obs, rew, done = (self._dev(t) for t in (obs, next_obs, rew, done))
+        total = torch.zeros(1, device=self.device)
+        for _ in range(self.critic_num_target_updates):
+            vn = self.value(next_obs)
+            q = rew + self.gamma * (1 - done) * vn
+            for _ in range(self.num_critic_updates_per_target):
+                total += self.critic_step(obs, q)
+        self.loss["critic"] = float(total.item()) / (self.critic_num_target_updates *
+                                                     self.num_critic_updates_per_target)
+        with torch.no_grad():
+            q = rew + self.gamma * (1 - done) * self.value(next_obs)
+            return q - self.value(obs)
+
+    # ------------------------------------------------------------------ actor
+    def actor_step(self, x, act, lp_old, adv, next_obs=None):
+        x, act, lp_old, adv = (self._dev(t) for t in (x, act, lp_old, adv))
+        nxt = self._dev(next_obs) if next_obs is not None else None
+        out = torch.zeros(4, device=self.device)
+        call("sppOnpActorGrads", self._h, ptr(x), ptr(act), ptr(lp_old.reshape(-1)), ptr(adv.reshape(-1)), ptr(nxt),
+             x.shape[0], ptr(out), stream_handle())
+        call("sppOnpActorApply", self._h, stream_handle())
+        self._keep = (x, act, lp_old, adv, nxt)
+        return out
+
+    def update_actor(self, advantages, obs, actions, logprobs, next_obs=None, generator=None):
+        """PPO minibatch epochs with the KL early stop (ppo.py:152-192); minibatches are a
+        random permutation per epoch like the reference's DataLoader(shuffle=True)."""
+        adv = self._dev(advantages).reshape(-1)
+        if self.normalize_adv:
+            adv = ppo.normalize_advantages(adv)
+        obs, actions, logprobs = self._dev(obs), self._dev(actions), self._dev(logprobs).reshape(-1)
+        nxt = self._dev(next_obs) if next_obs is not None else None
+        N = obs.shape[0]
+        kl, i = 0.0, 0
+        sums = torch.zeros(4, device=self.device)
+        for i in range(self.max_ppo_epochs):
+            if kl >= self.kl_div_threshold:
+                break
+            perm = torch.randperm(N, generator=generator).to(self.device)
+            for s in range(0, N, self.ppo_batch_size):
+                j = perm[s:s + self.ppo_batch_size]
+                out = self.actor_step(obs[j], actions[j], logprobs[j], adv[j], nxt[j] if nxt is not None else None)
+                sums += out
+            kl = float(out[1].item())  # KL of the epoch's last minibatch (ppo.py:188)
+        self.loss.update(actor=float(sums[0]) / (i + 1), entropy=float(sums[3]) / (i + 1), kl=kl)
+        return kl
+
+    def act(self, obs, eps=None):
+        """Actor.act: (action, log_prob); eps None -> deterministic mean."""
+        x = self._dev(obs)
+        N = x.shape[0]
+        a = torch.empty(N, self.aout, device=self.device)
+        lp = torch.empty(N, device=self.device)
+        e = self._dev(eps) if eps is not None else None
+        call("sppOnpAct", self._h, ptr(x), N, ptr(e), ptr(a), ptr(lp), stream_handle())
+        self._keep = (x, e)
+        return a, lp

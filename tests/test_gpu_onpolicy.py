@@ -1,0 +1,118 @@
+"""GPU parity of the on-policy (A2C / PPO) network kernels
+against the oracle restatement of rltoolkit/basic_model.py Actor / Critic
+(oracle/onpolicy.py; parity pinned by the oracle, which follows the reference modules line by line)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import onpolicy as oo
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+OB, AOUT = 17, 17
+
+
+def relerr(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+@pytest.fixture(scope="module")
+def nets():
+    from spprl.onpolicy import OnPolicyNets
+    n = OnPolicyNets(OB, AOUT, ac_lim=1.0, max_batch=5000, device=DEV, entropy_coef=0.01)
+    return n
+
+
+def _setup(nets, seed):
+    a = oo.init_flat(oo.actor_layout(OB, AOUT), seed)
+    a[:AOUT] += np.random.RandomState(seed).uniform(-0.3, 0.3, AOUT).astype(np.float32)
+    c = oo.init_flat(oo.critic_layout(OB), seed + 1)
+    nets.load_net(0, a)
+    nets.load_net(1, c)
+    return a, c
+
+
+@pytest.mark.parametrize("N", [1, 77, 3000])
+def test_value_and_critic_grad(nets, N):
+    a, c = _setup(nets, 3)
+    rng = np.random.RandomState(N)
+    x = (rng.randn(N, OB) * 1.5).astype(np.float32)
+    q = rng.randn(N).astype(np.float32)
+    v = nets.value(x).cpu().numpy()
+    with torch.no_grad():
+        want = oo.critic(oo._params(c, oo.critic_layout(OB)), torch.from_numpy(x)).squeeze(-1).numpy()
+    np.testing.assert_allclose(v, want, rtol=1e-5, atol=1e-5)
+    from spprl import _lib
+    xd, qd = torch.from_numpy(x).to(DEV), torch.from_numpy(q).to(DEV)
+    loss = torch.zeros(1, device=DEV)
+    _lib.call("sppOnpCriticGrads", nets._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), _lib.stream_handle())
+    torch.cuda.synchronize()
+    l_ref, g_ref = oo.critic_step(c, OB, x, q)
+    assert loss.item() == pytest.approx(l_ref, rel=1e-5)
+    assert relerr(nets.grads[1].cpu().numpy(), g_ref) < 2e-5
+
+
+@pytest.mark.parametrize("N", [1, 500, 2048])
+def test_actor_grad_clip_entropy(nets, N):
+    a, c = _setup(nets, 5)
+    rng = np.random.RandomState(N + 1)
+    x = (rng.randn(N, OB) * 1.2).astype(np.float32)
+    act = rng.uniform(-1.2, 1.2, (N, AOUT)).astype(np.float32)
+    lp_old = (rng.randn(N) * 2 - 10).astype(np.float32)
+    with torch.no_grad():
+        lp_cur = oo.actor_dist(oo._params(a, oo.actor_layout(OB, AOUT)), torch.from_numpy(x),
+                               torch.ones(AOUT)).log_prob(torch.from_numpy(act)).numpy()
+    lp_old = (lp_cur + rng.randn(N).astype(np.float32) * 0.2).astype(np.float32)  # ratios around 1 (both branches)
+    adv = rng.randn(N).astype(np.float32)
+    nxt = rng.randn(N, AOUT).astype(np.float32)
+    from spprl import _lib
+    t = lambda z: torch.from_numpy(np.ascontiguousarray(z)).to(DEV)  # noqa: E731
+    xd, ad, ld, vd, nd = t(x), t(act), t(lp_old), t(adv), t(nxt)
+    out = torch.zeros(4, device=DEV)
+    _lib.call("sppOnpActorGrads", nets._h, _lib.ptr(xd), _lib.ptr(ad), _lib.ptr(ld), _lib.ptr(vd), _lib.ptr(nd), N,
+              _lib.ptr(out), _lib.stream_handle())
+    torch.cuda.synchronize()
+    ref, g_ref = oo.actor_step(a, OB, AOUT, np.ones(AOUT, np.float32), x, act, lp_old, adv, entropy_coef=0.01,
+                               next_obs=nxt)
+    o = out.cpu().numpy()
+    assert o[0] == pytest.approx(ref["actor"], rel=1e-4, abs=1e-6)
+    assert o[1] == pytest.approx(ref["kl"], rel=1e-4, abs=1e-5)
+    assert o[2] == pytest.approx(ref["dist"], rel=1e-5)
+    assert o[3] == pytest.approx(ref["entropy"], rel=1e-5)
+    g = nets.grads[0].cpu().numpy()
+    assert relerr(g, g_ref) < 2e-4, relerr(g, g_ref)
+    np.testing.assert_allclose(g[:AOUT], g_ref[:AOUT], rtol=1e-3, atol=1e-6)  # log_scale
+
+
+def test_act_sample_and_deterministic(nets):
+    a, c = _setup(nets, 9)
+    rng = np.random.RandomState(4)
+    x = rng.randn(333, OB).astype(np.float32)
+    eps = rng.randn(333, AOUT).astype(np.float32)
+    for e in (None, eps):
+        act, lp = nets.act(x, e)
+        want_a, want_lp = oo.act(a, OB, AOUT, np.ones(AOUT, np.float32), x, e)
+        np.testing.assert_allclose(act.cpu().numpy(), want_a, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(lp.cpu().numpy(), want_lp, rtol=1e-4, atol=1e-4)
+
+
+def test_update_loops_run_and_improve(nets):
+    """update_critic (10x10 full-batch steps) reduces the critic loss; update_actor runs its
+    epochs with the KL stop and keeps parameters finite."""
+    _setup(nets, 11)
+    rng = np.random.RandomState(12)
+    N = 2000
+    obs = rng.randn(N, OB).astype(np.float32)
+    nobs = rng.randn(N, OB).astype(np.float32)
+    rew = rng.randn(N).astype(np.float32)
+    done = (rng.rand(N) < 0.05).astype(np.float32)
+    q0 = rew + 0.99 * (1 - done) * nets.value(nobs).cpu().numpy()
+    l0 = 0.5 * np.mean((q0 - nets.value(obs).cpu().numpy()) ** 2)
+    adv = nets.update_critic(obs, nobs, rew, done)
+    assert nets.loss["critic"] < l0
+    act, lp = nets.act(obs, rng.randn(N, AOUT).astype(np.float32))
+    nets.max_ppo_epochs = 3
+    kl = nets.update_actor(adv, obs, act, lp, generator=torch.Generator().manual_seed(0))
+    assert np.isfinite(kl)
+    assert all(torch.isfinite(p).all() for p in nets.params)

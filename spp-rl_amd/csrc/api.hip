@@ -73,7 +73,7 @@ using namespace spp;
 // ================================================================== replay handle
 struct sppReplay {
   ReplayDev d{};
-  int device = 0;
+  int device = 0, num_cu = 256;
   int64_t obs_idx = 0, ts_idx = 0, len = 0;
   // pinned ring for per-step index uploads
   static constexpr int kRing = 4;
@@ -84,7 +84,6 @@ struct sppReplay {
   // obs-stats scratch
   double* st_part = nullptr;
   double* st_mean = nullptr;
-  double* st_std = nullptr;
   uint32_t* st_state = nullptr;
   uint32_t* st_hist = nullptr;
 };
@@ -145,6 +144,10 @@ sppStatus sppReplayCreate(sppReplayHandle* out, int64_t cap, int ob, int aout, i
   SPP_CHECK_HIP(hipSetDevice(device));
   auto* h = new sppReplay;
   h->device = device;
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->num_cu = prop.multiProcessorCount;
+  }
   ReplayDev& d = h->d;
   d.cap = cap;
   d.ob = ob;
@@ -184,7 +187,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
     if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
     hipEventDestroy(h->ev[i]);
   }
-  hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_std); hipFree(h->st_state); hipFree(h->st_hist);
+  hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_state); hipFree(h->st_hist);
   delete h;
   return SPP_OK;
 }
@@ -286,35 +289,38 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   if (len <= 10) return SPP_OK;  // replay_buffer.py:84
   SPP_REQUIRE(len < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats: len too large");
   const int ob = h->d.ob;
-  const int nblk = 256, thr = 256;
-  const int G = std::min(ob, 16);
+  SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats: ob %d > %d", ob, 16 * kStatsColsPerThread);
+  const int nblk = kStatsBlocks;
+  const int G = std::min(ob, 32);  // columns per byte pass (LDS: G*4*256*4 B)
   if (!h->st_part) {
-    SPP_CHECK_HIP(hipMalloc(&h->st_part, sizeof(double) * nblk * ob));
-    SPP_CHECK_HIP(hipMalloc(&h->st_mean, sizeof(double) * ob));
-    SPP_CHECK_HIP(hipMalloc(&h->st_std, sizeof(double) * ob));
+    SPP_CHECK_HIP(hipMalloc(&h->st_part, sizeof(double) * nblk * ob * 2));
+    SPP_CHECK_HIP(hipMalloc(&h->st_mean, sizeof(double) * ob * 2));
     SPP_CHECK_HIP(hipMalloc(&h->st_state, sizeof(uint32_t) * ob * 4 * 3));
-    SPP_CHECK_HIP(hipMalloc(&h->st_hist, sizeof(uint32_t) * nblk * G * 4 * 256));
-  }
-  hipStream_t st = S(stream);
-  hipLaunchKernelGGL(k_stats_moments, dim3(nblk), dim3(thr), thr * sizeof(double), st, h->d, len,
-                     (const double*)nullptr, h->st_part, 0);
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(128), 0, st, h->st_part, nblk, ob, len, h->st_mean, 0);
-  hipLaunchKernelGGL(k_stats_moments, dim3(nblk), dim3(thr), thr * sizeof(double), st, h->d, len,
-                     (const double*)h->st_mean, h->st_part, 1);
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(128), 0, st, h->st_part, nblk, ob, len, h->st_std, 1);
-  hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(128), 0, st, h->st_state, ob, len);
-  for (int col0 = 0; col0 < ob; col0 += G) {
-    const int nc = std::min(G, ob - col0);
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hipLaunchKernelGGL(k_stats_hist, dim3(nblk), dim3(thr), nc * 4 * 256 * sizeof(uint32_t), st, h->d, len, col0,
-                         nc, shift, (const uint32_t*)h->st_state, h->st_hist);
-      hipLaunchKernelGGL(k_stats_select, dim3(nc * 4), dim3(256), 0, st, (const uint32_t*)h->st_hist, nblk, col0, nc,
-                         shift, h->st_state);
+    SPP_CHECK_HIP(hipMalloc(&h->st_hist, sizeof(uint32_t) * std::max(ob, G * 4) * 256));
+    SPP_CHECK_HIP(hipMemset(h->st_hist, 0, sizeof(uint32_t) * std::max(ob, G * 4) * 256));  // k_stats_sel re-zeroes
+    static bool attr = false;
+    if (!attr) {  // > 64 KiB dynamic LDS for wide observations
+      hipFuncSetAttribute((const void*)k_stats_p1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)k_stats_pk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
     }
   }
-  hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(128), 0, st, (const uint32_t*)h->st_state,
-                     (const double*)h->st_mean, (const double*)h->st_std, ob, len, mean, std, max_obs, min_obs,
-                     first_update);
+  hipStream_t st = S(stream);
+  const size_t lds1 = sizeof(uint32_t) * (((ob * 256 + 1) & ~1)) + sizeof(double) * 16 * 16 * 2;
+  hipLaunchKernelGGL(k_stats_p1, dim3(nblk), dim3(256), lds1, st, h->d, len, h->st_hist, h->st_part);
+  hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, h->st_hist, nblk, ob, 0, ob, 24, 1,
+                     (const double*)h->st_part, len, h->st_state, h->st_mean, max_obs, min_obs, first_update);
+  hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std);
+  for (int col0 = 0; col0 < ob; col0 += G) {
+    const int nc = std::min(G, ob - col0);
+    for (int shift = 16; shift >= 0; shift -= 8) {
+      hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * 3), dim3(256), sizeof(uint32_t) * nc * 4 * 256, st, h->d, len,
+                         col0, nc, shift, (const uint32_t*)h->st_state, h->st_hist);
+      hipLaunchKernelGGL(k_stats_sel, dim3(nc), dim3(256), 0, st, h->st_hist, nblk, ob, col0, nc,
+                         shift, 0, (const double*)nullptr, len, h->st_state, h->st_mean, max_obs, min_obs,
+                         first_update);
+    }
+  }
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

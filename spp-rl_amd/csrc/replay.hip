@@ -93,121 +93,239 @@ __device__ __forceinline__ float funkey(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// column sums (pass 0) / centred square sums (pass 1) in fp64, per-block partials
-__global__ void k_stats_moments(ReplayDev r, int64_t len, const double* mean, double* part, int pass) {
-  extern __shared__ double sred[];  // [blockDim.x]
-  const int ob = r.ob;
-  for (int c = 0; c < ob; ++c) {
-    double s = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
-      const double x = (double)r.obs[r.obs_idx[i] * ob + c];
-      if (pass == 0) s += x;
-      else {
-        const double d = x - mean[c];
-        s += d * d;
-      }
-    }
-    sred[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) sred[threadIdx.x] += sred[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * ob + c] = sred[0];
-    __syncthreads();
+// Exact order statistics by 4-pass 8-bit radix select over the fp32 keys, for the
+// 4 ranks of each column: lo / hi of the 99th percentile, lo / hi of the 1st.
+// state[(c*4 + q)*3 + {0,1,2}] = {prefix, mask, rank remaining}.
+//
+// Pass 1 (k_stats_p1): one read of every live row: shifted fp64 moments
+// (pivot = the first live row; var = E[(x-p)^2] - E[x-p]^2) and the top-byte
+// histogram, shared by the 4 ranks (empty prefix).  Threads (ty, tx) of a
+// 16x16 block take column tx (+16 j) of rows ty (+16 k): 64 B runs per row.
+// Passes 2-4 (k_stats_pk): per-rank histograms of the next byte among the rows
+// that match each rank's prefix.  k_stats_sel: one workgroup per column sums
+// the per-block slabs, picks each rank's digit and, after the last byte, writes
+// numpy's 'linear' percentile, running max / min and mean / std.
+constexpr int kStatsBlocks = 1024;      // pass-1 workgroups (moment partials)
+constexpr int kStatsColsPerThread = 8;  // columns per tx lane (ob <= 128)
+constexpr int kStatsRows = 8;           // rows in flight per thread (index then row loads)
+
+// Non-zero LDS bins -> the global histogram (device atomics; sparse after pass 1).
+__device__ __forceinline__ void flush_hist(const uint32_t* sh, int n, uint32_t* g) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = sh[i];
+    if (v) atomicAdd(&g[i], v);
   }
-}
-__global__ void k_stats_reduce(const double* part, int nblk, int ob, int64_t len, double* out, int sqrt_out) {
-  const int c = threadIdx.x;
-  if (c >= ob) return;
-  double s = 0.0;
-  for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * ob + c];
-  s /= (double)len;
-  out[c] = sqrt_out ? sqrt(s) : s;
 }
 
-// Radix select, 8 bits per pass, for 4 ranks per column:
-// state[c*4 + q] = {prefix, mask, rank_remaining} (uint32 x3, rank fits 32 bits)
-__global__ void k_stats_hist(ReplayDev r, int64_t len, int col0, int ncols, int shift, const uint32_t* state,
-                             uint32_t* hist /*[nblk][ncols][4][256]*/) {
-  extern __shared__ uint32_t sh[];  // [ncols][4][256]
-  const int nb = ncols * 4 * 256;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) sh[i] = 0;
-  __syncthreads();
+__global__ __launch_bounds__(256) void k_stats_p1(ReplayDev r, int64_t len, uint32_t* __restrict__ ghist,
+                                                  double* __restrict__ part) {
+  extern __shared__ uint32_t sh1[];  // [ob][256] + reduction scratch
   const int ob = r.ob;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
-    const float* row = r.obs + r.obs_idx[i] * ob + col0;
-    for (int c = 0; c < ncols; ++c) {
-      const uint32_t k = fkey(row[c]);
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  for (int i = threadIdx.x; i < ob * 256; i += blockDim.x) sh1[i] = 0;
+  __syncthreads();
+  const float* p0 = r.obs + r.obs_idx[0] * ob;
+  double s1[kStatsColsPerThread], s2[kStatsColsPerThread];
+  float piv[kStatsColsPerThread];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t* st = state + ((col0 + c) * 4 + q) * 3;
-        if ((k & st[1]) == st[0]) atomicAdd(&sh[(c * 4 + q) * 256 + ((k >> shift) & 255)], 1u);
-      }
+  for (int j = 0; j < kStatsColsPerThread; ++j) {
+    s1[j] = s2[j] = 0.0;
+    const int c = tx + 16 * j;
+    piv[j] = c < ob ? p0[c] : 0.f;
+  }
+  const int64_t stride = (int64_t)gridDim.x * 16;
+  for (int64_t i0 = (int64_t)blockIdx.x * 16 + ty; i0 < len; i0 += stride * kStatsRows) {
+    int64_t base[kStatsRows];
+#pragma unroll
+    for (int k = 0; k < kStatsRows; ++k) {
+      const int64_t i = i0 + k * stride;
+      base[k] = i < len ? r.obs_idx[i] * ob : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kStatsColsPerThread; ++j) {
+      const int c = tx + 16 * j;
+      if (c >= ob) break;
+      float x[kStatsRows];
+#pragma unroll
+      for (int k = 0; k < kStatsRows; ++k) x[k] = base[k] >= 0 ? r.obs[base[k] + c] : 0.f;
+#pragma unroll
+      for (int k = 0; k < kStatsRows; ++k)
+        if (base[k] >= 0) {
+          const double d = (double)x[k] - (double)piv[j];
+          s1[j] += d;
+          s2[j] += d * d;
+          atomicAdd(&sh1[c * 256 + (fkey(x[k]) >> 24)], 1u);
+        }
     }
   }
   __syncthreads();
-  uint32_t* out = hist + (int64_t)blockIdx.x * nb;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) out[i] = sh[i];
-}
-// one workgroup (256 threads) per (column, rank)
-__global__ void k_stats_select(const uint32_t* hist, int nblk, int col0, int ncols, int shift, uint32_t* state) {
-  __shared__ uint32_t cnt[256];
-  const int cq = blockIdx.x;  // local (c, q)
-  const int nb = ncols * 4 * 256;
-  uint32_t s = 0;
-  for (int k = 0; k < nblk; ++k) s += hist[(int64_t)k * nb + cq * 256 + threadIdx.x];
-  cnt[threadIdx.x] = s;
+  flush_hist(sh1, ob * 256, ghist);
+  // moments: reduce over ty (16 rows of threads) through LDS, per column
+  double* red = reinterpret_cast<double*>(sh1 + ((ob * 256 + 1) & ~1));
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t* st = state + (col0 * 4 + cq) * 3;
-    uint32_t rank = st[2], acc = 0;
+#pragma unroll
+  for (int j = 0; j < kStatsColsPerThread; ++j) {
+    const int c = tx + 16 * j;
+    if (16 * j >= ob) break;
+    red[(ty * 16 + tx) * 2 + 0] = s1[j];
+    red[(ty * 16 + tx) * 2 + 1] = s2[j];
+    __syncthreads();
+    if (ty == 0 && c < ob) {
+      double a = 0.0, b = 0.0;
+      for (int y = 0; y < 16; ++y) {
+        a += red[(y * 16 + tx) * 2 + 0];
+        b += red[(y * 16 + tx) * 2 + 1];
+      }
+      part[((int64_t)blockIdx.x * ob + c) * 2 + 0] = a;
+      part[((int64_t)blockIdx.x * ob + c) * 2 + 1] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// Passes 2-4 for columns [col0, col0 + ncols): per-rank histograms of byte `shift`.
+__global__ __launch_bounds__(256) void k_stats_pk(ReplayDev r, int64_t len, int col0, int ncols, int shift,
+                                                  const uint32_t* __restrict__ state, uint32_t* __restrict__ ghist) {
+  extern __shared__ uint32_t shk[];  // [ncols][4][256]
+  const int ob = r.ob;
+  const int nb = ncols * 4 * 256;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) shk[i] = 0;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  uint32_t pre[kStatsColsPerThread][4], msk[kStatsColsPerThread][4];
+#pragma unroll
+  for (int j = 0; j < kStatsColsPerThread; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = tx + 16 * j;
+      pre[j][q] = c < ncols ? state[((col0 + c) * 4 + q) * 3 + 0] : 0u;
+      msk[j][q] = c < ncols ? state[((col0 + c) * 4 + q) * 3 + 1] : 0u;
+    }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 16;
+  for (int64_t i0 = (int64_t)blockIdx.x * 16 + ty; i0 < len; i0 += stride * kStatsRows) {
+    int64_t base[kStatsRows];
+#pragma unroll
+    for (int k = 0; k < kStatsRows; ++k) {
+      const int64_t i = i0 + k * stride;
+      base[k] = i < len ? r.obs_idx[i] * ob + col0 : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kStatsColsPerThread; ++j) {
+      const int c = tx + 16 * j;
+      if (c >= ncols) break;
+      uint32_t kk[kStatsRows];
+#pragma unroll
+      for (int k = 0; k < kStatsRows; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
+#pragma unroll
+      for (int k = 0; k < kStatsRows; ++k)
+        if (base[k] >= 0)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if ((kk[k] & msk[j][q]) == pre[j][q])
+              atomicAdd(&shk[(c * 4 + q) * 256 + ((kk[k] >> shift) & 255)], 1u);
+    }
+  }
+  __syncthreads();
+  flush_hist(shk, nb, ghist);
+}
+
+// One workgroup (256 threads = bins) per column of the group; consumes (and
+// re-zeroes) the global histogram.  first: one shared [ob][256] histogram
+// (pass 1) and the moment partials are reduced too.
+__global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist, int nblk, int ob, int col0,
+                                                   int ncols, int shift, int first, const double* __restrict__ part,
+                                                   int64_t len, uint32_t* __restrict__ state, double* __restrict__ mom,
+                                                   float* max_out, float* min_out, int first_update) {
+  __shared__ uint32_t cnt[4][256];
+  __shared__ double rd[2][256];
+  const int c = col0 + blockIdx.x, t = threadIdx.x;
+  for (int q = 0; q < (first ? 1 : 4); ++q) {
+    const int64_t off = first ? (int64_t)c * 256 + t : ((int64_t)blockIdx.x * 4 + q) * 256 + t;
+    cnt[q][t] = ghist[off];
+    ghist[off] = 0;
+  }
+  if (first) {
+    // fp64 moments of column c (shifted by the pivot)
+    double a = 0.0, b = 0.0;
+    for (int k = t; k < nblk; k += 256) {
+      a += part[((int64_t)k * ob + c) * 2 + 0];
+      b += part[((int64_t)k * ob + c) * 2 + 1];
+    }
+    rd[0][t] = a;
+    rd[1][t] = b;
+  }
+  __syncthreads();
+  if (first) {
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) {
+        rd[0][t] += rd[0][t + o];
+        rd[1][t] += rd[1][t + o];
+      }
+      __syncthreads();
+    }
+  }
+  if (t < 4) {
+    const int q = t;
+    uint32_t* st = state + (c * 4 + q) * 3;
+    uint32_t rank;
+    if (first) {  // ranks of np.percentile's lerp neighbours: floor((len-1) q) and the next
+      const double qq = q < 2 ? 0.99 : 0.01;
+      const int64_t lo = (int64_t)floor((double)(len - 1) * qq);
+      const int64_t v = (q & 1) ? (lo + 1 < len ? lo + 1 : len - 1) : lo;
+      rank = (uint32_t)v;
+      st[0] = st[1] = 0;
+    } else {
+      rank = st[2];
+    }
+    const uint32_t* h = cnt[first ? 0 : q];
+    uint32_t acc = 0;
     int bin = 255;
     for (int d = 0; d < 256; ++d) {
-      if (acc + cnt[d] > rank) { bin = d; break; }
-      acc += cnt[d];
+      if (acc + h[d] > rank) {
+        bin = d;
+        break;
+      }
+      acc += h[d];
     }
     st[0] |= (uint32_t)bin << shift;
     st[1] |= 255u << shift;
     st[2] = rank - acc;
   }
-}
-// final: numpy 'linear' percentile lerp, fp32 cast, running max/min, mean/std cast
-__global__ void k_stats_finish(const uint32_t* state, const double* mean, const double* std, int ob, int64_t len,
-                               float* mean_out, float* std_out, float* max_out, float* min_out, int first) {
-  const int c = threadIdx.x;
-  if (c >= ob) return;
-  double res[2];
-  const double qs[2] = {0.99, 0.01};
-  for (int k = 0; k < 2; ++k) {
-    const double vi = (double)(len - 1) * qs[k];
-    const double lo = floor(vi);
-    const double g = vi - lo;
-    const double a = (double)funkey(state[(c * 4 + 2 * k) * 3 + 0]);
-    const double b = (double)funkey(state[(c * 4 + 2 * k + 1) * 3 + 0]);
-    const double diff = b - a;
-    res[k] = g >= 0.5 ? b - diff * (1.0 - g) : a + diff * g;
+  if (first && t == 0) {
+    const double n = (double)len;
+    const double m1 = rd[0][0] / n;
+    const double var = fmax(rd[1][0] / n - m1 * m1, 0.0);
+    mom[c * 2 + 0] = m1;  // mean - pivot (the pivot is added by k_stats_moments_out)
+    mom[c * 2 + 1] = sqrt(var);
   }
-  const float cmax = (float)res[0], cmin = (float)res[1];
-  mean_out[c] = (float)mean[c];
-  std_out[c] = (float)std[c];
-  max_out[c] = first ? cmax : fmaxf(cmax, max_out[c]);
-  min_out[c] = first ? cmin : fminf(cmin, min_out[c]);
-}
-__global__ void k_stats_init(uint32_t* state, int ob, int64_t len) {
-  const int c = threadIdx.x;
-  if (c >= ob) return;
-  const double qs[2] = {0.99, 0.01};
-  for (int k = 0; k < 2; ++k) {
-    const int64_t lo = (int64_t)floor((double)(len - 1) * qs[k]);
-    const int64_t hi = lo + 1 < len ? lo + 1 : len - 1;
-    uint32_t* a = state + (c * 4 + 2 * k) * 3;
-    uint32_t* b = state + (c * 4 + 2 * k + 1) * 3;
-    a[0] = a[1] = 0;
-    a[2] = (uint32_t)lo;
-    b[0] = b[1] = 0;
-    b[2] = (uint32_t)hi;
+  if (shift == 0) {
+    __syncthreads();
+    if (t == 0) {
+      double res[2];
+      const double qs[2] = {0.99, 0.01};
+      for (int k = 0; k < 2; ++k) {
+        const double vi = (double)(len - 1) * qs[k];
+        const double lo = floor(vi);
+        const double g = vi - lo;
+        const double a = (double)funkey(state[(c * 4 + 2 * k) * 3 + 0]);
+        const double b = (double)funkey(state[(c * 4 + 2 * k + 1) * 3 + 0]);
+        const double diff = b - a;
+        res[k] = g >= 0.5 ? b - diff * (1.0 - g) : a + diff * g;  // numpy _lerp
+      }
+      const float cmax = (float)res[0], cmin = (float)res[1];
+      max_out[c] = first_update ? cmax : fmaxf(cmax, max_out[c]);
+      min_out[c] = first_update ? cmin : fminf(cmin, min_out[c]);
+    }
   }
+}
+
+// mean = pivot + E[x - pivot]; std from the shifted moments (fp32 casts, replay_buffer.py:87-90)
+__global__ void k_stats_moments_out(ReplayDev r, const double* mom, float* mean_out, float* std_out) {
+  const int c = threadIdx.x;
+  if (c >= r.ob) return;
+  const double piv = (double)r.obs[r.obs_idx[0] * r.ob + c];
+  mean_out[c] = (float)(piv + mom[c * 2 + 0]);
+  std_out[c] = (float)mom[c * 2 + 1];
 }
 
 // ---------------------------------------------------------------- RNG

@@ -298,6 +298,9 @@ sppStatus sppOnpAct(sppOnPolicyHandle h, const float* x, int N, const float* eps
 sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y, int B, int K, int N, int act,
                         void* stream);
 
+/* Profiling builds only (-DSPP_PROF): per-region s_memtime totals of the phase kernels. */
+sppStatus sppDebugReadProf(unsigned long long* out64 /*[64]*/, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,13 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, prof=False, hopper_only=False):
+    if prof:  # region-timing variant (never the default library)
+        out = os.path.join(HERE, "spprl", "libspprl_prof.so")
+        extra = ["-DSPP_ONLY_HOPPER"] if hopper_only else []
+        cmd = [HIPCC] + FLAGS + ["-DSPP_PROF"] + extra + ["-o", out, os.path.join(CSRC, "api.hip")]
+        subprocess.check_call(cmd)
+        return out
     if not force and up_to_date():
         if verbose:
             print("libspprl.so up to date")
@@ -41,4 +47,4 @@ def build(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, prof="--prof" in sys.argv, hopper_only="--hopper-only" in sys.argv)

@@ -450,12 +450,14 @@ static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, KernelSet* 
   }
   if (algo == SPP_ALGO_SAC_ACM) {
     SPP_KS(11, 11, 3)   // Hopper-v2
+#ifndef SPP_ONLY_HOPPER  // kernel-development builds: one instantiation, fast compile
     SPP_KS(17, 17, 6)   // HalfCheetah-v2
     SPP_KS(111, 111, 8) // Ant
     SPP_KS(3, 3, 1)     // Pendulum-v0 (tests)
   } else if (algo == SPP_ALGO_DDPG_ACM) {
     SPP_DKS(17, 17, 6)  // HalfCheetah-v2 (SPP-DDPG, train/spp_ddpg_hcheetah.py)
     SPP_DKS(11, 11, 3)  // Hopper-v2
+#endif
   }
 #undef SPP_KS
 #undef SPP_DKS
@@ -1812,3 +1814,21 @@ sppStatus sppOnpAct(sppOnPolicyHandle o, const float* x, int N, const float* eps
 }
 
 }  // extern "C"
+
+extern "C" sppStatus sppDebugReadProf(unsigned long long* out64, int reset) {
+#ifdef SPP_PROF
+  SPP_REQUIRE(out64, SPP_E_INVALID_ARG, "null");
+  SPP_CHECK_HIP(hipDeviceSynchronize());
+  SPP_CHECK_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_tprof), sizeof(unsigned long long) * 64));
+  if (reset) {
+    unsigned long long z[64] = {};
+    SPP_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tprof), z, sizeof(z)));
+  }
+  return SPP_OK;
+#else
+  (void)out64;
+  (void)reset;
+  set_error("region profiling is only compiled into profiling builds (build.py --prof)");
+  return SPP_E_STATE;
+#endif
+}

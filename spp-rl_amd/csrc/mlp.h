@@ -17,6 +17,38 @@
 
 namespace spp {
 
+// Region timing of the phase kernels (profiling builds only, -DSPP_PROF): each
+// wave accumulates s_memtime deltas per region in LDS, flushed to g_tprof.
+#ifdef SPP_PROF
+__device__ unsigned long long g_tprof[64];
+__shared__ unsigned long long s_tprof[4][32];
+__shared__ unsigned long long s_tlast[4];
+#define SPP_TP_INIT()                                                            \
+  {                                                                              \
+    const int w_ = threadIdx.x >> 6;                                             \
+    if ((threadIdx.x & 63) < 32) s_tprof[w_][threadIdx.x & 63] = 0;              \
+    if ((threadIdx.x & 63) == 0) s_tlast[w_] = clock64();                        \
+  }
+#define SPP_TP(k)                                                                \
+  {                                                                              \
+    const unsigned long long t_ = clock64();                                     \
+    const int w_ = threadIdx.x >> 6;                                             \
+    if ((threadIdx.x & 63) == 0 && w_ < 4) {                                     \
+      s_tprof[w_][k] += t_ - s_tlast[w_];                                        \
+      s_tlast[w_] = t_;                                                          \
+    }                                                                            \
+  }
+#define SPP_TP_FLUSH()                                                           \
+  {                                                                              \
+    const int w_ = threadIdx.x >> 6, l_ = threadIdx.x & 63;                      \
+    if (l_ < 32) atomicAdd(&g_tprof[l_], s_tprof[w_][l_]);                       \
+  }
+#else
+#define SPP_TP_INIT()
+#define SPP_TP(k)
+#define SPP_TP_FLUSH()
+#endif
+
 // ---------------------------------------------------------------- layout maps
 // How (block, register, half) positions of a tile map to logical indices of a
 // vector.  Used by the pack kernels (device) and by loaders.
@@ -155,14 +187,30 @@ __device__ __forceinline__ f32x16 bias_tile(const float* biasL, int ob, int h) {
   return acc;
 }
 
+// Weight fragments through a buffer resource: wave-uniform byte offset in
+// soffset (pinned in an SGPR), the lane's 16 B slot in ONE shared voffset VGPR,
+// so no per-layer 64-bit lane addresses exist to be hoisted out of the tile loop.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t rsrc_n(const void* p, int nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nbytes, 0x00020000);
+}
+__device__ __forceinline__ rsrc_t rsrc(const void* p) { return rsrc_n(p, 0x7fffffff); }
+__device__ __forceinline__ float4 wfrag(rsrc_t w, uint32_t lane16, int off) {
+  asm volatile("" : "+s"(off));
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(w, lane16, off, 0));
+}
+
 // Register-input layer (small K): out blocks ob = 0..NBO-1 (runtime), acc
-// initialised from the LDS bias table (NULL -> 0), epi(ob, acc) consumes each
+// initialised from the LDS bias table (nullptr -> 0), epi(ob, acc) consumes each
 // block.  Weight image ob-major: Wf[((ob*NBI + ib)*4 + rq)*64 + lane].
 // Weight fragments stream through a 2-deep register ring of CH float4 so the
 // next chunk's loads are in flight while the current chunk's MFMAs issue.
-template <int NBI, uint64_t RV, typename Epi>
-__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
-                                      const float* biasL, Epi&& epi) {
+// Software-pipelined by one block: block ob's MFMA chain is issued before block
+// ob-1's epilogue, so the epilogue's VALU / LDS / store work fills the chain's
+// MFMA issue gaps instead of serialising behind it.
+template <int NBI, uint64_t RV, bool BIAS, typename Epi>
+__device__ __forceinline__ void dense_impl(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
+                                           const float* biasL, Epi&& epi) {
   constexpr int NQ = rv_total(RV, NBI);
   static_assert(NQ > 0, "empty layer");
   constexpr int CH = chunk_of(NQ);
@@ -170,25 +218,27 @@ __device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, co
   static_assert(NQ % CH == 0, "chunking");
   const int lane = lane_id();
   const int h = lane >> 5;
-  const float4* wl = Wf + lane;
-  constexpr int OBSTRIDE = NBI * 4 * 64;
+  const rsrc_t wr = rsrc(Wf);
+  const uint32_t l16 = 16u * lane;
+  constexpr int OBSTRIDE = NBI * 4 * 64 * 16;  // bytes per output block
   float4 cur[CH];
   static_for<0, CH>([&](auto I) {
     constexpr int q = decltype(I)::value;
-    cur[q] = wl[(q_ib(RV, NBI, q) * 4 + q_rq(RV, NBI, q)) * 64];
+    cur[q] = wfrag(wr, l16, (q_ib(RV, NBI, q) * 4 + q_rq(RV, NBI, q)) * 1024);
   });
-#pragma unroll 1
-  for (int ob = 0; ob < NBO; ++ob) {
-    f32x16 acc = biasL ? bias_tile(biasL, ob, h) : zero16();
+  auto chain = [&](int ob) {
+    f32x16 acc;
+    if constexpr (BIAS) acc = bias_tile(biasL, ob, h);
+    else acc = zero16();
     const int obn = ob + 1 < NBO ? ob + 1 : ob;
     static_for<0, NC>([&](auto C) {
       constexpr int c = decltype(C)::value;
       constexpr int nc = (c + 1 < NC) ? c + 1 : 0;
-      const float4* wn = wl + (size_t)((c + 1 < NC) ? ob : obn) * OBSTRIDE;
+      const int wn = ((c + 1 < NC) ? ob : obn) * OBSTRIDE;
       float4 nxt[CH];
       static_for<0, CH>([&](auto I) {
         constexpr int q = nc * CH + decltype(I)::value;
-        nxt[decltype(I)::value] = wn[(q_ib(RV, NBI, q) * 4 + q_rq(RV, NBI, q)) * 64];
+        nxt[decltype(I)::value] = wfrag(wr, l16, wn + (q_ib(RV, NBI, q) * 4 + q_rq(RV, NBI, q)) * 1024);
       });
       static_for<0, CH>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -203,8 +253,29 @@ __device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, co
 #pragma unroll
       for (int i = 0; i < CH; ++i) cur[i] = nxt[i];
     });
-    epi(ob, acc);
+    return acc;
+  };
+  SPP_TP(23);
+  f32x16 prev = chain(0);
+#pragma unroll 1
+  for (int ob = 1; ob < NBO; ++ob) {
+    const f32x16 acc = chain(ob);
+    epi(ob - 1, prev);
+    prev = acc;
   }
+  SPP_TP(24);
+  epi(NBO - 1, prev);
+  SPP_TP(25);
+}
+template <int NBI, uint64_t RV, typename Epi>
+__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
+                                      const float* biasL, Epi&& epi) {
+  dense_impl<NBI, RV, true>(Wf, NBO, in, biasL, static_cast<Epi&&>(epi));
+}
+template <int NBI, uint64_t RV, typename Epi>
+__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI], decltype(nullptr),
+                                      Epi&& epi) {
+  dense_impl<NBI, RV, false>(Wf, NBO, in, nullptr, static_cast<Epi&&>(epi));
 }
 
 constexpr int cgcd(int a, int b) { return b ? cgcd(b, a % b) : a; }
@@ -214,13 +285,16 @@ constexpr int cgcd(int a, int b) { return b ? cgcd(b, a % b) : a; }
 // (acc[NBO] lives in the accumulation registers), input blocks streamed in the
 // outer loop.  Weight image ib-major: Wf[((ib*NBO + ob)*4 + rq)*64 + lane], so
 // the whole layer is ONE linear stream of 1 KiB fragments, consumed in chunks
-// of CH float4 through a D-deep register ring: chunk g+D-1's loads are issued
-// (pinned by a scheduling barrier) before chunk g's MFMAs, i.e. (D-1)*CH*4
-// MFMAs of latency cover per load.  epi(ob, acc) runs once per block after the
-// last input block, so it may overwrite img.
-template <int NBO, typename Epi>
-__device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, const float* biasL,
-                                          Epi&& epi) {
+// of CH float4 (= one (input block, output block) pair) through a D-deep
+// register ring: chunk g+D-1's loads are issued (pinned by a scheduling
+// barrier) before chunk g's MFMAs, i.e. (D-1)*CH*4 MFMAs of latency cover per
+// load.  The last input block is peeled: output block ob is final after its
+// chunk there, and its epilogue epi(ob, acc) is issued together with block
+// ob+1's MFMAs.  All image reads happen before the peeled block, so epi may
+// overwrite img.
+template <int NBO, bool BIAS, typename Epi>
+__device__ __forceinline__ void dense_lds_impl(const float4* __restrict__ Wf, const float* img, const float* biasL,
+                                               Epi&& epi) {
   constexpr int NQ = NBO * 4;               // float4 per input block
   constexpr int CH = 4;                     // float4 per chunk
   constexpr int NCI = NQ / CH;              // chunks per input block (= NBO)
@@ -233,50 +307,71 @@ __device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const f
   const int lane = lane_id();
   const int h = lane >> 5;
   const float* l = img + 4 * h * 32 + (lane & 31);
-  const float4* wl = Wf + lane;
+  const rsrc_t wr = rsrc(Wf);
+  const uint32_t l16 = 16u * lane;
   f32x16 acc[NBO];
-  static_for<0, NBO>([&](auto O) { acc[O] = biasL ? bias_tile(biasL, O, h) : zero16(); });
+  static_for<0, NBO>([&](auto O) {
+    if constexpr (BIAS) acc[O] = bias_tile(biasL, O, h);
+    else acc[O] = zero16();
+  });
   float4 ring[D][CH];
   static_for<0, D - 1>([&](auto I) {
-    static_for<0, CH>([&](auto J) { ring[I][J] = wl[((int)I * CH + (int)J) * 64]; });
+    static_for<0, CH>([&](auto J) { ring[I][J] = wfrag(wr, l16, ((int)I * CH + (int)J) * 1024); });
   });
   f32x16 xin[IBU];
   static_for<0, IBU>([&](auto K) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) xin[K][r] = l[(32 * (int)K + ru(r)) * 32];
   });
+  // chunk u of iteration it: refill the ring D-1 chunks ahead, then its MFMAs
+  auto step = [&](auto UC, int it) {
+    constexpr int u = UC;
+    constexpr int sn = (u + D - 1) % D;
+    const int gn = it * U + u + D - 1;
+    if (gn < G) {
+      static_for<0, CH>([&](auto J) { ring[sn][J] = wfrag(wr, l16, (gn * CH + (int)J) * 1024); });
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int s = u % D;
+    constexpr int kb = u / NCI;
+    constexpr int ob = u % NCI;
+    static_for<0, CH>([&](auto J) {
+      constexpr int rq = J;
+      acc[ob] = mfma(ring[s][J].x, xin[kb][4 * rq + 0], acc[ob]);
+      acc[ob] = mfma(ring[s][J].y, xin[kb][4 * rq + 1], acc[ob]);
+      acc[ob] = mfma(ring[s][J].z, xin[kb][4 * rq + 2], acc[ob]);
+      acc[ob] = mfma(ring[s][J].w, xin[kb][4 * rq + 3], acc[ob]);
+    });
+  };
+  SPP_TP(20);
 #pragma unroll 1
-  for (int it = 0; it < NIT; ++it) {
-    const int itn = it + 1 < NIT ? it + 1 : it;
+  for (int it = 0; it < NIT - 1; ++it) {
     f32x16 xnx[IBU];
     static_for<0, IBU>([&](auto K) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xnx[K][r] = l[(32 * (itn * IBU + (int)K) + ru(r)) * 32];
+      for (int r = 0; r < 16; ++r) xnx[K][r] = l[(32 * ((it + 1) * IBU + (int)K) + ru(r)) * 32];
     });
-    static_for<0, U>([&](auto UC) {
-      constexpr int u = UC;
-      constexpr int sn = (u + D - 1) % D;
-      const int gn = it * U + u + D - 1;
-      if (gn < G) {
-        const float4* wn = wl + (size_t)gn * (CH * 64);
-        static_for<0, CH>([&](auto J) { ring[sn][J] = wn[(int)J * 64]; });
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      constexpr int s = u % D;
-      static_for<0, CH>([&](auto J) {
-        constexpr int f = u * CH + J;
-        constexpr int kb = f / NQ;
-        constexpr int ob = (f % NQ) / 4;
-        constexpr int rq = f % 4;
-        acc[ob] = mfma(ring[s][J].x, xin[kb][4 * rq + 0], acc[ob]);
-        acc[ob] = mfma(ring[s][J].y, xin[kb][4 * rq + 1], acc[ob]);
-        acc[ob] = mfma(ring[s][J].z, xin[kb][4 * rq + 2], acc[ob]);
-        acc[ob] = mfma(ring[s][J].w, xin[kb][4 * rq + 3], acc[ob]);
-      });
-    });
+    static_for<0, U>([&](auto UC) { step(UC, it); });
     static_for<0, IBU>([&](auto K) { xin[K] = xnx[K]; });
   }
-  static_for<0, NBO>([&](auto O) { epi(O, acc[O]); });
+  static_for<0, U>([&](auto UC) {
+    step(UC, NIT - 1);
+    constexpr int u = UC;
+    if constexpr (u / NCI == IBU - 1 && u % NCI >= 1) epi(IC<u % NCI - 1>{}, acc[u % NCI - 1]);
+  });
+  SPP_TP(21);
+  epi(IC<NBO - 1>{}, acc[NBO - 1]);
+  SPP_TP(22);
+}
+template <int NBO, typename Epi>
+__device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, const float* biasL,
+                                          Epi&& epi) {
+  dense_lds_impl<NBO, true>(Wf, img, biasL, static_cast<Epi&&>(epi));
+}
+template <int NBO, typename Epi>
+__device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, decltype(nullptr),
+                                          Epi&& epi) {
+  dense_lds_impl<NBO, false>(Wf, img, nullptr, static_cast<Epi&&>(epi));
 }
 
 // ---------------------------------------------------------------- loaders / stores
@@ -303,11 +398,6 @@ __device__ __forceinline__ void lds_load(f32x16 (&t)[NB], const float* lds) {
 // array's byte size) put it in voffset so the hardware range check returns 0 /
 // drops the access for rows past the array (raw-buffer checks exclude soffset).
 // Byte offsets stay below 2^31 (asserted on the host).
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-__device__ __forceinline__ rsrc_t rsrc_n(const void* p, int nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nbytes, 0x00020000);
-}
-__device__ __forceinline__ rsrc_t rsrc(const void* p) { return rsrc_n(p, 0x7fffffff); }
 __device__ __forceinline__ int soff(int row, int ld4) {
   int so = row * ld4;
   asm volatile("" : "+s"(so));

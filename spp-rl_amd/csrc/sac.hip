@@ -43,6 +43,7 @@ struct Cfg {
 };
 
 constexpr int kWavesPerWG = 4;
+
 constexpr int kLdsPerWave = 256 * 32;  // BIG [256][32] floats
 constexpr int kSmallRow = 192;         // SMALL [64][32] = BIG rows 192..255
 
@@ -196,6 +197,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
       setbits(m1lo, m1hi, ob, bits);
     });
   }
+  SPP_TP(1);
   {
     const rsrc_t hr = rsrc(H2g);
     dense_lds<8>(A.W2, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
@@ -211,6 +213,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
       setbits(m2lo, m2hi, ob, bits);
     });
   }
+  SPP_TP(2);
   {
     dense_lds<NBH>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
 #pragma unroll
@@ -220,6 +223,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
       }
     });
   }
+  SPP_TP(3);
 }
 
 // ACM forward (basic_model.py:118-126): in [s | a_d] -> tanh 64 -> tanh 32 -> tanh(ac)*lim.
@@ -265,7 +269,7 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
 
 // Critic forward through L2 with q = w3 . relu(h2) + b3 reduced per sample.
 // ST: store h1 / h2 feature-major.
-template <class C, bool ST>
+template <class C, bool ST, int R = 30>
 __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN], const Lane& L,
                                                 float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
                                                 uint64_t& m2lo, uint64_t& m2hi) {
@@ -282,6 +286,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
     }
     setbits(m1lo, m1hi, ob, bits);
   });
+  SPP_TP(R);
   float qp = 0.f;
   const float* w3 = L.tbl + Q.tw3;
   dense_lds<8>(Q.W2, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
@@ -295,6 +300,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
     }
     setbits(m2lo, m2hi, ob, bits);
   });
+  SPP_TP(R + 1);
   return qp + __shfl_xor(qp, 32, 64) + *Q.b3;
 }
 
@@ -336,6 +342,7 @@ template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  SPP_TP_INIT();
   load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
@@ -349,6 +356,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     const bool valid = b < p.B;
     uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
     // ---- target action: a' ~ pi(s'), a'_d, logpi'   (sac_acm.py:44-45)
+    SPP_TP(0);
     actor_trunk<C, false>(p.actor, p.S2, C::OB * L.ld4, L, nullptr, nullptr, d0, d1, d2, d3);
 #ifdef SPP_CUT
     if (SPP_CUT == 1) { p.part[tile] = L.bl[0]; continue; }
@@ -359,6 +367,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       load_pair<C>(hd, big);
       lp2 = squash_write<C>(p, hd, p.EPS1, L);
     }
+    SPP_TP(4);
     // ---- critic-target input: [s' | ACM(s', a'_d)] or [s' | a'_d]   (:46-48)
     f32x16 tin[C::NB_CIN];
     if constexpr (C::ACMC) {
@@ -373,8 +382,9 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     if (SPP_CUT == 2) { p.part[tile] = L.bl[0] + tin[0][3] + lp2; continue; }
 #endif
     // ---- soft-min twin target (:50-56)
-    const float q1t = critic_forward<C, false>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
-    const float q2t = critic_forward<C, false>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    SPP_TP(5);
+    const float q1t = critic_forward<C, false, 6>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
+    const float q2t = critic_forward<C, false, 8>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
     const float notdone = 1.f - p.DN[b];
     const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
 #ifdef SPP_CUT
@@ -388,7 +398,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       f32x16 xin[C::NB_CIN];
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
-      const float q = critic_forward<C, true>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
+      SPP_TP(10);
+      const float q = critic_forward<C, true, 11>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;  // d mse / dq
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
@@ -410,6 +421,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
           fm_st(d2r, ur, L.ld4, L.vo, v);
         }
       }
+      SPP_TP(13);
       // delta1 = (W2^T delta2) * relu'(h1)
       const rsrc_t d1r = rsrc(p.D1[i]);
       dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
@@ -418,12 +430,15 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
           fm_st(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
       });
     }
+    SPP_TP(14);
     const float s0 = wave_sum(lq0), s1 = wave_sum(lq1);
     if (lane == 0) {
       p.part[tile * kParts + 0] = s0;
       p.part[tile * kParts + 1] = s1;
     }
+    SPP_TP(15);
   }
+  SPP_TP_FLUSH();
 }
 
 // ============================================================================ actor phase
@@ -876,9 +891,9 @@ __global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const floa
     }
   };
   if constexpr (NBI == 8)
-    dense_lds<NBO>(Wf, img, bias ? tb : nullptr, epi);
+    dense_lds<NBO>(Wf, img, tb, epi);  // tb holds zeros without a bias
   else
-    dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, bias ? tb : nullptr, epi);
+    dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, tb, epi);
 }
 
 }  // namespace spp

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede the HIP library: shared runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libspprl.so")
+LIB_PATH = os.environ.get("SPPRL_LIB") or os.path.join(HERE, "libspprl.so")
 
 (SPP_NET_ACTOR, SPP_NET_CRITIC1, SPP_NET_CRITIC2, SPP_NET_CRITIC1_TARG, SPP_NET_CRITIC2_TARG, SPP_NET_ACM,
  SPP_NET_ACTOR_TARG) = range(7)
@@ -118,6 +118,7 @@ _SIGS = {
                             c_int, c_void_p, c_void_p, c_void_p]),
     "sppPpoClipLoss": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "sppAdvNormalize": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }
 EXPORTED = tuple(_SIGS)

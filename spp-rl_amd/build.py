@@ -1,20 +1,31 @@
-"""Build libspprl.so (gfx950) in-tree with hipcc.  Usage: python spp-rl_amd/build.py [--force]"""
+"""Build libspprl.so (gfx950) in-tree with hipcc.  Usage: python spp-rl_amd/build.py [--force]
+
+The library is one api.hip translation unit (C-ABI, non-template kernels) plus one
+translation unit per phase-kernel config family (csrc/ks_*.hip); they compile in
+parallel into build/ and link into spp-rl_amd/spprl/libspprl.so.
+"""
 import glob
 import os
 import subprocess
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "spprl", "libspprl.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(REPO, "include")]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include")]
 
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(REPO, "include", "spprl.h")]
+
+
+def units():
+    return [os.path.join(CSRC, "api.hip")] + sorted(glob.glob(os.path.join(CSRC, "ks_*.hip")))
 
 
 def up_to_date():
@@ -24,22 +35,39 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
-def build(force=False, verbose=True, prof=False, hopper_only=False):
-    if prof:  # region-timing variant (never the default library)
+def _compile(src, verbose):
+    obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
+    cmd = [HIPCC] + FLAGS + ["-c", "-o", obj, src]
+    t0 = time.time()
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stdout[-8000:]))
+    if verbose:
+        print("  %-22s %5.0fs" % (os.path.basename(src), time.time() - t0), flush=True)
+    return obj
+
+
+def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None):
+    if prof:  # region-timing variant (never the default library): single TU
         out = os.path.join(HERE, "spprl", "libspprl_prof.so")
         extra = ["-DSPP_ONLY_HOPPER"] if hopper_only else []
-        cmd = [HIPCC] + FLAGS + ["-DSPP_PROF"] + extra + ["-o", out, os.path.join(CSRC, "api.hip")]
+        cmd = [HIPCC] + FLAGS + ["-shared", "-DSPP_PROF", "-DSPP_SINGLE_TU"] + extra + [
+            "-o", out, os.path.join(CSRC, "api.hip")]
         subprocess.check_call(cmd)
         return out
     if not force and up_to_date():
         if verbose:
             print("libspprl.so up to date")
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", os.path.join(CSRC, "api.hip")]
+    os.makedirs(OBJ, exist_ok=True)
     t0 = time.time()
+    srcs = units()
+    jobs = jobs or min(len(srcs), max(1, min(os.cpu_count() or 1, 8)))
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+        print("hipcc %s  (%d units, %d jobs)" % (" ".join(FLAGS), len(srcs), jobs), flush=True)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs)
     os.replace(OUT + ".tmp", OUT)
     if verbose:
         print("built %s in %.0fs" % (OUT, time.time() - t0))

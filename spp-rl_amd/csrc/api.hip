@@ -19,6 +19,16 @@
 #include "replay.hip"
 #include "sac.hip"
 #include "ddpg.hip"
+#include "kset.h"
+#ifdef SPP_SINGLE_TU  // profiling / development builds: everything in one TU
+#include "ks_sac_hopper.hip"
+#ifndef SPP_ONLY_HOPPER
+#include "ks_sac_hcheetah.hip"
+#include "ks_sac_ant.hip"
+#include "ks_sac_small.hip"
+#include "ks_ddpg.hip"
+#endif
+#endif
 #include "onp.hip"
 
 namespace spp {
@@ -413,54 +423,19 @@ struct DwSet {
   void release() { slab.release(); jobs.release(); items.release(); }
 };
 
-// dims -> kernel instantiation
-struct KernelSet {
-  void (*critic)(SacArgs);
-  void (*actor)(SacArgs, AcmScratch);
-  void (*act)(SacArgs, ActArgs);
-  void (*acmreg)(SacArgs, AcmRegArgs);
-  // DDPG_AcM
-  void (*dcritic)(SacArgs, BAcmScratch);
-  void (*dactor)(SacArgs, BAcmScratch);
-  void (*dact)(SacArgs, ActArgs, BAcmScratch);
-  void (*dreg)(SacArgs, BAcmRegArgs);
-};
-template <int OB, int AOUT, int AC, bool ACMC>
-KernelSet make_kset() {
-  using C = Cfg<OB, AOUT, AC, ACMC>;
-  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>,
-          nullptr, nullptr, nullptr, nullptr};
-}
-template <int OB, int AOUT, int AC, bool ACMC>
-KernelSet make_dkset() {
-  using D = DCfg<OB, AOUT, AC, ACMC>;
-  return {nullptr, nullptr, nullptr, nullptr,
-          k_ddpg_critic_phase<D>, k_ddpg_actor_phase<D>, k_ddpg_policy_act<D>, k_bacm_regress<D>};
-}
+// dims -> kernel instantiation: one translation unit per config family (ks_*.hip),
+// compiled in parallel by build.py and linked into libspprl.so.
 static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, KernelSet* ks) {
-#define SPP_KS(o, a, c)                                                    \
-  if (ob == o && aout == a && ac == c) {                                   \
-    *ks = acmc ? make_kset<o, a, c, true>() : make_kset<o, a, c, false>(); \
-    return true;                                                           \
-  }
-#define SPP_DKS(o, a, c)                                                     \
-  if (ob == o && aout == a && ac == c) {                                     \
-    *ks = acmc ? make_dkset<o, a, c, true>() : make_dkset<o, a, c, false>(); \
-    return true;                                                             \
-  }
   if (algo == SPP_ALGO_SAC_ACM) {
-    SPP_KS(11, 11, 3)   // Hopper-v2
+    if (kset_sac_hopper(ob, aout, ac, acmc, ks)) return true;
 #ifndef SPP_ONLY_HOPPER  // kernel-development builds: one instantiation, fast compile
-    SPP_KS(17, 17, 6)   // HalfCheetah-v2
-    SPP_KS(111, 111, 8) // Ant
-    SPP_KS(3, 3, 1)     // Pendulum-v0 (tests)
+    if (kset_sac_hcheetah(ob, aout, ac, acmc, ks)) return true;
+    if (kset_sac_ant(ob, aout, ac, acmc, ks)) return true;
+    if (kset_sac_small(ob, aout, ac, acmc, ks)) return true;
   } else if (algo == SPP_ALGO_DDPG_ACM) {
-    SPP_DKS(17, 17, 6)  // HalfCheetah-v2 (SPP-DDPG, train/spp_ddpg_hcheetah.py)
-    SPP_DKS(11, 11, 3)  // Hopper-v2
+    if (kset_ddpg(ob, aout, ac, acmc, ks)) return true;
 #endif
   }
-#undef SPP_KS
-#undef SPP_DKS
   return false;
 }
 

@@ -9,7 +9,8 @@
 //
 // BasicAcM image rows (per-wave LDS image): h (fc1, 100 units) at rows 128..227 then
 // h1 (50 units) at rows 128..191; the output c goes to the SMALL rows 192.. .
-#include "sac_kernels.h"
+#pragma once
+#include "sac.hip"
 
 namespace spp {
 

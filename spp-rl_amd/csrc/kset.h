@@ -1,0 +1,47 @@
+// Kernel-set table: dims -> phase-kernel instantiations.  Each config family is
+// instantiated in its own translation unit (ks_*.hip) so the library builds in
+// parallel; api.hip only holds the function pointers.
+#pragma once
+#include "sac.hip"
+#include "ddpg.hip"
+
+namespace spp {
+
+struct KernelSet {
+  void (*critic)(SacArgs);
+  void (*actor)(SacArgs, AcmScratch);
+  void (*act)(SacArgs, ActArgs);
+  void (*acmreg)(SacArgs, AcmRegArgs);
+  // DDPG_AcM
+  void (*dcritic)(SacArgs, BAcmScratch);
+  void (*dactor)(SacArgs, BAcmScratch);
+  void (*dact)(SacArgs, ActArgs, BAcmScratch);
+  void (*dreg)(SacArgs, BAcmRegArgs);
+};
+
+template <int OB, int AOUT, int AC, bool ACMC>
+KernelSet make_kset() {
+  using C = Cfg<OB, AOUT, AC, ACMC>;
+  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>,
+          nullptr, nullptr, nullptr, nullptr};
+}
+template <int OB, int AOUT, int AC, bool ACMC>
+KernelSet make_dkset() {
+  using D = DCfg<OB, AOUT, AC, ACMC>;
+  return {nullptr, nullptr, nullptr, nullptr,
+          k_ddpg_critic_phase<D>, k_ddpg_actor_phase<D>, k_ddpg_policy_act<D>, k_bacm_regress<D>};
+}
+
+#define SPP_KSET_CASE(mk, o, a, c)                                     \
+  if (ob == o && aout == a && ac == c) {                               \
+    *ks = acmc ? mk<o, a, c, true>() : mk<o, a, c, false>();           \
+    return true;                                                       \
+  }
+
+bool kset_sac_hopper(int ob, int aout, int ac, bool acmc, KernelSet* ks);    // ks_sac_hopper.hip
+bool kset_sac_hcheetah(int ob, int aout, int ac, bool acmc, KernelSet* ks);  // ks_sac_hcheetah.hip
+bool kset_sac_ant(int ob, int aout, int ac, bool acmc, KernelSet* ks);       // ks_sac_ant.hip
+bool kset_sac_small(int ob, int aout, int ac, bool acmc, KernelSet* ks);     // ks_sac_small.hip
+bool kset_ddpg(int ob, int aout, int ac, bool acmc, KernelSet* ks);          // ks_ddpg.hip
+
+}  // namespace spp

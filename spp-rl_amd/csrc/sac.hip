@@ -10,6 +10,7 @@
 //                       frozen ACM and both updated critics) -> actor grad operands
 //  k_policy_act         ddpg_acm.py:40-50, off_policy.py:50-54, :89-106 (rollout)
 //  k_acm_regress        acm.py:246-258 (ACM regression forward + backward)
+#pragma once
 #include "sac_kernels.h"
 
 namespace spp {
@@ -808,6 +809,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
   }
 }
 
+#ifndef SPP_KSET_TU  // non-template kernels live in the api.hip translation unit only
 // ============================================================================ staging
 // Row-major caller batch (sample_batch layout) -> feature-major padded scratch.
 struct StageArgs {
@@ -857,6 +859,8 @@ __global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint6
     if (idx < n) E[idx] = ((idx % Bp) < B) ? (k ? n1 : n0) : 0.f;
   }
 }
+
+#endif  // SPP_KSET_TU
 
 // ============================================================================ debug dense
 // One layer on a [B][K] row-major batch with a natural bias b (NULL -> 0).

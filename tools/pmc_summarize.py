@@ -1,0 +1,38 @@
+"""Summarise FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) into pmc_traffic.json.
+
+FETCH_SIZE is doubled: gfx950 reports half of the bytes of wide streaming reads
+(MI355X_MICROARCH.md, "HBM").  Both counters are in KB; converted to bytes x1024.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+out = sys.argv[1]
+per = collections.defaultdict(dict)
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(out, "pmc_%s" % c, "run_counter_collection.csv"))):
+        vals[r["Kernel_Name"][:80]].append(float(r["Counter_Value"]))
+    for k, v in vals.items():
+        per[k][c.lower() + "_kb_avg"] = sum(v) / len(v)
+        per[k]["dispatches_" + c.lower()] = len(v)
+
+
+def launch_bytes(prefix):
+    for k, d in per.items():
+        if prefix in k:
+            return int(1024 * (2 * d.get("fetch_size_kb_avg", 0.0) + d.get("write_size_kb_avg", 0.0)))
+    return None
+
+
+res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 2 --warmup 1",
+       "correction": "FETCH_SIZE doubled (gfx950 half-count of wide streaming reads); KB -> B x1024",
+       "critic_phase_bytes_per_launch": launch_bytes("k_sac_critic_phase"),
+       "actor_phase_bytes_per_launch": launch_bytes("k_sac_actor_phase"),
+       "ddpg_critic_phase_bytes_per_launch": launch_bytes("k_ddpg_critic_phase"),
+       "per_kernel_kb": per}
+json.dump(res, open(os.path.join(out, "pmc_traffic.json"), "w"), indent=1)
+for k in ("critic_phase_bytes_per_launch", "actor_phase_bytes_per_launch"):
+    print(k, res[k])

@@ -140,6 +140,8 @@ sppStatus sppAgentBindAlpha(sppAgentHandle h, double* alpha_state_dev, float* al
 /* Adam step counters (host). */
 sppStatus sppAgentSetSteps(sppAgentHandle h, int64_t actor_step, int64_t critic_step, int64_t alpha_step,
                            int64_t acm_step);
+/* Learning rates (torch.optim.lr_scheduler.StepLR of the ACM, acm.py:176-183); < 0 keeps the value. */
+sppStatus sppAgentSetLr(sppAgentHandle h, float actor_lr, float critic_lr, float alpha_lr, float acm_lr);
 sppStatus sppAgentGetSteps(sppAgentHandle h, int64_t* steps4);
 
 /* Update batch in the reference row-major layout (sample_batch output). */
@@ -231,6 +233,19 @@ sppStatus sppPolicyAct(sppAgentHandle h, const float* obs /*[E][ob]*/, int E, co
  * lockstep on device: s' = tanh(A s) + 0.1*resize(a, ob); r = -|a|^2 + s'[0]. */
 sppStatus sppSynthEnvStep(const float* A /*[ob][ob]*/, const float* obs /*[E][ob]*/, const float* action /*[E][ac]*/,
                           int E, int ob, int ac, float* next_obs, float* reward, void* stream);
+
+/* gym Box.sample() stand-in for the pre-train collector (rltoolkit/acm/acm.py:187-196,
+ * off_policy.py:56-87): out[j] ~ U[lo[j % period], hi[j % period]). */
+sppStatus sppRandUniform(float* out_dev, int64_t n, const float* lo_dev, const float* hi_dev, int period,
+                         uint64_t seed, uint64_t offset, void* stream);
+/* Episode returns of E vectorized envs (StatsLogger.calc_running_return input,
+ * rltoolkit/stats_logger.py:19-26; Memory.average_returns_per_rollout):
+ * ep_ret[e] += rew[e]; where end[e], sums[0] += ep_ret[e], sums[1] += 1 (fp64) and
+ * ep_ret[e] = 0.  end may be NULL. */
+sppStatus sppEpisodeAccum(const float* rew, const uint8_t* end, int E, float* ep_ret, double* sums, void* stream);
+/* SynthEnv.reset for the rows with mask[e] != 0 (all rows when mask is NULL). */
+sppStatus sppSynthEnvReset(float* obs /*[E][ob]*/, const uint8_t* mask, int E, int ob, uint64_t seed,
+                           uint64_t offset, void* stream);
 
 /* ------------------------------------------------------------------ PPO path
  * PPO.calculate_q_val + calculate_gae (rltoolkit/algorithms/a2c/a2c.py:247-265,

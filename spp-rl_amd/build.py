@@ -35,8 +35,29 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
+KSET_DEPS = ("kset.h", "sac.hip", "ddpg.hip", "sac_kernels.h", "mlp.h", "common.h")
+
+
+def _obj(src):
+    return os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
+
+
+def _stale(src):
+    """api.hip depends on every csrc file; ks_*.hip only on the phase-kernel headers."""
+    obj = _obj(src)
+    if not os.path.exists(obj):
+        return True
+    if os.path.basename(src).startswith("ks_"):
+        deps = [src] + [os.path.join(CSRC, d) for d in KSET_DEPS]
+    else:
+        deps = [f for f in glob.glob(os.path.join(CSRC, "*")) if not os.path.basename(f).startswith("ks_")]
+    deps.append(os.path.join(REPO, "include", "spprl.h"))
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
 def _compile(src, verbose):
-    obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
+    obj = _obj(src)
     cmd = [HIPCC] + FLAGS + ["-c", "-o", obj, src]
     t0 = time.time()
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
@@ -65,8 +86,10 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None):
     jobs = jobs or min(len(srcs), max(1, min(os.cpu_count() or 1, 8)))
     if verbose:
         print("hipcc %s  (%d units, %d jobs)" % (" ".join(FLAGS), len(srcs), jobs), flush=True)
+    todo = [s for s in srcs if force or _stale(s)]
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+        list(ex.map(lambda s: _compile(s, verbose), todo))
+    objs = [_obj(s) for s in srcs]
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs)
     os.replace(OUT + ".tmp", OUT)
     if verbose:

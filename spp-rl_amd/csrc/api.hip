@@ -388,6 +388,32 @@ sppStatus sppSynthEnvStep(const float* A, const float* obs, const float* action,
   return SPP_OK;
 }
 
+
+sppStatus sppRandUniform(float* out, int64_t n, const float* lo, const float* hi, int period, uint64_t seed,
+                         uint64_t offset, void* stream) {
+  SPP_REQUIRE((out || n == 0) && lo && hi && period > 0, SPP_E_INVALID_ARG, "rand uniform: bad args");
+  if (n == 0) return SPP_OK;
+  hipLaunchKernelGGL(k_rand_uniform, dim3(cdiv((n + 3) / 4, 256)), dim3(256), 0, S(stream), out, n, lo, hi, period,
+                     seed, offset);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppEpisodeAccum(const float* rew, const uint8_t* end, int E, float* ep_ret, double* sums, void* stream) {
+  SPP_REQUIRE(rew && ep_ret && sums && E > 0, SPP_E_INVALID_ARG, "episode accum: bad args");
+  hipLaunchKernelGGL(k_episode_accum, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), rew, end, E, ep_ret, sums);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppSynthEnvReset(float* obs, const uint8_t* mask, int E, int ob, uint64_t seed, uint64_t offset,
+                           void* stream) {
+  SPP_REQUIRE(obs && E > 0 && ob > 0, SPP_E_INVALID_ARG, "synth reset: bad args");
+  hipLaunchKernelGGL(k_synth_reset, dim3(cdiv((int64_t)E * ob, 256)), dim3(256), 0, S(stream), obs, mask, E, ob, seed,
+                     offset);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
 }  // extern "C"
 
 // ================================================================== agent
@@ -1065,6 +1091,14 @@ sppStatus sppAgentBindAlpha(sppAgentHandle a, double* st, float* af) {
   return SPP_OK;
 }
 
+sppStatus sppAgentSetLr(sppAgentHandle a, float actor_lr, float critic_lr, float alpha_lr, float acm_lr) {
+  SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null handle");
+  if (actor_lr >= 0.f) a->cfg.actor_lr = actor_lr;
+  if (critic_lr >= 0.f) a->cfg.critic_lr = critic_lr;
+  if (alpha_lr >= 0.f) a->cfg.alpha_lr = alpha_lr;
+  if (acm_lr >= 0.f) a->cfg.acm_lr = acm_lr;
+  return SPP_OK;
+}
 sppStatus sppAgentSetSteps(sppAgentHandle a, int64_t s0, int64_t s1, int64_t s2, int64_t s3) {
   SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
   a->steps[0] = s0; a->steps[1] = s1; a->steps[2] = s2; a->steps[3] = s3;

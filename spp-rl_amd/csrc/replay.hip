@@ -383,4 +383,61 @@ __global__ void k_synth_env(const float* A, const float* obs, const float* act, 
   rew[e] = -n2 + s0;
 }
 
+
+// uniform floats in [lo, hi) per element (gym Box.sample for the pre-train collector)
+__global__ void k_rand_uniform(float* out, int64_t n, const float* lo, const float* hi, int period, uint64_t seed,
+                               uint64_t offset) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * i >= n) return;
+  const u32x4 r = philox(seed, offset, (uint64_t)i);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  for (int k = 0; k < 4; ++k) {
+    const int64_t j = 4 * i + k;
+    if (j >= n) break;
+    const int c = (int)(j % period);
+    const float u = (float)(w[k] >> 8) * (1.0f / 16777216.0f);  // [0, 1), 24 bits
+    out[j] = lo[c] + u * (hi[c] - lo[c]);
+  }
+}
+
+// Per-env episode bookkeeping of the vectorized collector (StatsLogger /
+// Memory.average_returns_per_rollout, rltoolkit/stats_logger.py:19-26):
+// ep_ret += r; at an episode end the return is folded into sums = {sum, count}
+// (fp64) and ep_ret restarts at 0.  end may be NULL (no env ended this step).
+__global__ void k_episode_accum(const float* rew, const uint8_t* end, int E, float* ep_ret, double* sums) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  double s = 0.0, c = 0.0;
+  if (e < E) {
+    const float r = ep_ret[e] + rew[e];
+    if (end && end[e]) {
+      s = (double)r;
+      c = 1.0;
+      ep_ret[e] = 0.f;
+    } else {
+      ep_ret[e] = r;
+    }
+  }
+  if (!end) return;
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_down(s, o);
+    c += __shfl_down(c, o);
+  }
+  if ((threadIdx.x & 63) == 0 && c > 0.0) {
+    atomicAdd(&sums[0], s);
+    atomicAdd(&sums[1], c);
+  }
+}
+
+// Rows of obs for which mask[e] != 0 are replaced by fresh N(0,1) states
+// (SynthEnv.reset), the rest are kept.
+__global__ void k_synth_reset(float* obs, const uint8_t* mask, int E, int ob, uint64_t seed, uint64_t offset) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)E * ob) return;
+  if (mask && !mask[i / ob]) return;
+  const u32x4 r = philox(seed, offset, (uint64_t)i);
+  float a, b;
+  box_muller(r.x, r.y, a, b);
+  obs[i] = a;
+}
+
 }  // namespace spp

@@ -118,6 +118,10 @@ _SIGS = {
                             c_int, c_void_p, c_void_p, c_void_p]),
     "sppPpoClipLoss": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     "sppAdvNormalize": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "sppRandUniform": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_uint64, c_uint64, c_void_p]),
+    "sppEpisodeAccum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "sppSynthEnvReset": (c_int, [c_void_p, c_void_p, c_int, c_int, c_uint64, c_uint64, c_void_p]),
+    "sppAgentSetLr": (c_int, [c_void_p, c_float, c_float, c_float, c_float]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

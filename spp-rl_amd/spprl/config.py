@@ -1,8 +1,12 @@
 """Defaults of the hot path, mirroring rltoolkit/config.py (reference @ v0).
 
-Only the constants that shape the SPP off-policy rollout/update path are kept.
+Only the constants that shape the SPP off-policy rollout/update path and its
+training loop (rl.py, ddpg.py, acm.py cadence) are kept.
 """
+ITERATIONS = 2000
 GAMMA = 0.95
+BATCH_SIZE = 200
+STATS_FREQ = 20
 DDPG_LR = 1e-3
 TAU = 0.005
 UPDATE_BATCH_SIZE = 100
@@ -14,6 +18,13 @@ ACT_NOISE = 0.1
 ALPHA_LR = 1e-3
 ALPHA = 0.2
 ACM_LR = 3e-3
+ACM_EPOCHS = 1
+ACM_PRE_TRAIN_SAMPLES = 1000
+ACM_PRE_TRAIN_N_EPOCHS = 10
+ACM_SCHEDULER_STEP = 25
+ACM_SCHEDULER_GAMMA = 0.5
+ACM_UPDATE_BATCHES = False
+ACM_KEEP_PRE_TRAIN = True
 ACM_BATCH_SIZE = 128
 ACM_UPDATE_FREQ = 1
 ACM_CRITIC = False

@@ -16,12 +16,13 @@ import torch
 from . import _lib, config, nets
 from ._lib import call, ptr, stream_handle
 from .replay import BufferAcMOffPolicy
+from .trainer import OffPolicyLoop
 
 _NETS = {"actor": _lib.SPP_NET_ACTOR, "critic": _lib.SPP_NET_CRITIC1, "actor_targ": _lib.SPP_NET_ACTOR_TARG,
          "critic_targ": _lib.SPP_NET_CRITIC1_TARG, "acm": _lib.SPP_NET_ACM}
 
 
-class DDPG_AcM:
+class DDPG_AcM(OffPolicyLoop):
     def __init__(self, env_name="HalfCheetah-v2", gamma=config.GAMMA, actor_lr=config.DDPG_LR,
                  critic_lr=config.DDPG_LR, tau=config.TAU, act_noise=config.ACT_NOISE,
                  update_batch_size=config.UPDATE_BATCH_SIZE, buffer_size=config.BUFFER_SIZE, acm_lr=config.ACM_LR,
@@ -30,6 +31,7 @@ class DDPG_AcM:
                  obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None, seed=None, **unused):
         _lib.load()
         ob, ac, ac_high, _ = env_spec or config.ENV_SPECS[env_name]
+        self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
         self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
         self.device = torch.device(device)
         self.gamma, self.actor_lr, self.critic_lr, self.acm_lr, self.tau = gamma, actor_lr, critic_lr, acm_lr, tau
@@ -82,6 +84,7 @@ class DDPG_AcM:
         rb = self.replay_buffer
         call("sppAgentBindNormalizer", self._h, ptr(rb.min_obs), ptr(rb.max_obs), ptr(rb.obs_mean), ptr(rb.obs_std))
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
+        self._init_loop(update_batch_size=update_batch_size, **unused)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -118,6 +121,9 @@ class DDPG_AcM:
         if allreduce is not None:
             allreduce(self.bucket_actor)
         call("sppDdpgAcmActorApply", self._h, st)
+
+    def _fused_update(self, idx, counter, allreduce=None):
+        self.update_from_replay_dp(idx, allreduce)
 
     @property
     def loss(self):

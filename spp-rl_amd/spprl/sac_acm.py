@@ -21,9 +21,10 @@ import torch
 from . import _lib, config, nets
 from ._lib import call, ptr, stream_handle
 from .replay import BufferAcMOffPolicy
+from .trainer import OffPolicyLoop
 
 
-class SAC_AcM:
+class SAC_AcM(OffPolicyLoop):
     def __init__(self, env_name="Hopper-v2", gamma=config.GAMMA, actor_lr=config.DDPG_LR,
                  critic_lr=config.DDPG_LR, alpha_lr=config.ALPHA_LR, alpha=config.ALPHA, tau=config.TAU,
                  act_noise=0.0, update_batch_size=config.UPDATE_BATCH_SIZE, buffer_size=config.BUFFER_SIZE,
@@ -33,6 +34,7 @@ class SAC_AcM:
                  seed=None, **unused):
         _lib.load()
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
+        self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
         self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
         self.max_ep_len = None  # Q3: AcMOffPolicy never masks time-limit done (off_policy.py:43)
         self.device = torch.device(device)
@@ -108,6 +110,7 @@ class SAC_AcM:
                                                 min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
         self.bind_normalizer(self.replay_buffer)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
+        self._init_loop(update_batch_size=update_batch_size, **unused)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -171,6 +174,9 @@ class SAC_AcM:
         if allreduce is not None:
             allreduce(self.bucket_actor)
         call("sppSacAcmActorApply", self._h, ptr(self._losses), st)
+
+    def _fused_update(self, idx, counter, allreduce=None):
+        self.update_from_replay_dp(idx, self.loop_seed + 1, counter, allreduce)
 
     def acm_update_from_replay(self, idx, x, y, loss, allreduce=None):
         """update_acm_batches body (acm.py:356-372) for one device-sampled batch."""
@@ -249,12 +255,3 @@ class SAC_AcM:
             rb.min_obs.copy_(torch.as_tensor(d["min_obs"]))
             rb.max_obs.copy_(torch.as_tensor(d["max_obs"]))
             rb._have_minmax = True
-
-    def save(self, path):
-        with open(path, "wb") as f:
-            pickle.dump(self.collect_params_dict(), f)
-
-    def load(self, path):
-        # our own checkpoints only (never unpickle files that ship with the reference)
-        with open(path, "rb") as f:
-            self.apply_params_dict(pickle.load(f))

@@ -1,0 +1,547 @@
+"""Vectorized rollout -> HBM replay -> update loop (the callers either side of the update).
+
+Mirrors the reference's control plane for the SPP off-policy agents, batched over
+E lockstep env instances per GPU:
+
+  RL.train                      rltoolkit/rl.py:192-229        -> OffPolicyLoop.train
+  DDPG.perform_iteration        algorithms/ddpg/ddpg.py:159-170 -> perform_iteration
+  DDPG.collect_batch_and_train  ddpg.py:182-223                -> collect_batch_and_train
+  DDPG(_AcM).make_update        ddpg.py:225-237, acm/off_policy/ddpg_acm.py:52-85
+  AcMTrainer.pre_train          acm/acm.py:234-244 (+ AcMOffPolicy.collect_samples, off_policy.py:56-87)
+  AcMTrainer.update_acm         acm.py:266-303 (shuffled full-buffer epochs, StepLR)
+  AcMTrainer.update_acm_batches acm.py:356-372
+  DDPG.test                     ddpg.py:385-410
+  StatsLogger                   stats_logger.py:9-26
+
+Two schedules:
+  * "reference" (E == 1): the reference cadence frame by frame -- grad_steps updates of
+    update_batch_size samples every update_freq frames, indices from numpy's global
+    MT19937 stream (np.random.randint, replay_buffer.py:234), episodes run to their end
+    inside an iteration.
+  * "fused" (E > 1): each vector step of E frames does one grad step on
+    rho*E device-sampled transitions, rho = update_batch_size*grad_steps/update_freq, and
+    (acm_update_batches mode) one ACM step on sigma*E samples, sigma =
+    acm_update_batches*acm_batch_size/acm_update_freq.  FLOPs per env-step equal the
+    reference's.  With a host (CPU) env the update of step t is enqueued before the CPU
+    envs step, so GPU work overlaps the simulator ("pipelined": the update sees the
+    transitions up to t-1).
+
+Envs: ``SynthVecEnv`` (SURVEY.md Appendix A dynamics, on device) or ``HostVecEnv``
+(gym-style envs stepped on the host CPU -- MuJoCo when available -- with pinned staging
+buffers and H2D/D2H copies on a side stream).  Everything device-side runs in
+libspprl.so; this module only sequences calls.
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import config
+from ._lib import call, ptr, stream_handle
+from .dp import make_allreduce
+
+# ---------------------------------------------------------------- stats
+
+
+class StatsLogger:
+    """rltoolkit/stats_logger.py:9-26 (running return with alpha = 0.9)."""
+
+    def __init__(self, alpha=0.9):
+        self.running_return = None
+        self.test_return = None
+        self._alpha = 0.9  # the reference ignores its argument (stats_logger.py:13)
+        self.frames = 0
+        self.rollouts = 0
+        self.time_list = []
+        self.stats = []
+
+    def calc_running_return(self, new_mean_return):
+        if new_mean_return is None:
+            return self.running_return
+        if self.running_return is None:
+            self.running_return = new_mean_return
+        else:
+            self.running_return *= self._alpha
+            self.running_return += (1 - self._alpha) * new_mean_return
+        return self.running_return
+
+
+# ---------------------------------------------------------------- envs
+
+
+class SynthVecEnv:
+    """E SynthEnv instances stepped in lockstep on device:
+    s' = tanh(A s) + 0.1 resize(a, ob), r = -|a|^2 + s'[0], episodes of ``max_episode_steps``.
+    ``A`` is shared (seeded by ``dyn_seed``) so data-parallel ranks simulate the same MDP."""
+
+    is_host = False
+
+    def __init__(self, n_envs, ob, ac, max_episode_steps=1000, ac_high=1.0, seed=0, dyn_seed=1234, device="cuda"):
+        self.n, self.ob, self.ac = int(n_envs), int(ob), int(ac)
+        self.device = torch.device(device)
+        self._max_episode_steps = int(max_episode_steps)
+        g = torch.Generator(device="cpu").manual_seed(dyn_seed)
+        self.A = (torch.randn(ob, ob, generator=g) * 0.05).to(self.device)
+        self.ac_low = torch.full((ac,), -float(ac_high), device=self.device)
+        self.ac_high = torch.full((ac,), float(ac_high), device=self.device)
+        self.seed, self._ctr = int(seed), 0
+        self.obs = torch.empty(self.n, ob, device=self.device)
+        self.nobs = torch.empty(self.n, ob, device=self.device)
+        self.rew = torch.empty(self.n, device=self.device)
+        self.end_dev = torch.empty(self.n, dtype=torch.uint8, device=self.device)
+        self.t = 0
+
+    def _next(self):
+        self._ctr += 1
+        return self._ctr
+
+    def reset(self, mask=None):
+        """Reset all envs (mask None) or those with mask[e]; returns the device obs [E, ob]."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(np.asarray(mask, np.uint8)).to(self.device)
+        call("sppSynthEnvReset", ptr(self.obs), ptr(m), self.n, self.ob, self.seed, self._next(), stream_handle())
+        self._keep = m
+        if mask is None:
+            self.t = 0
+        return self.obs
+
+    def step(self, action):
+        """action [E, ac] device -> (next_obs [E, ob], rew [E], end host bool [E], end device u8 [E])."""
+        call("sppSynthEnvStep", ptr(self.A), ptr(self.obs), ptr(action), self.n, self.ob, self.ac, ptr(self.nobs),
+             ptr(self.rew), stream_handle())
+        self.obs, self.nobs = self.nobs, self.obs
+        self.t += 1
+        end = self.t >= self._max_episode_steps
+        self.end_dev.fill_(1 if end else 0)
+        if end:
+            self.t = 0
+        return self.obs, self.rew, np.full(self.n, end), self.end_dev
+
+    def sample_actions(self, out):
+        """action_space.sample() for every env, on device (pre-train collector)."""
+        call("sppRandUniform", ptr(out), out.numel(), ptr(self.ac_low), ptr(self.ac_high), self.ac, self.seed + 7,
+             self._next(), stream_handle())
+        return out
+
+    def spawn(self, n_envs, seed):
+        return SynthVecEnv(n_envs, self.ob, self.ac, self._max_episode_steps, float(self.ac_high[0]), seed=seed,
+                           device=self.device)
+
+
+class HostVecEnv:
+    """gym-style envs stepped on the host CPU (MuJoCo when installed).
+
+    Actions go device -> pinned host on a side stream; observations/rewards come back
+    pinned host -> device on the same side stream; the compute stream waits on an event,
+    so the copies overlap whatever the compute stream has queued (the update)."""
+
+    is_host = True
+
+    def __init__(self, envs, device="cuda", env_fn=None):
+        self.env_fn = env_fn
+        self.envs = list(envs)
+        self.n = len(self.envs)
+        e0 = self.envs[0]
+        self.ob = int(np.prod(e0.observation_space.shape))
+        self.ac = int(np.prod(e0.action_space.shape))
+        self._max_episode_steps = getattr(e0, "_max_episode_steps", None)
+        self.device = torch.device(device)
+        self.side = torch.cuda.Stream(device=self.device)
+        pin = dict(pin_memory=True)
+        self.h_obs = torch.empty(self.n, self.ob, **pin)
+        self.h_rew = torch.empty(self.n, **pin)
+        self.h_end = torch.empty(self.n, dtype=torch.uint8, **pin)
+        self.h_act = torch.empty(self.n, self.ac, **pin)
+        self.obs = torch.empty(self.n, self.ob, device=self.device)
+        self.rew = torch.empty(self.n, device=self.device)
+        self.end_dev = torch.empty(self.n, dtype=torch.uint8, device=self.device)
+        self._act_ev = torch.cuda.Event()
+        self._pending = False
+
+    def _upload(self):
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.side):
+            self.side.wait_stream(main)  # do not overwrite obs still being read by queued kernels
+            self.obs.copy_(self.h_obs, non_blocking=True)
+            self.rew.copy_(self.h_rew, non_blocking=True)
+            self.end_dev.copy_(self.h_end, non_blocking=True)
+        main.wait_stream(self.side)
+
+    def reset(self, mask=None):
+        idx = range(self.n) if mask is None else np.flatnonzero(mask)
+        for e in idx:
+            self.h_obs[e] = torch.as_tensor(np.asarray(self.envs[e].reset(), np.float32).reshape(-1))
+        self._upload()
+        return self.obs
+
+    def send(self, action):
+        """Start the D2H copy of the actions (non-blocking)."""
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.side):
+            self.side.wait_stream(main)
+            self.h_act.copy_(action, non_blocking=True)
+            self._act_ev.record(self.side)
+        self._pending = True
+
+    def recv(self):
+        self._act_ev.synchronize()
+        self._pending = False
+        act = self.h_act.numpy()
+        end = np.zeros(self.n, bool)
+        for e, env in enumerate(self.envs):
+            o, r, d, _ = env.step(act[e])
+            self.h_obs[e] = torch.as_tensor(np.asarray(o, np.float32).reshape(-1))
+            self.h_rew[e] = float(r)
+            end[e] = bool(d)
+        self.h_end.copy_(torch.from_numpy(end.astype(np.uint8)))
+        self._upload()
+        return self.obs, self.rew, end, self.end_dev
+
+    def step(self, action):
+        self.send(action)
+        return self.recv()
+
+    def spawn(self, n_envs, seed):
+        if self.env_fn is None:
+            raise NotImplementedError("HostVecEnv.spawn needs env_fn")
+        return HostVecEnv([self.env_fn() for _ in range(n_envs)], self.device, self.env_fn)
+
+    def sample_actions(self, out):
+        a = np.stack([np.asarray(env.action_space.sample(), np.float32).reshape(-1) for env in self.envs])
+        out.copy_(torch.from_numpy(a))
+        return out
+
+
+# ---------------------------------------------------------------- loop
+
+
+class OffPolicyLoop:
+    """Trainer mixin of SAC_AcM / DDPG_AcM.  The host class provides ``act``,
+    ``update``, ``replay_buffer``, ``bucket_acm``, ``_h`` and ``_fused_update(idx, ctr, allreduce)``."""
+
+    def _init_loop(self, iterations=config.ITERATIONS, batch_size=config.BATCH_SIZE, stats_freq=config.STATS_FREQ,
+                   test_episodes=None, return_done=None, max_frames=None, random_frames=config.RANDOM_FRAMES,
+                   update_freq=config.UPDATE_FREQ, grad_steps=config.GRAD_STEPS, acm_epochs=config.ACM_EPOCHS,
+                   acm_batch_size=config.ACM_BATCH_SIZE, acm_update_freq=config.ACM_UPDATE_FREQ,
+                   acm_update_batches=config.ACM_UPDATE_BATCHES, acm_pre_train_samples=config.ACM_PRE_TRAIN_SAMPLES,
+                   acm_pre_train_epochs=config.ACM_PRE_TRAIN_N_EPOCHS, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
+                   acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=config.ACM_KEEP_PRE_TRAIN,
+                   n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, **unused):
+        if max_frames is not None and max_frames > iterations * batch_size:
+            raise AssertionError("max_frames should be smaller or equal than iterations * batch_size")  # rl.py:166
+        self.iterations, self.batch_size, self.stats_freq = int(iterations), int(batch_size), int(stats_freq)
+        self.test_episodes, self.return_done, self.max_frames = test_episodes, return_done, max_frames
+        self.random_frames, self.update_freq, self.grad_steps = int(random_frames), int(update_freq), int(grad_steps)
+        self.acm_epochs, self.acm_batch_size, self.acm_update_freq = int(acm_epochs), int(acm_batch_size), int(
+            acm_update_freq)
+        self.acm_update_batches = acm_update_batches
+        self.acm_pre_train_samples, self.acm_pre_train_epochs = int(acm_pre_train_samples), int(acm_pre_train_epochs)
+        self.acm_scheduler_step, self.acm_scheduler_gamma = int(acm_scheduler_step), float(acm_scheduler_gamma)
+        self.acm_keep_pretrain = bool(acm_keep_pretrain)
+        self._acm_sched_epochs = 0  # StepLR.last_epoch
+        self.iteration = 0
+        self.stats_logger = StatsLogger()
+        ob, ac = self.ob_dim, self.ac_dim
+        if env is None:
+            spec = getattr(self, "env_spec", None) or config.ENV_SPECS.get(self.env_name, (ob, ac, 1.0, 1000))
+            env = SynthVecEnv(n_envs, ob, ac, max_episode_steps=spec[3], ac_high=spec[2], seed=loop_seed,
+                              device=self.device)
+        self.env = env
+        self.n_envs = env.n
+        self.schedule = schedule or ("reference" if self.n_envs == 1 else "fused")
+        if self.schedule not in ("reference", "fused"):
+            raise ValueError("schedule must be 'reference' or 'fused'")
+        self.allreduce = allreduce if allreduce is not None else make_allreduce()
+        self.loop_seed = int(loop_seed)
+        self._ctr = 0
+        E = self.n_envs
+        self.rho = self.update_batch_size * self.grad_steps / self.update_freq
+        self.sigma = (self.acm_update_batches * self.acm_batch_size / self.acm_update_freq
+                      if self.acm_update_batches else 0.0)
+        d = self.device
+        self._eps = torch.empty(E, self.actor_output_dim, device=d)
+        self._noise = torch.empty(E, self.actor_output_dim, device=d)
+        self._ep_ret = torch.zeros(E, device=d)
+        self._ret_sums = torch.zeros(2, dtype=torch.float64, device=d)
+        self._acm_loss = torch.zeros(1, device=d)
+        self._acm_loss_acc = torch.zeros(1, device=d)
+        self._obs = None
+        self._prev_slots = None
+
+    # ---------------------------------------------------------- helpers
+    def _next(self):
+        self._ctr += 1
+        return self._ctr
+
+    def _randn(self, t):
+        call("sppRandNormal", ptr(t), t.numel(), self.loop_seed, self._next(), stream_handle())
+        return t
+
+    def _set_acm_lr(self, lr):
+        call("sppAgentSetLr", self._h, -1.0, -1.0, -1.0, float(lr))
+
+    # ---------------------------------------------------------- RL.train (rl.py:192-229)
+    def train(self, iterations=None):
+        if iterations:
+            self.iterations += iterations
+        ret = None
+        while self.iteration < self.iterations:
+            t0 = time.perf_counter()
+            ret = self.perform_iteration()
+            self.stats_logger.time_list.append(time.perf_counter() - t0)
+            running = self.stats_logger.calc_running_return(ret)
+            if self.return_done is not None and running is not None and running >= self.return_done:
+                break
+            if self.iteration % self.stats_freq == 0:
+                self.logs_after_iteration(ret)
+            self.iteration += 1
+            if self.max_frames is not None and self.max_frames < self.stats_logger.frames:
+                break
+        self.logs_after_iteration(ret, done=True)
+        return self.stats_logger.running_return
+
+    def logs_after_iteration(self, ret, done=False):
+        if self.test_episodes:
+            self.stats_logger.test_return = self.test()
+        self.stats_logger.stats.append({"iteration": self.iteration, "frames": self.stats_logger.frames,
+                                        "running_return": self.stats_logger.running_return,
+                                        "test_return": self.stats_logger.test_return, "loss": dict(self.loss)})
+
+    # ---------------------------------------------------------- DDPG.perform_iteration (ddpg.py:159-170)
+    def perform_iteration(self):
+        """Collect batch_size frames (training as they arrive), then update the obs stats.
+        Returns the mean return of the episodes completed in this iteration (None if none)."""
+        self._ret_sums.zero_()
+        self.collect_batch_and_train(self.batch_size)
+        self.replay_buffer.update_obs_mean_std()
+        s = self._ret_sums.cpu().numpy()
+        return float(s[0] / s[1]) if s[1] > 0 else None
+
+    def _start_episodes(self):
+        obs = self.env.reset()
+        self._obs = obs
+        self._prev_slots = self.replay_buffer.add_obs_batch(obs)
+        self._ep_ret.zero_()
+
+    def collect_batch_and_train(self, batch_size):
+        collected = 0
+        if self.schedule == "reference":
+            while collected < batch_size:  # whole episodes (ddpg.py:192-223)
+                self.stats_logger.rollouts += 1
+                self._start_episodes()
+                end = False
+                while not end:
+                    end = bool(self._vector_step()[0])
+                    collected += 1
+                    self.make_update()
+            return
+        if self._obs is None:
+            self._start_episodes()
+            self.stats_logger.rollouts += self.n_envs
+        while collected < batch_size:
+            self._vector_step()
+            collected += self.n_envs
+
+    def _vector_step(self):
+        """One step of every env: act -> env -> replay writes (-> fused update)."""
+        E = self.n_envs
+        rb = self.replay_buffer
+        mode = 0 if self.stats_logger.frames < self.random_frames else 1  # initial_act (off_policy.py:50-54)
+        self._randn(self._eps)
+        if mode == 1:
+            self._randn(self._noise)
+        obs_in = rb.normalize(self._obs)
+        tgt, env_act = self.act(obs_in, eps=self._eps, noise=self._noise, mode=mode)
+        pipelined = self.schedule == "fused" and self.env.is_host
+        if pipelined:
+            self.env.send(env_act)
+            self._fused_make_update()  # overlaps the CPU envs
+            nobs, rew, end, end_dev = self.env.recv()
+        else:
+            nobs, rew, end, end_dev = self.env.step(env_act)
+        any_end = bool(end.any())
+        call("sppEpisodeAccum", ptr(rew), ptr(end_dev) if any_end else None, E, ptr(self._ep_ret),
+             ptr(self._ret_sums), stream_handle())
+        slots = rb.add_obs_batch(nobs)
+        # AcMOffPolicy keeps max_ep_len None: done == end (Q3, off_policy.py:43, ddpg.py:210-211)
+        rb.add_timestep_batch(self._prev_slots, slots, tgt, rew, end_dev, end_dev, env_act)
+        self._prev_slots = slots
+        self._obs = nobs
+        self.stats_logger.frames += E
+        if any_end and self.schedule == "fused":
+            self.stats_logger.rollouts += int(end.sum())
+            self._obs = self.env.reset(end)
+            rs = rb.add_obs_batch(self._obs[torch.as_tensor(np.flatnonzero(end), device=self.device)])
+            self._prev_slots = self._prev_slots.copy()
+            self._prev_slots[np.flatnonzero(end)] = rs
+        if self.schedule == "fused" and not pipelined:
+            self._fused_make_update()
+        return end
+
+    # ---------------------------------------------------------- make_update
+    def update_condition(self):  # ddpg.py:225-229
+        return len(self.replay_buffer) > self.update_batch_size and self.stats_logger.frames % self.update_freq == 0
+
+    def acm_update_condition(self):  # ddpg_acm.py:52-57
+        return self.iteration > 0 and self.acm_epochs > 0 and self.stats_logger.frames % self.acm_update_freq == 0
+
+    def make_update(self):
+        """Reference cadence (ddpg.py:231-237, ddpg_acm.py:75-85), one frame at a time."""
+        if self.update_condition():
+            for _ in range(self.grad_steps):
+                self.update(*self.replay_buffer.sample_batch(self.update_batch_size, self.device))
+        if self.acm_update_condition():
+            if self.acm_update_batches:
+                self.update_acm_batches(self.acm_update_batches)
+            else:
+                self.update_acm(self.acm_epochs)
+
+    def _fused_make_update(self):
+        """Batched cadence: rho*E transitions in one grad step, sigma*E in one ACM step."""
+        rb = self.replay_buffer
+        n = len(rb)
+        B, BA = self.fused_batch_sizes()
+        if n > self.update_batch_size:
+            idx = torch.empty(B, dtype=torch.int64, device=self.device)
+            call("sppRandIndex", ptr(idx), B, n, self.loop_seed, self._next(), stream_handle())
+            self._fused_update(idx, self._ctr, self.allreduce)
+            self._keep_idx = idx
+        if self.iteration > 0 and self.acm_epochs > 0:
+            if self.acm_update_batches:
+                self._acm_step_from_idx(self._rand_idx(BA, n))
+                self._acm_loss_acc.copy_(self._acm_loss)
+            else:  # epoch mode at every crossed multiple of acm_update_freq
+                f1 = self.stats_logger.frames
+                if f1 // self.acm_update_freq > (f1 - self.n_envs) // self.acm_update_freq:
+                    self.update_acm(self.acm_epochs)
+
+    def fused_batch_sizes(self):
+        """(grad-step batch, ACM batch) of one fused vector step: rho*E and sigma*E."""
+        E = self.n_envs
+        return max(1, int(round(self.rho * E))), max(1, int(round(self.sigma * E))) if self.sigma else 0
+
+    def _rand_idx(self, B, n):
+        idx = torch.empty(B, dtype=torch.int64, device=self.device)
+        call("sppRandIndex", ptr(idx), B, n, self.loop_seed, self._next(), stream_handle())
+        return idx
+
+    # ---------------------------------------------------------- ACM regression
+    def _acm_step_from_idx(self, idx):
+        """acm_cat + batch_update (acm.py:246-264) on gathered replay rows."""
+        B = idx.numel()
+        st = stream_handle()
+        x = torch.empty(B, 2 * self.ob_dim, device=self.device)
+        y = torch.empty(B, self.ac_dim, device=self.device)
+        call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), B, ptr(x), ptr(y), st)
+        call("sppAcmRegressGrads", self._h, ptr(x), ptr(y), B, ptr(self._acm_loss), st)
+        if self.allreduce is not None:
+            self.allreduce(self.bucket_acm)
+        call("sppAcmRegressApply", self._h, st)
+        self._keep_acm_xy = (idx, x, y)
+
+    def update_acm_batches(self, n_batches):
+        """acm.py:356-372: n batches of acm_batch_size uniform samples; loss = batch mean."""
+        n = len(self.replay_buffer)
+        self._acm_loss_acc.zero_()
+        for _ in range(n_batches):
+            self._acm_step_from_idx(self._rand_idx(self.acm_batch_size, n))
+            self._acm_loss_acc += self._acm_loss
+        self._acm_loss_acc /= n_batches
+
+    def update_acm(self, epochs, pretrain=False):
+        """acm.py:266-303: shuffled epochs over every live row, batches of acm_batch_size,
+        StepLR(acm_scheduler_step, acm_scheduler_gamma) stepped once per epoch."""
+        n = len(self.replay_buffer)
+        if n == 0:
+            return
+        g = torch.Generator(device="cpu").manual_seed(self.loop_seed * 7919 + self._next())
+        for _ in range(epochs):
+            lr = self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step)
+            self._set_acm_lr(lr)
+            perm = torch.randperm(n, generator=g).to(self.device)
+            self._acm_loss_acc.zero_()
+            nb = 0
+            for s in range(0, n, self.acm_batch_size):
+                self._acm_step_from_idx(perm[s:s + self.acm_batch_size].contiguous())
+                self._acm_loss_acc += self._acm_loss
+                nb += 1
+            self._acm_loss_acc /= max(nb, 1)
+            self._acm_sched_epochs += 1
+        self._set_acm_lr(self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step))
+
+    # ---------------------------------------------------------- pre-train (acm.py:234-244)
+    def collect_samples(self):
+        """AcMOffPolicy.collect_samples (off_policy.py:56-87): random env actions; the
+        buffer's ``action`` slot holds the next obs; time-limit ends are kept as done."""
+        rb, E = self.replay_buffer, self.n_envs
+        collected = 0
+        obs = self.env.reset()
+        prev = rb.add_obs_batch(obs)
+        act = torch.empty(E, self.ac_dim, device=self.device)
+        while collected < self.acm_pre_train_samples:
+            self.env.sample_actions(act)
+            nobs, rew, end, end_dev = self.env.step(act)
+            slots = rb.add_obs_batch(nobs)
+            rb.add_timestep_batch(prev, slots, nobs, rew, end_dev, end_dev, act)
+            prev = slots
+            collected += E
+            if end.any():
+                obs = self.env.reset(end)
+                rs = rb.add_obs_batch(obs[torch.as_tensor(np.flatnonzero(end), device=self.device)])
+                prev = prev.copy()
+                prev[np.flatnonzero(end)] = rs
+        self._obs = None
+
+    def pre_train(self):
+        self.collect_samples()
+        self.update_acm(epochs=self.acm_pre_train_epochs, pretrain=True)
+        self.replay_buffer.update_obs_mean_std()
+        if not self.acm_keep_pretrain:
+            self.replay_buffer.reset_idx()
+
+    # ---------------------------------------------------------- DDPG.test (ddpg.py:385-410)
+    def test(self, episodes=None):
+        """Deterministic policy (act_noise 0, mode det) for ``episodes`` env instances run in
+        parallel, one episode each; returns the mean episode return."""
+        episodes = episodes or self.test_episodes or 1
+        env = self.env.spawn(episodes, seed=self.loop_seed + 99991)
+        obs = env.reset()
+        ret = torch.zeros(episodes, device=self.device)
+        sums = torch.zeros(2, dtype=torch.float64, device=self.device)
+        alive = np.ones(episodes, bool)
+        while alive.any():
+            _, env_act = self.act(self.replay_buffer.normalize(obs), mode=2, act_noise=0.0)
+            obs, rew, end, _ = env.step(env_act)
+            first = end & alive
+            m = torch.as_tensor(first.astype(np.uint8), device=self.device)
+            call("sppEpisodeAccum", ptr(rew), ptr(m), episodes, ptr(ret), ptr(sums), stream_handle())
+            alive &= ~end
+            if end.any() and alive.any():
+                obs = env.reset(end)
+        s = sums.cpu().numpy()
+        return float(s[0] / s[1])
+
+    @property
+    def acm_loss(self):
+        return float(self._acm_loss_acc.item())
+
+    # ---------------------------------------------------------- checkpoints (rl.py:286-301)
+    def save(self, path):
+        import pickle
+
+        with open(path, "wb") as f:
+            pickle.dump(self.collect_params_dict(), f)
+
+    def load(self, path):
+        """Our own checkpoints only (never unpickle files that ship with the reference)."""
+        import pickle
+
+        with open(path, "rb") as f:
+            self.apply_params_dict(pickle.load(f))
+
+
+def acm_lr_at(acm_lr, gamma, step, epochs_done):
+    """StepLR value after ``epochs_done`` scheduler steps (torch.optim.lr_scheduler.StepLR)."""
+    return acm_lr * gamma ** (epochs_done // step)
+

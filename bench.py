@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
-"""bench.py — env-steps/sec (rollout+update), SPP-SAC Hopper-v2, on N MI355X.
+"""bench.py — env-steps/sec (rollout+update) of the SPP off-policy loop on N MI355X.
 
-One "step" = one vector step of E lockstep envs per GPU through the whole
-SPP-SAC loop, all on device (SURVEY.md §8d batched schedule):
-  rollout   policy act (actor rsample + act_noise + clip + denorm + ACM)    ddpg_acm.py:40-50, off_policy.py:89-106
-            synthetic fixed-shape env step (SURVEY Appendix A SynthEnv)     (MuJoCo is not in this image)
-            replay writes: obs ring + timestep ring (Q6 rule)               replay_buffer.py:56-75,133-137,332-333
-  update    B = rho*E uniform samples (rho = 100 = 100*50/50, train/spp_sac_hopper.py:19-22),
-            one SAC_AcM grad step on them                                   sac_acm.py:89-162
-  ACM       sigma*E samples (sigma = 10 = 100*100/1000, train/spp_sac_hopper.py:31-36),
-            one AcMTrainer regression step                                  acm.py:246-258, 356-372
-  stats     update_obs_mean_std over the live replay rows                   replay_buffer.py:83-96
-FLOPs per env-step match the reference cadence (1 grad step of 100 samples per env step).
-N > 1: one process per GPU (torchrun), each with E envs and a local 1e6-row replay
-shard; gradient buckets are averaged with RCCL all-reduce at the update's two exchange
-points (critic grads, actor grads) and at the ACM step; value = all ranks' env-steps / max time.
+One "step" = one vector step of E lockstep envs per GPU through the product training
+loop (spprl.trainer.OffPolicyLoop, fused schedule), all on device:
+  rollout   policy act (actor sample + act_noise + clip + denorm + ACM)     ddpg_acm.py:40-50, off_policy.py:89-106
+            synthetic fixed-shape env step (SURVEY Appendix A SynthEnv)      (MuJoCo is not in this image)
+            replay writes: obs ring + timestep ring (Q6 rule)                replay_buffer.py:56-75,133-137,332-333
+  update    B = rho*E uniform samples, one grad step on them                 sac_acm.py:89-162 / ddpg_acm.py:147-201
+            rho = update_batch_size*grad_steps/update_freq = 100 (train/spp_*.py)
+  ACM       sigma*E samples, one AcMTrainer regression step                  acm.py:246-258, 356-372
+            sigma = acm_update_batches*acm_batch_size/acm_update_freq (10 SAC, 51.2 DDPG)
+  stats     update_obs_mean_std over the live replay rows                    replay_buffer.py:83-96
+FLOPs per env-step equal the reference cadence (one grad step of 100 samples per env step).
+
+--config sac_hopper (default; BASELINE.json configs[1]: SPP-SAC Hopper-v2, 4096 envs, fp32)
+         ddpg_hcheetah (configs[2]: SPP-DDPG HalfCheetah-v2, 8192 envs, 10M-transition HBM replay)
+         sac_ant (configs[4] per-GPU shape: SPP-SAC Ant, 32768 envs / 8 GPUs = 4096 per GPU, fp32 MLP)
+N > 1: one process per GPU (torchrun), each with E envs and a local replay shard; gradient
+buckets are averaged with RCCL all-reduce at the update's exchange points (critic grads,
+actor grads, ACM grads); value = all ranks' env-steps / max-over-ranks time.
 """
 import argparse
 import json
@@ -31,21 +35,34 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-# Hopper SPP-SAC (train/spp_sac_hopper.py)
-OB, AC = 11, 3
-EP_LEN = 1000
-PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA = f32 vector peak
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA peak
 PEAK_HBM_GBS = 8000.0
 
-# algorithmic MACs per replayed sample, Hopper dims, H = 256
-A_MAC = OB * 256 + 256 * 256 + 256 * 2 * OB            # actor forward
-M_MAC = 2 * OB * 64 + 64 * 32 + 32 * AC                # ACM forward
-C_MAC = (OB + AC) * 256 + 256 * 256 + 256              # critic forward
-CRITIC_PHASE_MAC = A_MAC + M_MAC + 2 * C_MAC + 2 * C_MAC + 2 * (256 + 256 * 256)
-ACTOR_PHASE_MAC = A_MAC + M_MAC + 2 * C_MAC + 2 * (256 + 256 * 256 + AC * 256) + (AC * 32 + 32 * 64 + 64 * OB) + (
-    2 * OB * 256 + 256 * 256)
-DW_MAC = 2 * C_MAC + A_MAC                               # weight gradients of both critics + actor
-ACM_REG_MAC = M_MAC + M_MAC + (AC * 32 + 32 * 64)        # ACM fwd + dW + dX (regression step)
+CONFIGS = {
+    "sac_hopper": dict(
+        algo="sac", env="Hopper-v2", ob=11, ac=3, envs=4096, buffer=1_000_000, baseline_idx=1,
+        workload="SPP-SAC Hopper-v2, %d vectorized envs per GPU, fp32 (BASELINE.json configs[1])",
+        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
+                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
+                   acm_update_batches=100, acm_batch_size=100)),
+    "ddpg_hcheetah": dict(
+        algo="ddpg", env="HalfCheetah-v2", ob=17, ac=6, envs=8192, buffer=10_000_000, baseline_idx=2,
+        workload="SPP-DDPG HalfCheetah-v2, %d vectorized envs per GPU, 10M-transition HBM replay, fp32 "
+                 "(BASELINE.json configs[2])",
+        agent=dict(gamma=0.95, actor_lr=5e-4, critic_lr=5e-4, acm_lr=0.005, act_noise=0.05, acm_critic=True,
+                   custom_loss=1.0, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=500,
+                   acm_update_batches=200, acm_batch_size=128)),
+    "sac_ant": dict(
+        algo="sac", env="Ant-v2", ob=111, ac=8, envs=4096, buffer=1_000_000, baseline_idx=4,
+        workload="SPP-SAC Ant (111-dim obs), %d vectorized envs per GPU, fp32 MLP (BASELINE.json configs[4] "
+                 "per-GPU shape)",
+        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
+                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
+                   acm_update_batches=100, acm_batch_size=100)),
+}
 
 
 def parse():
@@ -53,73 +70,110 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--rho", type=int, default=100)
-    ap.add_argument("--sigma", type=int, default=10)
-    ap.add_argument("--buffer", type=int, default=1_000_000)
+    ap.add_argument("--config", default="sac_hopper", choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=None)
+    ap.add_argument("--buffer", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
-    """The oracle (CPU restatement of SAC_AcM.update etc., torch 1 thread) run at the
-    reference cadence: per env step one policy act, one grad step of B=100, 1/10 of an
-    ACM batch step of 100, 1/1000 of an obs-stats pass over a 1e6-row buffer."""
+def cpu_baseline(cfg, seconds):
+    """The oracle (CPU restatement of the reference update path, torch 1 thread) run at
+    the reference cadence: per env step one policy act and one grad step of B=100; the
+    ACM regression at its reference rate (sigma/100 batches of 100 per env step); one
+    obs-stats pass over a 1e6-row buffer amortised over an iteration of 1000 frames."""
     import oracle.nets as onets
-    from oracle.acm import OracleAcmTrainer
     from oracle.nets import Norm
-    from oracle.sac_acm import OracleSacAcm
     from tests.golden.weights import fill_params
 
     torch.set_num_threads(1)
     rng = np.random.RandomState(0)
-    lay = {"actor": onets.sac_actor_layout(OB, OB), "critic_1": onets.critic_layout(OB + AC),
-           "critic_2": onets.critic_layout(OB + AC), "critic_1_targ": onets.critic_layout(OB + AC),
-           "critic_2_targ": onets.critic_layout(OB + AC), "acm": onets.acm_layout(2 * OB, AC)}
-    params = {k: fill_params(v, i) for i, (k, v) in enumerate(lay.items())}
-    norm = Norm(True, torch.full((OB,), -2.0), torch.full((OB,), 2.0))
-    o = OracleSacAcm(OB, OB, AC, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm,
-                     acm_lim=np.ones(AC, np.float32), gamma=0.99, params=params)
-    acm = OracleAcmTrainer(2 * OB, AC, lr=1e-3, params=params["acm"])
-    B = 100
-    P = {k: {n: torch.as_tensor(v) for n, v in params[k].items()} for k in ("actor", "acm")}
+    ob, ac = cfg["ob"], cfg["ac"]
+    sac = cfg["algo"] == "sac"
+    norm = Norm(True, torch.full((ob,), -2.0), torch.full((ob,), 2.0))
+    if sac:
+        from oracle.acm import OracleAcmTrainer
+        from oracle.sac_acm import OracleSacAcm
 
-    def act(obs, eps):
-        with torch.no_grad():
-            a, _, _ = onets.sac_actor(P["actor"], obs, torch.tensor(1.0), eps)
-            ad = norm.denormalize(a)
-            return onets.acm(P["acm"], torch.cat([obs, ad], 1), torch.ones(AC))
+        lay = {"actor": onets.sac_actor_layout(ob, ob), "critic_1": onets.critic_layout(ob + ac),
+               "critic_2": onets.critic_layout(ob + ac), "critic_1_targ": onets.critic_layout(ob + ac),
+               "critic_2_targ": onets.critic_layout(ob + ac), "acm": onets.acm_layout(2 * ob, ac)}
+        params = {k: fill_params(v, i) for i, (k, v) in enumerate(lay.items())}
+        o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm,
+                         acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params)
+        acm = OracleAcmTrainer(2 * ob, ac, lr=1e-3, params=params["acm"])
+        P = {k: {n: torch.as_tensor(v) for n, v in params[k].items()} for k in ("actor", "acm")}
+
+        def act(obs):
+            with torch.no_grad():
+                a, _, _ = onets.sac_actor(P["actor"], obs, torch.tensor(1.0), torch.randn(1, ob))
+                return onets.acm(P["acm"], torch.cat([obs, norm.denormalize(a)], 1), torch.ones(ac))
+
+        def upd(batch):
+            o.update(*batch, rng.randn(100, ob).astype(np.float32), rng.randn(100, ob).astype(np.float32))
+
+        acm_step = acm.batch_update
+        acm_every = 100.0 / (cfg["agent"]["acm_update_batches"] * cfg["agent"]["acm_batch_size"] /
+                             cfg["agent"]["acm_update_freq"])
+    else:
+        from oracle.ddpg_acm import OracleDdpgAcm
+
+        lay = {"actor": onets.ddpg_actor_layout(ob, ob), "critic": onets.critic_layout(ob + ac),
+               "actor_targ": onets.ddpg_actor_layout(ob, ob), "critic_targ": onets.critic_layout(ob + ac),
+               "acm": onets.basic_acm_layout(2 * ob, ac)}
+        params = {k: fill_params(v, i) for i, (k, v) in enumerate(lay.items())}
+        o = OracleDdpgAcm(ob, ob, ac, acm_critic=True, custom_loss=1.0, norm_closs=False, norm=norm, gamma=0.95,
+                          params=params)
+        Pa = {n: torch.as_tensor(v) for n, v in params["actor"].items()}
+        Pm = {n: torch.as_tensor(v).clone().requires_grad_(True) for n, v in params["acm"].items()}
+        opt = torch.optim.Adam(Pm.values(), lr=0.005)
+
+        def act(obs):
+            with torch.no_grad():
+                a = onets.ddpg_actor(Pa, obs, torch.tensor(1.0)) + 0.05 * torch.randn(1, ob)
+                return onets.basic_acm(Pm, torch.cat([obs, norm.denormalize(a.clamp(-1.1, 1.1))], 1))
+
+        def upd(batch):
+            o.update(*batch)
+
+        def acm_step(x, y):
+            loss = torch.nn.functional.mse_loss(onets.basic_acm(Pm, torch.as_tensor(x)), torch.as_tensor(y))
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+
+        acm_every = 128.0 / (cfg["agent"]["acm_update_batches"] * cfg["agent"]["acm_batch_size"] /
+                             cfg["agent"]["acm_update_freq"])
 
     t_stats0 = time.perf_counter()
-    big = rng.randn(1_000_000, OB)
+    big = rng.randn(1_000_000, ob)
     big.mean(0), big.std(0), np.percentile(big, 99, axis=0), np.percentile(big, 1, axis=0)
     t_stats = time.perf_counter() - t_stats0
-    n = 0
-    t_upd = t_act = t_acm = 0.0
+    n, acc, t_loop = 0, 0.0, 0.0
+    B = 100
     start = time.perf_counter()
     while time.perf_counter() - start < seconds:
-        obs = torch.from_numpy(rng.randn(1, OB).astype(np.float32))
+        obs = torch.from_numpy(rng.randn(1, ob).astype(np.float32))
+        batch = (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
+                 rng.randn(B, ob).astype(np.float32), rng.randn(B).astype(np.float32),
+                 (rng.rand(B) < 0.01).astype(np.int8), rng.uniform(-1, 1, (B, ac)).astype(np.float32))
+        xa = rng.randn(100 if sac else 128, 2 * ob).astype(np.float32)
+        ya = rng.uniform(-1, 1, (xa.shape[0], ac)).astype(np.float32)
         t0 = time.perf_counter()
-        act(obs, torch.from_numpy(rng.randn(1, OB).astype(np.float32)))
-        t1 = time.perf_counter()
-        batch = (rng.randn(B, OB).astype(np.float32), rng.randn(B, OB).astype(np.float32),
-                 rng.randn(B, OB).astype(np.float32), rng.randn(B).astype(np.float32),
-                 (rng.rand(B) < 0.01).astype(np.int8), rng.uniform(-1, 1, (B, AC)).astype(np.float32))
-        o.update(*batch, rng.randn(B, OB).astype(np.float32), rng.randn(B, OB).astype(np.float32))
-        t2 = time.perf_counter()
-        if n % 10 == 0:
-            acm.batch_update(rng.randn(B, 2 * OB).astype(np.float32), rng.uniform(-1, 1, (B, AC)).astype(np.float32))
-        t3 = time.perf_counter()
-        t_act += t1 - t0
-        t_upd += t2 - t1
-        t_acm += t3 - t2
+        act(obs)
+        upd(batch)
+        acc += 1.0
+        while acc >= acm_every:
+            acm_step(xa, ya)
+            acc -= acm_every
+        t_loop += time.perf_counter() - t0
         n += 1
-    per_step = (t_act + t_upd + t_acm) / n + t_stats / 1000.0
+    per_step = t_loop / n + t_stats / 1000.0
     return {"value": round(1.0 / per_step, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d env steps of the SPP-SAC Hopper reference cadence (1 act + 1 grad step B=100 per env step, "
-                      "ACM batch 100 every 10 steps, obs stats of a 1e6-row buffer amortised /1000); oracle = "
-                      "torch-CPU restatement, 1 thread; %.1f s" % (n, time.perf_counter() - start)}
+            "sample": "%d env steps of the %s reference cadence (1 act + 1 grad step B=100 per env step, ACM "
+                      "regression at its reference rate, obs stats of a 1e6-row buffer amortised /1000); oracle = "
+                      "torch-CPU restatement, 1 thread; %.1f s" % (n, cfg["env"], time.perf_counter() - start)}
 
 
 def main():
@@ -134,86 +188,46 @@ def main():
     torch.cuda.set_device(dev)
 
     import spprl
-    from spprl import _lib
-    from spprl._lib import call, ptr, stream_handle
-    from spprl.dp import make_allreduce, shard_seed
+    from spprl import flops
+    from spprl.dp import shard_seed
 
-    E, rho, sigma = args.envs, args.rho, args.sigma
-    B, BA = rho * E, sigma * E
-    ag = spprl.SAC_AcM(env_name="Hopper-v2", gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2,
-                       acm_lr=1e-3, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
-                       denormalize_actor_out=True, max_batch=max(B, BA), buffer_size=args.buffer, device=dev, seed=0)
-    rb = ag.replay_buffer
-    allreduce = make_allreduce()  # RCCL over xGMI; None at N=1
-
-    g = torch.Generator(device="cpu").manual_seed(1234)  # SynthEnv dynamics: shared across ranks
-    A = (torch.randn(OB, OB, generator=g) * 0.05).to(dev)
+    cfg = CONFIGS[args.config]
+    ob, ac = cfg["ob"], cfg["ac"]
+    E = args.envs or cfg["envs"]
+    cap = args.buffer or cfg["buffer"]
+    a = cfg["agent"]
+    rho = a["update_batch_size"] * a["grad_steps"] / a["update_freq"]
+    sigma = a["acm_update_batches"] * a["acm_batch_size"] / a["acm_update_freq"]
+    B, BA = int(round(rho * E)), int(round(sigma * E))
     seed = shard_seed(1000, rank)
-    st = stream_handle()
+    Agent = spprl.SAC_AcM if cfg["algo"] == "sac" else spprl.DDPG_AcM
+    ag = Agent(env_name=cfg["env"], buffer_size=cap, max_batch=max(B, BA), device=dev, seed=0, n_envs=E,
+               schedule="fused", random_frames=0, batch_size=E, iterations=10 ** 9, loop_seed=seed,
+               acm_epochs=1, **a)
+    rb = ag.replay_buffer
+    assert ag.fused_batch_sizes() == (B, BA)
 
-    # ---- pre-fill the replay shard (min(capacity, 1e6) rows of N(0,1) obs)
+    # ---- pre-fill the replay shard with N(0,1) transitions
     torch.manual_seed(seed)
-    fill = min(args.buffer - 2 * E, 1_000_000 - 2 * E)
-    chunk = 65536
-    prev = rb.add_obs_batch(torch.randn(1, OB, device=dev))
+    fill = cap - 2 * E
+    chunk = 1 << 18
+    prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
     done_fill = 0
     while done_fill < fill:
         n = min(chunk, fill - done_fill)
-        slots = rb.add_obs_batch(torch.randn(n, OB, device=dev))
+        slots = rb.add_obs_batch(torch.randn(n, ob, device=dev))
         prevs = np.concatenate([prev[-1:], slots[:-1]])
-        rb.add_timestep_batch(prevs, slots, torch.randn(n, OB, device=dev), torch.randn(n, device=dev),
-                              torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8,
-                                                                                           device=dev),
-                              torch.rand(n, AC, device=dev) * 2 - 1)
+        z = torch.zeros(n, dtype=torch.uint8, device=dev)
+        rb.add_timestep_batch(prevs, slots, torch.randn(n, ob, device=dev), torch.randn(n, device=dev), z, z,
+                              torch.rand(n, ac, device=dev) * 2 - 1)
         prev = slots
         done_fill += n
     rb.update_obs_mean_std()
-
-    # ---- rollout state
-    obs = torch.randn(E, OB, device=dev)
-    prev_slots = rb.add_obs_batch(obs)
-    ep_t = 0
-    eps = torch.empty(E, OB, device=dev)
-    noise = torch.empty(E, OB, device=dev)
-    nobs = torch.empty(E, OB, device=dev)
-    rew = torch.empty(E, device=dev)
-    zeros_u8 = torch.zeros(E, dtype=torch.uint8, device=dev)
-    ones_u8 = torch.ones(E, dtype=torch.uint8, device=dev)
-    idx = torch.empty(B, dtype=torch.int64, device=dev)
-    idx_acm = torch.empty(BA, dtype=torch.int64, device=dev)
-    xa = torch.empty(BA, 2 * OB, device=dev)
-    ya = torch.empty(BA, AC, device=dev)
-    acm_loss = torch.zeros(1, device=dev)
-    counter = [0]
+    ag.iteration = 1  # past the first iteration: ACM regression is on (ddpg_acm.py:52-57)
+    ag.stats_logger.frames = fill
 
     def vector_step():
-        nonlocal obs, prev_slots, ep_t, nobs
-        c = counter[0]
-        counter[0] += 1
-        # rollout: noisy actor action -> ACM env action (mode 1), then the env
-        call("sppRandNormal", ptr(eps), E * OB, seed, 4 * c, st)
-        call("sppRandNormal", ptr(noise), E * OB, seed, 4 * c + 1, st)
-        tgt, env_act = ag.act(obs, eps=eps, noise=noise, mode=1)
-        call("sppSynthEnvStep", ptr(A), ptr(obs), ptr(env_act), E, OB, AC, ptr(nobs), ptr(rew), st)
-        ep_t += 1
-        end = ep_t >= EP_LEN
-        flag = ones_u8 if end else zeros_u8  # Q3: SPP keeps time-limit done (max_ep_len None)
-        slots = rb.add_obs_batch(nobs)
-        rb.add_timestep_batch(prev_slots, slots, tgt, rew, flag, flag, env_act)
-        obs, nobs = nobs, obs
-        prev_slots = slots
-        if end:
-            obs = torch.randn(E, OB, device=dev)
-            prev_slots = rb.add_obs_batch(obs)
-            ep_t = 0
-        n_live = len(rb)
-        # update: one SAC_AcM grad step on rho*E uniform samples
-        call("sppRandIndex", ptr(idx), B, n_live, seed, 4 * c + 2, st)
-        ag.update_from_replay_dp(idx, seed, c, allreduce)
-        # ACM regression on sigma*E samples
-        call("sppRandIndex", ptr(idx_acm), BA, n_live, seed, 4 * c + 3, st)
-        ag.acm_update_from_replay(idx_acm, xa, ya, acm_loss, allreduce)
-        # obs statistics (replay_buffer.py:83-96)
+        ag.collect_batch_and_train(E)  # act -> env -> replay -> rho*E grad step -> sigma*E ACM step
         rb.update_obs_mean_std()
 
     for _ in range(args.warmup):
@@ -241,23 +255,28 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
 
-    env_steps = world * E * args.steps
-    value = env_steps / elapsed
+    mac = flops.sac_macs(ob, ac) if cfg["algo"] == "sac" else flops.ddpg_macs(ob, ac)
+    value = world * E * args.steps / elapsed
     k_ms = {name: ms[i] / max(cnt[i], 1) for i, name in enumerate(["critic_phase", "actor_phase", "dw_gemm",
                                                                       "adam", "acm_regress"])}
-    crit_tf = 2.0 * CRITIC_PHASE_MAC * B / (k_ms["critic_phase"] * 1e-3) / 1e12
-    act_tf = 2.0 * ACTOR_PHASE_MAC * B / (k_ms["actor_phase"] * 1e-3) / 1e12
-    dw_tf = 2.0 * DW_MAC * B / 2 / (k_ms["dw_gemm"] * 1e-3) / 1e12  # two dW launches per step
+    tf = lambda m, t: 2.0 * m * B / (t * 1e-3) / 1e12  # noqa: E731
+    crit_tf, act_tf = tf(mac["critic_phase"], k_ms["critic_phase"]), tf(mac["actor_phase"], k_ms["actor_phase"])
+    dw_tf = tf(mac["dw"] / 2, k_ms["dw_gemm"])  # two dW launches per grad step
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("critic_phase_bytes_per_launch")
+            key = "critic_phase_bytes_per_launch" if cfg["algo"] == "sac" else "ddpg_critic_phase_bytes_per_launch"
+            t = json.load(open(pmc))
+            if t.get("config", "sac_hopper") == args.config:
+                traffic = t.get(key)
         except Exception:
             traffic = None
-    flop_step = 2.0 * ((CRITIC_PHASE_MAC + ACTOR_PHASE_MAC + DW_MAC) * B + ACM_REG_MAC * BA + (A_MAC + M_MAC) * E)
+    flop_step = 2.0 * (mac["update"] * B + mac["acm_reg"] * BA + mac["act"] * E)
+    kname = "k_sac_critic_phase" if cfg["algo"] == "sac" else "k_ddpg_critic_phase"
     result = {
-        "metric": "env-steps/sec (rollout+update) SPP-SAC Hopper-v2",
+        "metric": "env-steps/sec (rollout+update) %s" % ("SPP-SAC " + cfg["env"] if cfg["algo"] == "sac"
+                                                         else "SPP-DDPG " + cfg["env"]),
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -268,14 +287,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic: SynthEnv linear-tanh dynamics (Hopper shapes ob=11, ac=3), random-init networks",
-        "config": {"workload": "SPP-SAC Hopper-v2, %d vectorized envs per GPU, fp32 (BASELINE.json configs[1])" % E,
-                   "envs_per_gpu": E, "update_batch": B, "acm_batch": BA, "rho": rho, "sigma": sigma,
-                   "replay_rows_per_gpu": args.buffer, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "kernel": "k_sac_critic_phase (critic targets + both critics fwd/bwd)",
+        "data": "synthetic: SynthEnv linear-tanh dynamics (%s shapes ob=%d, ac=%d), random-init networks, replay "
+                "pre-filled with N(0,1) transitions" % (cfg["env"], ob, ac),
+        "config": {"workload": cfg["workload"] % E, "envs_per_gpu": E, "update_batch": B, "acm_batch": BA,
+                   "rho": rho, "sigma": sigma, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world},
+        "roofline": {"bound": "mfma", "kernel": "%s (critic targets + critic fwd/bwd)" % kname,
                      "achieved": round(crit_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(crit_tf / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "flop_per_launch": 2.0 * CRITIC_PHASE_MAC * B, "avg_launch_ms": round(k_ms["critic_phase"], 3)},
+                     "flop_per_launch": 2.0 * mac["critic_phase"] * B, "avg_launch_ms": round(k_ms["critic_phase"], 3)},
         "kernels_ms_per_launch": {k: round(v, 3) for k, v in k_ms.items()},
         "kernels_tflops": {"critic_phase": round(crit_tf, 2), "actor_phase": round(act_tf, 2),
                            "dw_gemm": round(dw_tf, 2)},
@@ -283,7 +302,7 @@ def main():
         "losses": {k: round(v, 5) for k, v in losses.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -188,15 +188,6 @@ class SAC_AcM(OffPolicyLoop):
             allreduce(self.bucket_acm)
         call("sppAcmRegressApply", self._h, st)
 
-    def set_timing(self, on=True):
-        call("sppAgentSetTiming", self._h, int(on))
-
-    def get_timing(self):
-        ms = np.zeros(5, np.float64)
-        cnt = np.zeros(5, np.int64)
-        call("sppAgentGetTiming", self._h, ms.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p))
-        return ms, cnt
-
     @property
     def loss(self):
         v = self._losses.detach().cpu().numpy()

@@ -31,6 +31,7 @@ Envs: ``SynthVecEnv`` (SURVEY.md Appendix A dynamics, on device) or ``HostVecEnv
 buffers and H2D/D2H copies on a side stream).  Everything device-side runs in
 libspprl.so; this module only sequences calls.
 """
+import ctypes
 import time
 
 import numpy as np
@@ -525,6 +526,17 @@ class OffPolicyLoop:
     @property
     def acm_loss(self):
         return float(self._acm_loss_acc.item())
+
+    # ---------------------------------------------------------- per-kernel device timing
+    def set_timing(self, on=True):
+        call("sppAgentSetTiming", self._h, int(on))
+
+    def get_timing(self):
+        """(total ms, launch count) per kind: critic phase, actor phase, dW, Adam, ACM regression."""
+        ms = np.zeros(5, np.float64)
+        cnt = np.zeros(5, np.int64)
+        call("sppAgentGetTiming", self._h, ms.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p))
+        return ms, cnt
 
     # ---------------------------------------------------------- checkpoints (rl.py:286-301)
     def save(self, path):

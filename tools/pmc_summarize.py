@@ -27,7 +27,8 @@ def launch_bytes(prefix):
     return None
 
 
-res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 2 --warmup 1",
+res = {"config": os.environ.get("BENCH_CONFIG", "sac_hopper"),
+       "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 2 --warmup 1",
        "correction": "FETCH_SIZE doubled (gfx950 half-count of wide streaming reads); KB -> B x1024",
        "critic_phase_bytes_per_launch": launch_bytes("k_sac_critic_phase"),
        "actor_phase_bytes_per_launch": launch_bytes("k_sac_actor_phase"),

@@ -7,6 +7,6 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $c -d $R/gpurun_out/pmc_$c -o run --output-format csv \
-     -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $R/gpurun_out/pmc_$c.log 2>&1
+     -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --config ${BENCH_CONFIG:-sac_hopper} > $R/gpurun_out/pmc_$c.log 2>&1
 done
 python3 $R/tools/pmc_summarize.py $R/gpurun_out

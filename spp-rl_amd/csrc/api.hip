@@ -324,7 +324,9 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   for (int col0 = 0; col0 < ob; col0 += G) {
     const int nc = std::min(G, ob - col0);
     for (int shift = 16; shift >= 0; shift -= 8) {
-      hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * 3), dim3(256), sizeof(uint32_t) * nc * 4 * 256, st, h->d, len,
+      const size_t ldsk = sizeof(uint32_t) * nc * 4 * 256;
+      const int resident = std::max(1, std::min(8, (int)((160 * 1024) / ldsk)));  // blocks per CU by LDS
+      hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(256), ldsk, st, h->d, len,
                          col0, nc, shift, (const uint32_t*)h->st_state, h->st_hist);
       hipLaunchKernelGGL(k_stats_sel, dim3(nc), dim3(256), 0, st, h->st_hist, nblk, ob, col0, nc,
                          shift, 0, (const double*)nullptr, len, h->st_state, h->st_mean, max_obs, min_obs,
@@ -382,7 +384,7 @@ sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream)
 sppStatus sppSynthEnvStep(const float* A, const float* obs, const float* action, int E, int ob, int ac,
                           float* next_obs, float* reward, void* stream) {
   SPP_REQUIRE(A && obs && action && next_obs && reward && E > 0, SPP_E_INVALID_ARG, "synth env: bad args");
-  hipLaunchKernelGGL(k_synth_env, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), A, obs, action, E, ob, ac, next_obs,
+  hipLaunchKernelGGL(k_synth_env, dim3(cdiv((int64_t)E * ob, 256)), dim3(256), 0, S(stream), A, obs, action, E, ob, ac, next_obs,
                      reward);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
@@ -1362,7 +1364,8 @@ sppStatus sppAgentStageFromReplay(sppAgentHandle a, sppReplayHandle r, const int
   SPP_REQUIRE(a && r && idx && B > 0 && B <= a->Bmax, SPP_E_INVALID_ARG, "stage_from_replay: bad args");
   SPP_REQUIRE(r->d.ob == a->cfg.ob && r->d.ac == a->cfg.ac && r->d.aout == a->cfg.aout, SPP_E_SHAPE, "dims differ");
   const int Bp = (int)round_up(B, 32);
-  hipLaunchKernelGGL(k_replay_stage_fm, dim3(cdiv(Bp, 256)), dim3(256), 0, S(stream), r->d, idx, B, Bp, a->S, a->S2,
+  hipLaunchKernelGGL(k_replay_stage_fm, dim3(cdiv(Bp, kStageTile)), dim3(256),
+                     sizeof(float) * kStageTile * std::max(r->d.ob, r->d.aout), S(stream), r->d, idx, B, Bp, a->S, a->S2,
                      a->cfg.acm_critic ? nullptr : a->ACT, a->AENV, a->R, a->DN);
   SPP_CHECK_HIP(hipGetLastError());
   a->cur_B = B;
@@ -1438,7 +1441,7 @@ sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, in
 
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx, int B, float* x, float* y, void* stream) {
   SPP_REQUIRE(h && idx && x && y && B > 0, SPP_E_INVALID_ARG, "gather_acm: bad args");
-  hipLaunchKernelGGL(k_replay_gather_acm, dim3(cdiv(B, 256)), dim3(256), 0, S(stream), h->d, idx, B, x, y);
+  hipLaunchKernelGGL(k_replay_gather_acm, dim3(cdiv(B, kStageTile)), dim3(256), 0, S(stream), h->d, idx, B, x, y);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

@@ -51,36 +51,77 @@ __global__ void k_replay_gather_rm(ReplayDev r, const int64_t* __restrict__ idx,
 
 // Fused sample -> feature-major staging of the update batch (zero padded to Bp).
 // One thread per (sample, feature-row) so each feature row is written coalesced.
-__global__ void k_replay_stage_fm(ReplayDev r, const int64_t* __restrict__ idx, int B, int Bp, float* S, float* S2,
-                                  float* ACT, float* AENV, float* R, float* DN) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= Bp) return;
-  const bool v = b < B;
-  const int64_t t = v ? idx[b] : 0;
-  const int64_t o = v ? r.obs_idx[t] : 0, n = v ? r.next_idx[t] : 0;
-  for (int f = 0; f < r.ob; ++f) {
-    S[f * (int64_t)Bp + b] = v ? r.obs[o * r.ob + f] : 0.f;
-    S2[f * (int64_t)Bp + b] = v ? r.obs[n * r.ob + f] : 0.f;
+// Tile of kStageTile samples per 256-thread workgroup: each replay row is read
+// contiguously (consecutive lanes = consecutive floats of one row), staged in LDS
+// [tile][w], then written feature-major (consecutive lanes = consecutive samples),
+// so both the random-row gather and the transposed store are coalesced.
+constexpr int kStageTile = 64;
+
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, const int64_t* rows, int w, int valid,
+                                           float* lds, float* dst, int64_t Bp, int64_t b0) {
+  // rows [b0, b0 + kStageTile) of the padded batch; only b < Bp exist in dst
+  const int n = kStageTile * w;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int s = i / w, f = i - s * w;
+    lds[s * w + f] = s < valid ? src[rows[s] * w + f] : 0.f;
   }
-  if (ACT)
-    for (int f = 0; f < r.aout; ++f) ACT[f * (int64_t)Bp + b] = v ? r.act[t * r.aout + f] : 0.f;
-  for (int f = 0; f < r.ac; ++f) AENV[f * (int64_t)Bp + b] = v ? r.acm[t * r.ac + f] : 0.f;
-  R[b] = v ? r.rew[t] : 0.f;
-  DN[b] = v ? (float)r.done[t] : 0.f;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int f = i / kStageTile, s = i - f * kStageTile;
+    if (b0 + s < Bp) dst[f * Bp + b0 + s] = lds[s * w + f];
+  }
+  __syncthreads();
 }
 
-// rbuffer_sample_acm (:404-430) + AcMTrainer.acm_cat (acm.py:260-264)
-__global__ void k_replay_gather_acm(ReplayDev r, const int64_t* __restrict__ idx, int B, float* x, float* y) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int64_t t = idx[b];
-  const int64_t o = r.obs_idx[t], n = r.next_idx[t];
-  const int ob = r.ob;
-  for (int f = 0; f < ob; ++f) {
-    x[(int64_t)b * 2 * ob + f] = r.obs[o * ob + f];
-    x[(int64_t)b * 2 * ob + ob + f] = r.obs[n * ob + f];
+__global__ __launch_bounds__(256) void k_replay_stage_fm(ReplayDev r, const int64_t* __restrict__ idx, int B, int Bp,
+                                                         float* S, float* S2, float* ACT, float* AENV, float* R,
+                                                         float* DN) {
+  extern __shared__ float stg[];  // [kStageTile][max(ob, aout)]
+  __shared__ int64_t rt[kStageTile], ro[kStageTile], rn[kStageTile];
+  const int64_t b0 = (int64_t)blockIdx.x * kStageTile;
+  const int valid = (int)min((int64_t)kStageTile, (int64_t)B - b0 > 0 ? (int64_t)B - b0 : 0);
+  if (threadIdx.x < kStageTile) {
+    const int s = threadIdx.x;
+    const int64_t t = s < valid ? idx[b0 + s] : 0;
+    rt[s] = t;
+    ro[s] = s < valid ? r.obs_idx[t] : 0;
+    rn[s] = s < valid ? r.next_idx[t] : 0;
+    if (b0 + s < Bp) {
+      R[b0 + s] = s < valid ? r.rew[t] : 0.f;
+      DN[b0 + s] = s < valid ? (float)r.done[t] : 0.f;
+    }
   }
-  for (int f = 0; f < r.ac; ++f) y[(int64_t)b * r.ac + f] = r.acm[t * r.ac + f];
+  __syncthreads();
+  stage_rows(r.obs, ro, r.ob, valid, stg, S, Bp, b0);
+  stage_rows(r.obs, rn, r.ob, valid, stg, S2, Bp, b0);
+  if (ACT) stage_rows(r.act, rt, r.aout, valid, stg, ACT, Bp, b0);
+  stage_rows(r.acm, rt, r.ac, valid, stg, AENV, Bp, b0);
+}
+
+// rbuffer_sample_acm (:404-430) + AcMTrainer.acm_cat (acm.py:260-264): row-major
+// x[b] = [obs | next_obs], y[b] = acm action; kStageTile samples per workgroup,
+// consecutive lanes read and write consecutive floats of one row.
+__global__ __launch_bounds__(256) void k_replay_gather_acm(ReplayDev r, const int64_t* __restrict__ idx, int B,
+                                                           float* x, float* y) {
+  __shared__ int64_t rt[kStageTile], ro[kStageTile], rn[kStageTile];
+  const int64_t b0 = (int64_t)blockIdx.x * kStageTile;
+  const int valid = (int)min((int64_t)kStageTile, (int64_t)B - b0);
+  if (threadIdx.x < valid) {
+    const int64_t t = idx[b0 + threadIdx.x];
+    rt[threadIdx.x] = t;
+    ro[threadIdx.x] = r.obs_idx[t];
+    rn[threadIdx.x] = r.next_idx[t];
+  }
+  __syncthreads();
+  const int ob = r.ob, w = 2 * ob;
+  for (int i = threadIdx.x; i < valid * w; i += blockDim.x) {
+    const int s = i / w, f = i - s * w;
+    x[(b0 + s) * w + f] = f < ob ? r.obs[ro[s] * ob + f] : r.obs[rn[s] * ob + (f - ob)];
+  }
+  for (int i = threadIdx.x; i < valid * r.ac; i += blockDim.x) {
+    const int s = i / r.ac, f = i - s * r.ac;
+    y[(b0 + s) * r.ac + f] = r.acm[rt[s] * r.ac + f];
+  }
 }
 
 // ---------------------------------------------------------------- obs statistics
@@ -108,6 +149,7 @@ __device__ __forceinline__ float funkey(uint32_t k) {
 constexpr int kStatsBlocks = 1024;      // pass-1 workgroups (moment partials)
 constexpr int kStatsColsPerThread = 8;  // columns per tx lane (ob <= 128)
 constexpr int kStatsRows = 8;           // rows in flight per thread (index then row loads)
+constexpr int kStatsRowsK = 16;         // passes 2-4: fewer resident waves (64 KiB LDS) -> more loads in flight
 
 // Non-zero LDS bins -> the global histogram (device atomics; sparse after pass 1).
 __device__ __forceinline__ void flush_hist(const uint32_t* sh, int n, uint32_t* g) {
@@ -202,10 +244,10 @@ __global__ __launch_bounds__(256) void k_stats_pk(ReplayDev r, int64_t len, int 
     }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * 16;
-  for (int64_t i0 = (int64_t)blockIdx.x * 16 + ty; i0 < len; i0 += stride * kStatsRows) {
-    int64_t base[kStatsRows];
+  for (int64_t i0 = (int64_t)blockIdx.x * 16 + ty; i0 < len; i0 += stride * kStatsRowsK) {
+    int64_t base[kStatsRowsK];
 #pragma unroll
-    for (int k = 0; k < kStatsRows; ++k) {
+    for (int k = 0; k < kStatsRowsK; ++k) {
       const int64_t i = i0 + k * stride;
       base[k] = i < len ? r.obs_idx[i] * ob + col0 : -1;
     }
@@ -213,11 +255,11 @@ __global__ __launch_bounds__(256) void k_stats_pk(ReplayDev r, int64_t len, int 
     for (int j = 0; j < kStatsColsPerThread; ++j) {
       const int c = tx + 16 * j;
       if (c >= ncols) break;
-      uint32_t kk[kStatsRows];
+      uint32_t kk[kStatsRowsK];
 #pragma unroll
-      for (int k = 0; k < kStatsRows; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
+      for (int k = 0; k < kStatsRowsK; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
 #pragma unroll
-      for (int k = 0; k < kStatsRows; ++k)
+      for (int k = 0; k < kStatsRowsK; ++k)
         if (base[k] >= 0)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -366,21 +408,23 @@ __global__ void k_rand_index(int64_t* out, int64_t n, int64_t high, uint64_t see
 // SURVEY.md Appendix A SynthEnv: s' = tanh(A s) + 0.1 * resize(a, ob); r = -|a|^2 + s'[0]
 __global__ void k_synth_env(const float* A, const float* obs, const float* act, int E, int ob, int ac, float* nobs,
                             float* rew) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const float* s = obs + (int64_t)e * ob;
-  const float* a = act + (int64_t)e * ac;
-  float s0 = 0.f;
-  for (int i = 0; i < ob; ++i) {
-    float acc = 0.f;
-    for (int j = 0; j < ob; ++j) acc = fmaf(A[i * ob + j], s[j], acc);
-    const float v = tanhf(acc) + 0.1f * a[i % ac];
-    nobs[(int64_t)e * ob + i] = v;
-    if (i == 0) s0 = v;
+  // one thread per (env, state unit): s'_i = tanh(A_i . s) + 0.1 a[i % ac]; unit 0 also writes r
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)E * ob) return;
+  const int64_t e = t / ob;
+  const int i = (int)(t - e * ob);
+  const float* s = obs + e * ob;
+  const float* a = act + e * ac;
+  const float* Ai = A + (int64_t)i * ob;
+  float acc = 0.f;
+  for (int j = 0; j < ob; ++j) acc = fmaf(Ai[j], s[j], acc);
+  const float v = tanhf(acc) + 0.1f * a[i % ac];
+  nobs[t] = v;
+  if (i == 0) {
+    float n2 = 0.f;
+    for (int j = 0; j < ac; ++j) n2 = fmaf(a[j], a[j], n2);
+    rew[e] = -n2 + v;
   }
-  float n2 = 0.f;
-  for (int j = 0; j < ac; ++j) n2 = fmaf(a[j], a[j], n2);
-  rew[e] = -n2 + s0;
 }
 
 

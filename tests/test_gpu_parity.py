@@ -247,3 +247,69 @@ def test_staged_update_runs_and_is_finite():
         assert all(np.isfinite(v) for v in ag.loss.values())
         outs.append(p)
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def _filled_agent(env_name, ob, ac, n_rows, seed=1, max_batch=4096):
+    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
+                       denormalize_actor_out=True, max_batch=max_batch, buffer_size=n_rows + 64, device=DEV, seed=seed)
+    rb = ag.replay_buffer
+    rng = np.random.RandomState(0)
+    slots = rb.add_obs_batch(torch.from_numpy(rng.randn(n_rows + 1, ob).astype(np.float32)))
+    rb.add_timestep_batch(slots[:n_rows], slots[1:], torch.from_numpy(rng.randn(n_rows, ob).astype(np.float32)),
+                          rng.randn(n_rows).astype(np.float32), rng.rand(n_rows) < 0.05, rng.rand(n_rows) < 0.05,
+                          torch.from_numpy(rng.uniform(-1, 1, (n_rows, ac)).astype(np.float32)))
+    rb.update_obs_mean_std()
+    return ag
+
+
+@pytest.mark.parametrize("env_name,ob,ac,B", [("Hopper-v2", 11, 3, 1000), ("Ant-v2", 111, 8, 613)])
+def test_replay_staged_update_bit_exact_vs_explicit_batch(env_name, ob, ac, B):
+    """sppAgentStageFromReplay (tiled random-row gather -> feature-major scratch, ragged last
+    tile) feeds the same kernels as the caller-batch path: identical bits after a full step."""
+    a1 = _filled_agent(env_name, ob, ac, 3000)
+    a2 = _filled_agent(env_name, ob, ac, 3000)
+    idx = torch.from_numpy(np.random.RandomState(5).randint(0, 3000, B)).to(DEV)
+    rng = np.random.RandomState(9)
+    e1 = torch.from_numpy(rng.randn(B, ob).astype(np.float32)).to(DEV)
+    e2 = torch.from_numpy(rng.randn(B, ob).astype(np.float32)).to(DEV)
+    st = _lib.stream_handle()
+    _lib.call("sppAgentStageFromReplay", a1._h, a1.replay_buffer._h, _lib.ptr(idx), B, st)
+    _lib.call("sppSacAcmCriticGrads", a1._h, None, _lib.ptr(e1), _lib.ptr(a1._losses), st)
+    _lib.call("sppSacAcmCriticApply", a1._h, st)
+    _lib.call("sppSacAcmActorGrads", a1._h, _lib.ptr(e2), _lib.ptr(a1._losses), st)
+    _lib.call("sppSacAcmActorApply", a1._h, _lib.ptr(a1._losses), st)
+    a2.update(*a2.replay_buffer.gather(idx), eps_next=e1, eps_cur=e2)
+    torch.cuda.synchronize()
+    for net in (_lib.SPP_NET_ACTOR, _lib.SPP_NET_CRITIC1, _lib.SPP_NET_CRITIC2):
+        np.testing.assert_array_equal(a1.params[net].cpu().numpy(), a2.params[net].cpu().numpy())
+    assert a1.loss == a2.loss
+
+
+@pytest.mark.parametrize("env_name,ob,ac,B", [("Hopper-v2", 11, 3, 1000), ("Ant-v2", 111, 8, 613)])
+def test_replay_gather_acm_bit_exact(env_name, ob, ac, B):
+    ag = _filled_agent(env_name, ob, ac, 3000)
+    rb = ag.replay_buffer
+    idx = torch.from_numpy(np.random.RandomState(7).randint(0, 3000, B)).to(DEV)
+    x = torch.empty(B, 2 * ob, device=DEV)
+    y = torch.empty(B, ac, device=DEV)
+    _lib.call("sppReplayGatherAcm", rb._h, _lib.ptr(idx), B, _lib.ptr(x), _lib.ptr(y), _lib.stream_handle())
+    o, no, _, _, _, acm = rb.gather(idx)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(x.cpu().numpy(), torch.cat([o, no], 1).cpu().numpy())
+    np.testing.assert_array_equal(y.cpu().numpy(), acm.cpu().numpy())
+
+
+def test_synth_env_step_matches_numpy():
+    E, ob, ac = 37, 111, 8
+    rng = np.random.RandomState(3)
+    A = (rng.randn(ob, ob) * 0.05).astype(np.float32)
+    s = rng.randn(E, ob).astype(np.float32)
+    a = rng.uniform(-1, 1, (E, ac)).astype(np.float32)
+    dA, ds, da = (torch.from_numpy(v).to(DEV) for v in (A, s, a))
+    ns = torch.empty(E, ob, device=DEV)
+    r = torch.empty(E, device=DEV)
+    _lib.call("sppSynthEnvStep", _lib.ptr(dA), _lib.ptr(ds), _lib.ptr(da), E, ob, ac, _lib.ptr(ns), _lib.ptr(r),
+              _lib.stream_handle())
+    ref = np.tanh(s.astype(np.float64) @ A.T.astype(np.float64)) + 0.1 * np.resize(a, (E, ac))[:, np.arange(ob) % ac]
+    np.testing.assert_allclose(ns.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(r.cpu().numpy(), -np.square(a).sum(1) + ref[:, 0], rtol=1e-5, atol=1e-5)

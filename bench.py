@@ -222,13 +222,13 @@ def main():
                               torch.rand(n, ac, device=dev) * 2 - 1)
         prev = slots
         done_fill += n
-    rb.update_obs_mean_std()
+    ag.update_obs_stats()
     ag.iteration = 1  # past the first iteration: ACM regression is on (ddpg_acm.py:52-57)
     ag.stats_logger.frames = fill
 
     def vector_step():
         ag.collect_batch_and_train(E)  # act -> env -> replay -> rho*E grad step -> sigma*E ACM step
-        rb.update_obs_mean_std()
+        ag.update_obs_stats()  # global across ranks (RCCL) when N > 1
 
     for _ in range(args.warmup):
         vector_step()

@@ -85,6 +85,19 @@ sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx_dev, int B, floa
  * written (first_update != 0 overwrites them). */
 sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
                             int first_update, void* stream);
+/* Data-parallel update_obs_mean_std over the union of the ranks' replay shards
+ * (SURVEY.md §8e): exact global mean / std (fp64 sums about a replicated pivot,
+ * e.g. the current obs_mean) and exact global 99th / 1st percentiles (radix select
+ * over all-reduced histograms).  Call with step = 0, 1, 2, ... until *done:
+ *   step 0   local pass 1 -> sums[ob][2] (fp64) and hist (top byte)
+ *   step k   selection with the global counts (n_global = sum of the ranks' len),
+ *            then the next local byte pass -> hist
+ * and all-reduce (sum) `sums` after step 0 and `hist` after every step that did
+ * not set *done.  hist: sppReplayObsStatsDPHistSize(h) uint32 counters. */
+int sppReplayObsStatsDPHistSize(sppReplayHandle h);
+sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot /*[ob], replicated*/,
+                              double* sums /*[ob][2]*/, uint32_t* hist, int64_t n_global, float* mean, float* std,
+                              float* max_obs, float* min_obs, int first_update, int* done, void* stream);
 /* Raw device pointers of the ring (for the fused sample+update path). */
 typedef struct {
   float* obs;          /* [capacity][ob]    */

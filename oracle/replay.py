@@ -107,3 +107,59 @@ def percentile_linear(col_sorted, q):
     a, b = col_sorted[lo], col_sorted[hi]
     diff = b - a
     return (b - diff * (1 - g)) if g >= 0.5 else (a + diff * g)
+
+
+def _fkey(x):
+    """float32 -> order-preserving uint32 key (the device kernels' fkey)."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000).astype(np.uint64)
+
+
+def _funkey(k):
+    k = np.uint64(k)
+    u = (k & np.uint64(0x7FFFFFFF)) if (k & np.uint64(0x80000000)) else ((~k) & np.uint64(0xFFFFFFFF))
+    return np.array([u], np.uint32).view(np.float32)[0]
+
+
+def dp_obs_stats(shard, allreduce_sum, pivot):
+    """Data-parallel update_obs_mean_std (replay_buffer.py:83-96) over the union of the
+    ranks' shards, the protocol of sppReplayObsStatsDP restated: fp64 sums about a
+    replicated pivot and 8-bit radix selects of numpy's 'linear' percentile neighbours
+    (ranks floor((n-1)q) and +1) over histograms all-reduced across ranks.
+    shard: (n_r, ob) float32.  allreduce_sum(np array) -> summed array.  Returns
+    (mean, std, p99, p1) as float32."""
+    x = np.asarray(shard, np.float32)
+    ob = x.shape[1]
+    d = x.astype(np.float64) - np.asarray(pivot, np.float32).astype(np.float64)
+    sums = allreduce_sum(np.concatenate([d.sum(0), (d * d).sum(0)]))
+    n = int(allreduce_sum(np.array([x.shape[0]], np.int64))[0])
+    m1 = sums[:ob] / n
+    mean = (np.asarray(pivot, np.float64) + m1).astype(np.float32)
+    std = np.sqrt(np.maximum(sums[ob:] / n - m1 * m1, 0.0)).astype(np.float32)
+    keys = _fkey(x)
+    out = []
+    for q in (0.99, 0.01):
+        vi = (n - 1) * q
+        lo = int(np.floor(vi))
+        vals = []
+        for rank in (lo, min(lo + 1, n - 1)):
+            col = []
+            for c in range(ob):
+                prefix, mask, r = 0, 0, rank
+                for shift in (24, 16, 8, 0):
+                    sel = (keys[:, c] & np.uint64(mask)) == np.uint64(prefix)
+                    h = np.bincount(((keys[sel, c] >> np.uint64(shift)) & np.uint64(255)).astype(np.int64),
+                                    minlength=256).astype(np.int64)
+                    h = allreduce_sum(h)
+                    cum = np.cumsum(h)
+                    b = int(np.searchsorted(cum, r, side="right"))
+                    r -= int(cum[b - 1]) if b > 0 else 0
+                    prefix |= b << shift
+                    mask |= 255 << shift
+                col.append(_funkey(prefix))
+            vals.append(np.array(col, np.float64))
+        g = vi - lo
+        a, b = vals
+        diff = b - a
+        out.append(np.where(g >= 0.5, b - diff * (1.0 - g), a + diff * g).astype(np.float32))  # numpy _lerp
+    return mean, std, out[0], out[1]

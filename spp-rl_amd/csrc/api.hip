@@ -292,18 +292,11 @@ sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* v) {
   return SPP_OK;
 }
 
-sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
-                            int first_update, void* stream) {
-  SPP_REQUIRE(h && mean && std && max_obs && min_obs, SPP_E_INVALID_ARG, "obs_stats: bad args");
-  const int64_t len = h->len;
-  if (len <= 10) return SPP_OK;  // replay_buffer.py:84
-  SPP_REQUIRE(len < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats: len too large");
+static sppStatus stats_alloc(sppReplayHandle h) {
   const int ob = h->d.ob;
-  SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats: ob %d > %d", ob, 16 * kStatsColsPerThread);
-  const int nblk = kStatsBlocks;
-  const int G = std::min(ob, 32);  // columns per byte pass (LDS: G*4*256*4 B)
+  const int G = std::min(ob, 32);
   if (!h->st_part) {
-    SPP_CHECK_HIP(hipMalloc(&h->st_part, sizeof(double) * nblk * ob * 2));
+    SPP_CHECK_HIP(hipMalloc(&h->st_part, sizeof(double) * kStatsBlocks * ob * 2));
     SPP_CHECK_HIP(hipMalloc(&h->st_mean, sizeof(double) * ob * 2));
     SPP_CHECK_HIP(hipMalloc(&h->st_state, sizeof(uint32_t) * ob * 4 * 3));
     SPP_CHECK_HIP(hipMalloc(&h->st_hist, sizeof(uint32_t) * std::max(ob, G * 4) * 256));
@@ -315,22 +308,108 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
       attr = true;
     }
   }
-  hipStream_t st = S(stream);
+  return SPP_OK;
+}
+
+static void stats_pass1(sppReplayHandle h, uint32_t* hist, const float* pivot, hipStream_t st) {
+  const int ob = h->d.ob;
   const size_t lds1 = sizeof(uint32_t) * (((ob * 256 + 1) & ~1)) + sizeof(double) * 16 * 16 * 2;
-  hipLaunchKernelGGL(k_stats_p1, dim3(nblk), dim3(256), lds1, st, h->d, len, h->st_hist, h->st_part);
-  hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, h->st_hist, nblk, ob, 0, ob, 24, 1,
+  hipLaunchKernelGGL(k_stats_p1, dim3(kStatsBlocks), dim3(256), lds1, st, h->d, h->len, hist, h->st_part, pivot);
+}
+
+// byte pass p (0-based) of the per-group radix select: (group col0, shift)
+static void stats_pass_coords(int ob, int p, int* col0, int* nc, int* shift) {
+  const int G = std::min(ob, 32);
+  *col0 = (p / 3) * G;
+  *nc = std::min(G, ob - *col0);
+  *shift = 16 - 8 * (p % 3);
+}
+
+static void stats_pk(sppReplayHandle h, int p, uint32_t* hist, hipStream_t st) {
+  int col0, nc, shift;
+  stats_pass_coords(h->d.ob, p, &col0, &nc, &shift);
+  const size_t ldsk = sizeof(uint32_t) * nc * 4 * 256;
+  const int resident = std::max(1, std::min(8, (int)((160 * 1024) / ldsk)));  // blocks per CU by LDS
+  hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(256), ldsk, st, h->d, h->len, col0, nc, shift,
+                     (const uint32_t*)h->st_state, hist);
+}
+
+static void stats_sel(sppReplayHandle h, int p, uint32_t* hist, int64_t n, float* max_obs, float* min_obs,
+                      int first_update, hipStream_t st) {
+  int col0, nc, shift;
+  stats_pass_coords(h->d.ob, p, &col0, &nc, &shift);
+  hipLaunchKernelGGL(k_stats_sel, dim3(nc), dim3(256), 0, st, hist, kStatsBlocks, h->d.ob, col0, nc, shift, 0,
+                     (const double*)nullptr, n, h->st_state, h->st_mean, max_obs, min_obs, first_update);
+}
+
+sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
+                            int first_update, void* stream) {
+  SPP_REQUIRE(h && mean && std && max_obs && min_obs, SPP_E_INVALID_ARG, "obs_stats: bad args");
+  const int64_t len = h->len;
+  if (len <= 10) return SPP_OK;  // replay_buffer.py:84
+  SPP_REQUIRE(len < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats: len too large");
+  const int ob = h->d.ob;
+  SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats: ob %d > %d", ob, 16 * kStatsColsPerThread);
+  sppStatus s = stats_alloc(h);
+  if (s) return s;
+  hipStream_t st = S(stream);
+  stats_pass1(h, h->st_hist, nullptr, st);
+  hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, h->st_hist, kStatsBlocks, ob, 0, ob, 24, 1,
                      (const double*)h->st_part, len, h->st_state, h->st_mean, max_obs, min_obs, first_update);
-  hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std);
-  for (int col0 = 0; col0 < ob; col0 += G) {
-    const int nc = std::min(G, ob - col0);
-    for (int shift = 16; shift >= 0; shift -= 8) {
-      const size_t ldsk = sizeof(uint32_t) * nc * 4 * 256;
-      const int resident = std::max(1, std::min(8, (int)((160 * 1024) / ldsk)));  // blocks per CU by LDS
-      hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(256), ldsk, st, h->d, len,
-                         col0, nc, shift, (const uint32_t*)h->st_state, h->st_hist);
-      hipLaunchKernelGGL(k_stats_sel, dim3(nc), dim3(256), 0, st, h->st_hist, nblk, ob, col0, nc,
-                         shift, 0, (const double*)nullptr, len, h->st_state, h->st_mean, max_obs, min_obs,
-                         first_update);
+  hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std,
+                     (const float*)nullptr);
+  const int npass = 3 * ((ob + std::min(ob, 32) - 1) / std::min(ob, 32));
+  for (int p = 0; p < npass; ++p) {
+    stats_pk(h, p, h->st_hist, st);
+    stats_sel(h, p, h->st_hist, len, max_obs, min_obs, first_update, st);
+  }
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+int sppReplayObsStatsDPHistSize(sppReplayHandle h) {
+  if (!h) return -1;
+  const int ob = h->d.ob;
+  return std::max(ob, std::min(ob, 32) * 4) * 256;
+}
+
+sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot, double* sums, uint32_t* hist,
+                              int64_t n_global, float* mean, float* std, float* max_obs, float* min_obs,
+                              int first_update, int* done, void* stream) {
+  SPP_REQUIRE(h && pivot && sums && hist && mean && std && max_obs && min_obs && done && step >= 0,
+              SPP_E_INVALID_ARG, "obs_stats_dp: bad args");
+  const int ob = h->d.ob;
+  SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats_dp: ob %d > %d", ob, 16 * kStatsColsPerThread);
+  SPP_REQUIRE(n_global > 10 && n_global < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats_dp: n_global %lld",
+              (long long)n_global);
+  sppStatus s = stats_alloc(h);
+  if (s) return s;
+  hipStream_t st = S(stream);
+  const int npass = 3 * ((ob + std::min(ob, 32) - 1) / std::min(ob, 32));
+  SPP_REQUIRE(step <= npass + 1, SPP_E_INVALID_ARG, "obs_stats_dp: step %d > %d", step, npass + 1);
+  *done = 0;
+  if (step == 0) {  // local pass 1 -> sums [ob][2] about the shared pivot, top-byte histogram
+    SPP_CHECK_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * sppReplayObsStatsDPHistSize(h), st));
+    if (h->len > 0) {
+      stats_pass1(h, hist, pivot, st);
+      hipLaunchKernelGGL(k_stats_reduce_part, dim3(ob), dim3(256), 0, st, (const double*)h->st_part, kStatsBlocks,
+                         ob, sums);
+    } else {
+      SPP_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * ob * 2, st));
+    }
+  } else {
+    if (step == 1) {  // global top byte + moments
+      hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, hist, 1, ob, 0, ob, 24, 1, (const double*)sums,
+                         n_global, h->st_state, h->st_mean, max_obs, min_obs, first_update);
+      hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std,
+                         pivot);
+    } else {
+      stats_sel(h, step - 2, hist, n_global, max_obs, min_obs, first_update, st);
+    }
+    if (step - 1 < npass) {
+      if (h->len > 0) stats_pk(h, step - 1, hist, st);
+    } else {
+      *done = 1;
     }
   }
   SPP_CHECK_HIP(hipGetLastError());

@@ -160,13 +160,13 @@ __device__ __forceinline__ void flush_hist(const uint32_t* sh, int n, uint32_t* 
 }
 
 __global__ __launch_bounds__(256) void k_stats_p1(ReplayDev r, int64_t len, uint32_t* __restrict__ ghist,
-                                                  double* __restrict__ part) {
+                                                  double* __restrict__ part, const float* __restrict__ pivot) {
   extern __shared__ uint32_t sh1[];  // [ob][256] + reduction scratch
   const int ob = r.ob;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   for (int i = threadIdx.x; i < ob * 256; i += blockDim.x) sh1[i] = 0;
   __syncthreads();
-  const float* p0 = r.obs + r.obs_idx[0] * ob;
+  const float* p0 = pivot ? pivot : r.obs + r.obs_idx[0] * ob;  // moment shift
   double s1[kStatsColsPerThread], s2[kStatsColsPerThread];
   float piv[kStatsColsPerThread];
 #pragma unroll
@@ -361,11 +361,38 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
   }
 }
 
+// Sum of the pass-1 block partials per column -> out[ob][2] (the data-parallel
+// exchange operand: ranks all-reduce these sums and their histograms).
+__global__ void k_stats_reduce_part(const double* __restrict__ part, int nblk, int ob, double* __restrict__ out) {
+  __shared__ double rd[2][256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int k = t; k < nblk; k += 256) {
+    a += part[((int64_t)k * ob + c) * 2 + 0];
+    b += part[((int64_t)k * ob + c) * 2 + 1];
+  }
+  rd[0][t] = a;
+  rd[1][t] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      rd[0][t] += rd[0][t + o];
+      rd[1][t] += rd[1][t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[c * 2 + 0] = rd[0][0];
+    out[c * 2 + 1] = rd[1][0];
+  }
+}
+
 // mean = pivot + E[x - pivot]; std from the shifted moments (fp32 casts, replay_buffer.py:87-90)
-__global__ void k_stats_moments_out(ReplayDev r, const double* mom, float* mean_out, float* std_out) {
+__global__ void k_stats_moments_out(ReplayDev r, const double* mom, float* mean_out, float* std_out,
+                                    const float* pivot) {
   const int c = threadIdx.x;
   if (c >= r.ob) return;
-  const double piv = (double)r.obs[r.obs_idx[0] * r.ob + c];
+  const double piv = (double)(pivot ? pivot[c] : r.obs[r.obs_idx[0] * r.ob + c]);
   mean_out[c] = (float)(piv + mom[c * 2 + 0]);
   std_out[c] = (float)mom[c * 2 + 1];
 }

@@ -122,6 +122,9 @@ _SIGS = {
     "sppEpisodeAccum": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "sppSynthEnvReset": (c_int, [c_void_p, c_void_p, c_int, c_int, c_uint64, c_uint64, c_void_p]),
     "sppAgentSetLr": (c_int, [c_void_p, c_float, c_float, c_float, c_float]),
+    "sppReplayObsStatsDPHistSize": (c_int, [c_void_p]),
+    "sppReplayObsStatsDP": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_int, P(c_int), c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -29,6 +29,18 @@ def make_allreduce(group=None):
     return allreduce
 
 
+def make_allreduce_sum(group=None):
+    """Returns ``allreduce_sum(t)`` (in-place sum over the group; exact for integer
+    histograms, fp64 for moment sums) or None with a single rank."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return None
+
+    def allreduce_sum(t):
+        dist.all_reduce(t, group=group)
+
+    return allreduce_sum
+
+
 def shard_seed(base, rank):
     """Per-rank seed of the env / sampling / eps streams (ranks must differ)."""
     return int(base) + 1000 * int(rank)

@@ -142,6 +142,45 @@ class BufferAcMOffPolicy:
              ptr(self.min_obs), 0 if self._have_minmax else 1, stream_handle())
         self._have_minmax = True
 
+    def update_obs_mean_std_dp(self, allreduce_sum, n_global=None):
+        """update_obs_mean_std over the union of the data-parallel ranks' shards (SURVEY.md
+        §8e): ``allreduce_sum(t)`` sums a device tensor in place across ranks (RCCL).  Exact
+        global percentiles (radix select on all-reduced histograms); mean / std from fp64
+        sums about the replicated current mean.  ``n_global`` (total live rows) may be given
+        when known on the host; otherwise it is all-reduced (one host sync)."""
+        if n_global is None:
+            n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
+            allreduce_sum(n)
+            n_global = int(n.item())
+        if n_global <= 10:  # replay_buffer.py:84, on the global buffer
+            return
+        if getattr(self, "_dp_hist", None) is None:
+            hs = _lib.load().sppReplayObsStatsDPHistSize(self._h)
+            self._dp_hist = torch.zeros(hs, dtype=torch.int32, device=self.device)
+            self._dp_sums = torch.zeros(self.obs_shape, 2, dtype=torch.float64, device=self.device)
+            self._dp_pivot = torch.zeros(self.obs_shape, device=self.device)
+        for step in self.obs_stats_dp_steps(n_global):
+            if step == 0:
+                allreduce_sum(self._dp_sums)
+            allreduce_sum(self._dp_hist)
+
+    def obs_stats_dp_steps(self, n_global):
+        """Generator over the stepwise protocol: yields after each step whose outputs
+        (sums after step 0, hist after every step) must be all-reduced before the next."""
+        self._dp_pivot.copy_(self.obs_mean)  # replicated across ranks
+        done = ctypes.c_int(0)
+        step = 0
+        first = 0 if self._have_minmax else 1
+        while True:
+            call("sppReplayObsStatsDP", self._h, step, ptr(self._dp_pivot), ptr(self._dp_sums), ptr(self._dp_hist),
+                 n_global, ptr(self.obs_mean), ptr(self.obs_std), ptr(self.max_obs), ptr(self.min_obs), first,
+                 ctypes.byref(done), stream_handle())
+            if done.value:
+                break
+            yield step
+            step += 1
+        self._have_minmax = True
+
     def normalize(self, obs, force=False):
         if not (self.obs_norm or force):
             return obs

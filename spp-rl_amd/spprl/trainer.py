@@ -39,7 +39,7 @@ import torch
 
 from . import config
 from ._lib import call, ptr, stream_handle
-from .dp import make_allreduce
+from .dp import make_allreduce, make_allreduce_sum
 
 # ---------------------------------------------------------------- stats
 
@@ -254,6 +254,7 @@ class OffPolicyLoop:
         if self.schedule not in ("reference", "fused"):
             raise ValueError("schedule must be 'reference' or 'fused'")
         self.allreduce = allreduce if allreduce is not None else make_allreduce()
+        self.allreduce_sum = make_allreduce_sum() if self.allreduce is not None else None
         self.loop_seed = int(loop_seed)
         self._ctr = 0
         E = self.n_envs
@@ -315,9 +316,21 @@ class OffPolicyLoop:
         Returns the mean return of the episodes completed in this iteration (None if none)."""
         self._ret_sums.zero_()
         self.collect_batch_and_train(self.batch_size)
-        self.replay_buffer.update_obs_mean_std()
+        self.update_obs_stats()
         s = self._ret_sums.cpu().numpy()
         return float(s[0] / s[1]) if s[1] > 0 else None
+
+    def update_obs_stats(self):
+        """update_obs_mean_std (rl.py:93-112); global over the ranks' shards under DP."""
+        if self.allreduce_sum is not None:
+            # every rank runs the same cadence over the same number of envs, so the shards
+            # hold equally many rows: no host sync to learn the global count
+            import torch.distributed as dist
+
+            n_global = len(self.replay_buffer) * dist.get_world_size()
+            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, n_global)
+        else:
+            self.replay_buffer.update_obs_mean_std()
 
     def _start_episodes(self):
         obs = self.env.reset()
@@ -497,7 +510,7 @@ class OffPolicyLoop:
     def pre_train(self):
         self.collect_samples()
         self.update_acm(epochs=self.acm_pre_train_epochs, pretrain=True)
-        self.replay_buffer.update_obs_mean_std()
+        self.update_obs_stats()
         if not self.acm_keep_pretrain:
             self.replay_buffer.reset_idx()
 

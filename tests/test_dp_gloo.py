@@ -137,3 +137,43 @@ def test_make_allreduce_single_process_is_none():
     assert shard_batch(409600, 8) == 51200
     with pytest.raises(ValueError):
         shard_batch(100, 3)
+
+
+def _stats_worker(rank, port, shards, pivot, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=len(shards))
+    from oracle.replay import dp_obs_stats
+
+    def allreduce_sum(a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    q.put((rank, dp_obs_stats(shards[rank], allreduce_sum, pivot)))
+    dist.destroy_process_group()
+
+
+def test_dp_obs_stats_protocol_gloo():
+    """update_obs_mean_std over W=2 shards via all-reduced fp64 sums and radix-select
+    histograms (the sppReplayObsStatsDP protocol, oracle form) equals numpy over the union."""
+    rng = np.random.RandomState(4)
+    shards = [(rng.standard_t(3, size=(n, 11)) * 2 + 1).astype(np.float32) for n in (3001, 4217)]
+    pivot = rng.randn(11).astype(np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, port, shards, pivot, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    allx = np.concatenate(shards).astype(np.float64)
+    for r in range(2):
+        mean, std, p99, p1 = res[r]
+        np.testing.assert_array_equal(p99, np.percentile(allx, 99, axis=0).astype(np.float32))
+        np.testing.assert_array_equal(p1, np.percentile(allx, 1, axis=0).astype(np.float32))
+        np.testing.assert_allclose(mean, allx.mean(0).astype(np.float32), rtol=1e-6)
+        np.testing.assert_allclose(std, allx.std(0).astype(np.float32), rtol=1e-6)
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)

@@ -313,3 +313,58 @@ def test_synth_env_step_matches_numpy():
     ref = np.tanh(s.astype(np.float64) @ A.T.astype(np.float64)) + 0.1 * np.resize(a, (E, ac))[:, np.arange(ob) % ac]
     np.testing.assert_allclose(ns.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(r.cpu().numpy(), -np.square(a).sum(1) + ref[:, 0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("ob,ranks", [(11, 2), (17, 3), (111, 2)])
+def test_obs_stats_data_parallel_protocol_matches_union(ob, ranks):
+    """sppReplayObsStatsDP over W shards, all-reduced in lockstep here on one GPU, equals the
+    single-buffer statistics of the union of the shards (percentiles, max/min bit-exact;
+    mean / std rtol 1e-6, the fp64 sums differ only in summation order / pivot)."""
+    rng = np.random.RandomState(ob)
+    sizes = [5000 + 997 * r for r in range(ranks)]
+    data = [(rng.standard_t(3, size=(n, ob)) * rng.uniform(0.5, 3, ob) + rng.randn(ob)).astype(np.float32)
+            for n in sizes]
+
+    def buf(rows):
+        rb = spprl.BufferAcMOffPolicy(len(rows) + 8, ob, ob, 2, device=DEV, min_max_denormalize=True)
+        sl = rb.add_obs_batch(torch.from_numpy(np.concatenate([rows, rows[:1]])))
+        n = len(rows)
+        z = np.zeros(n, bool)
+        rb.add_timestep_batch(sl[:n], sl[1:], torch.zeros(n, ob), np.zeros(n, np.float32), z, z,
+                              torch.zeros(n, 2))
+        return rb
+
+    shards = [buf(d) for d in data]
+    union = buf(np.concatenate(data))
+    union.update_obs_mean_std()
+    for rb in shards:
+        rb.obs_mean.copy_(torch.from_numpy(rng.randn(ob).astype(np.float32)))  # any replicated pivot works
+        rb._dp_hist = torch.zeros(_lib.load().sppReplayObsStatsDPHistSize(rb._h), dtype=torch.int32, device=DEV)
+        rb._dp_sums = torch.zeros(ob, 2, dtype=torch.float64, device=DEV)
+        rb._dp_pivot = torch.zeros(ob, device=DEV)
+    pivot = shards[0].obs_mean.clone()
+    for rb in shards:
+        rb.obs_mean.copy_(pivot)
+    n_global = sum(sizes)
+    gens = [rb.obs_stats_dp_steps(n_global) for rb in shards]
+    while True:
+        steps = [next(g, None) for g in gens]
+        if steps[0] is None:
+            assert all(s is None for s in steps)
+            break
+        if steps[0] == 0:
+            tot = sum(rb._dp_sums for rb in shards)
+            for rb in shards:
+                rb._dp_sums.copy_(tot)
+        tot = sum(rb._dp_hist for rb in shards)
+        for rb in shards:
+            rb._dp_hist.copy_(tot)
+    torch.cuda.synchronize()
+    for rb in shards:
+        np.testing.assert_array_equal(rb.max_obs.cpu().numpy(), union.max_obs.cpu().numpy())
+        np.testing.assert_array_equal(rb.min_obs.cpu().numpy(), union.min_obs.cpu().numpy())
+        np.testing.assert_allclose(rb.obs_mean.cpu().numpy(), union.obs_mean.cpu().numpy(), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(rb.obs_std.cpu().numpy(), union.obs_std.cpu().numpy(), rtol=1e-6)
+    allx = np.concatenate(data).astype(np.float64)
+    np.testing.assert_array_equal(union.max_obs.cpu().numpy(), np.percentile(allx, 99, axis=0).astype(np.float32))
+    np.testing.assert_array_equal(union.min_obs.cpu().numpy(), np.percentile(allx, 1, axis=0).astype(np.float32))

@@ -236,6 +236,7 @@ sppStatus sppAgentGetTiming(sppAgentHandle h, double* ms_out /*[5]*/, int64_t* c
  *   mode 0 random : a = lim * eps                      (initial_act)
  *   mode 1 noisy  : a = clip(tanh(mu + sigma*eps)*lim + act_noise*lim*noise, +-1.1 lim)
  *   mode 2 det    : a = clip(tanh(mu)*lim, +-1.1 lim)
+ *   mode 3 given  : a = eps (the caller's action; on-policy process_action, acm/on_policy.py:32-50)
  * then a_d = denormalize(a) if denormalize_actor_out, env action = ACM(cat(obs, a_d)).
  * target_state_out receives a_d (what the buffer stores as `action`). */
 sppStatus sppPolicyAct(sppAgentHandle h, const float* obs /*[E][ob]*/, int E, const float* eps /*[E][aout]*/,
@@ -259,6 +260,11 @@ sppStatus sppEpisodeAccum(const float* rew, const uint8_t* end, int E, float* ep
 /* SynthEnv.reset for the rows with mask[e] != 0 (all rows when mask is NULL). */
 sppStatus sppSynthEnvReset(float* obs /*[E][ob]*/, const uint8_t* mask, int E, int ob, uint64_t seed,
                            uint64_t offset, void* stream);
+
+/* MemoryMeta.normalize (inverse = 0) / denormalize (inverse = 1), rltoolkit/buffer/memory.py:76-127,
+ * elementwise over x[rows][ob]; min_max selects (lo, hi) else (mean, std). out may alias x. */
+sppStatus sppObsNormalize(const float* x, int64_t rows, int ob, const float* lo, const float* hi, const float* mean,
+                          const float* std, int min_max, int inverse, float* out, void* stream);
 
 /* ------------------------------------------------------------------ PPO path
  * PPO.calculate_q_val + calculate_gae (rltoolkit/algorithms/a2c/a2c.py:247-265,

@@ -495,6 +495,18 @@ sppStatus sppSynthEnvReset(float* obs, const uint8_t* mask, int E, int ob, uint6
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
+
+sppStatus sppObsNormalize(const float* x, int64_t rows, int ob, const float* lo, const float* hi, const float* mean,
+                          const float* std, int min_max, int inverse, float* out, void* stream) {
+  SPP_REQUIRE(x && out && rows >= 0 && ob > 0, SPP_E_INVALID_ARG, "normalize: bad args");
+  SPP_REQUIRE(min_max ? (lo && hi) : (mean && std), SPP_E_INVALID_ARG, "normalize: missing statistics");
+  if (rows == 0) return SPP_OK;
+  const int64_t n = rows * ob;
+  hipLaunchKernelGGL(k_obs_normalize, dim3(cdiv(n, 256)), dim3(256), 0, S(stream), x, n, ob, lo, hi, mean, std,
+                     min_max, inverse, out);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
 }  // extern "C"
 
 // ================================================================== agent
@@ -1528,8 +1540,9 @@ sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx, int B, float
 sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* eps, const float* noise,
                        float act_noise, int mode, int denorm_out, float* target_out, float* env_out, void* stream) {
   SPP_REQUIRE(a && obs && E > 0 && target_out && env_out, SPP_E_INVALID_ARG, "policy_act: bad args");
-  SPP_REQUIRE(mode >= 0 && mode <= 2, SPP_E_INVALID_ARG, "mode");
-  SPP_REQUIRE(mode != 0 || eps, SPP_E_INVALID_ARG, "random mode needs eps");
+  SPP_REQUIRE(mode >= 0 && mode <= 3, SPP_E_INVALID_ARG, "mode");
+  SPP_REQUIRE((mode != 0 && mode != 3) || eps, SPP_E_INVALID_ARG, "modes 0 / 3 need eps");
+  SPP_REQUIRE(mode != 3 || !a->ddpg, SPP_E_INVALID_ARG, "mode 3 (caller action) is a SAC_AcM-handle (AcM) mode");
   hipStream_t st = S(stream);
   sppStatus s = check_ready(a);
   if (s) return s;

@@ -511,4 +511,27 @@ __global__ void k_synth_reset(float* obs, const uint8_t* mask, int E, int ob, ui
   obs[i] = a;
 }
 
+
+// MemoryMeta.normalize / denormalize (rltoolkit/buffer/memory.py:76-127) elementwise
+// over [rows][ob], the same fp32 operation order as the fused device helpers:
+//   min-max : (x - mid) / (hi - mid + 1e-8)     |  mid + x * (hi - lo) / 2
+//   z-score : clamp((x - mean) / (std + 1e-8), -10, 10)  |  (std + 1e-8) * x + mean
+__global__ void k_obs_normalize(const float* __restrict__ x, int64_t n, int ob, const float* lo, const float* hi,
+                                const float* mean, const float* std, int min_max, int inverse, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int j = (int)(i % ob);
+  const float v = x[i];
+  float r;
+  if (min_max) {
+    const float l = lo[j], h = hi[j];
+    const float mid = fadd_rn(h, l) * 0.5f;
+    r = inverse ? fadd_rn(mid, fmul_rn(v, fsub_rn(h, l) * 0.5f)) : fdiv_rn(fsub_rn(v, mid), fadd_rn(fsub_rn(h, mid), 1e-8f));
+  } else {
+    r = inverse ? fadd_rn(fmul_rn(fadd_rn(std[j], 1e-8f), v), mean[j])
+                : fminf(fmaxf(fdiv_rn(fsub_rn(v, mean[j]), fadd_rn(std[j], 1e-8f)), -10.f), 10.f);
+  }
+  out[i] = r;
+}
+
 }  // namespace spp

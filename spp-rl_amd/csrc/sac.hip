@@ -664,12 +664,13 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
     const int er = valid ? e : 0;
     // row-major obs: element (unit u, env e) = obs[e*OB + u] -> ld = 1, offset 4h + e*OB
     Lane L = make_lane(big, small, tbl, 1, er * C::OB);
-    if (a.mode != 0) {
+    const bool use_actor = a.mode == 1 || a.mode == 2;
+    if (use_actor) {
       uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
       actor_trunk<C, false>(p.actor, a.obs, a.E * C::OB * 4, L, nullptr, nullptr, d0, d1, d2, d3);
     }
     f32x16 hd[C::NB_PAIR];
-    if (a.mode != 0) load_pair<C>(hd, big);
+    if (use_actor) load_pair<C>(hd, big);
     const int h8 = 8 * L.h;
 #pragma unroll
     for (int ib = 0; ib < C::NB_PAIR; ++ib)
@@ -682,6 +683,8 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
           float act;
           if (a.mode == 0) {
             act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;  // off_policy.py:50-54
+          } else if (a.mode == 3) {
+            act = valid ? a.eps[er * C::AOUT + j] : 0.f;  // caller's action (on-policy process_action)
           } else {
             const float mu = hd[ib][r];
             float u = mu;

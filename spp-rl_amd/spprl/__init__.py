@@ -9,5 +9,7 @@ from ._lib import SppError, load  # noqa: F401
 from .replay import BufferAcMOffPolicy  # noqa: F401
 from .sac_acm import SAC_AcM  # noqa: F401
 from .ddpg_acm import DDPG_AcM  # noqa: F401
+from .ppo_acm import PPO_AcM  # noqa: F401
+from .trainer import HostVecEnv, SynthVecEnv  # noqa: F401
 
-__all__ = ["SAC_AcM", "DDPG_AcM", "BufferAcMOffPolicy", "SppError", "load"]
+__all__ = ["SAC_AcM", "DDPG_AcM", "PPO_AcM", "SynthVecEnv", "HostVecEnv", "BufferAcMOffPolicy", "SppError", "load"]

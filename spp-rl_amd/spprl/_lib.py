@@ -125,6 +125,8 @@ _SIGS = {
     "sppReplayObsStatsDPHistSize": (c_int, [c_void_p]),
     "sppReplayObsStatsDP": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, P(c_int), c_void_p]),
+    "sppObsNormalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                c_void_p, c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

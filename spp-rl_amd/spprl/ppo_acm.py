@@ -1,0 +1,271 @@
+"""PPO_AcM: rltoolkit's SPP-PPO loop on the MI355X library, vectorized over E envs.
+
+Mirrors rltoolkit/acm/on_policy.py (AcMOnPolicyTrainer / A2C_AcM / PPO_AcM) with
+A2C (algorithms/a2c/a2c.py) and PPO (algorithms/ppo/ppo.py) underneath:
+
+  collect_batch         a2c.py:144-184 + on_policy.py:32-50 (process_action: denormalise ->
+                        AcM -> env), SURVEY.md §8a row a21
+  update_critic         a2c.py:186-225 (critic_num_target_updates x num_critic_updates_per_target
+                        full-batch steps), row a22
+  calculate_gae         ppo.py:117-150 (device scan over [T][E] streams), row a23
+  update_actor_acm      on_policy.py:164-216 + advantage_dataset.py:30-42 (clip loss, entropy,
+                        custom dist loss on the buffer's (denormalised) actions, KL early stop), row a24
+  update_acm(_batches)  acm.py:266-303, 356-372 every acm_update_freq iterations
+  update_obs_mean_std   on the ACM ring when denormalize_actor_out (on_policy.py:70-71)
+  pre_train             acm.py:234-244
+
+Device pieces: actor / critic = ``OnPolicyNets`` (libspprl sppOnp*), GAE = sppGaeScan, the AcM
+(64-32 tanh, basic_model.py:108-132) and its replay ring = the AcM half of an SPP agent handle
+(sppPolicyAct mode 3 for the act, sppAcmRegress* for the regression, BufferAcMOffPolicy for the
+ring).  Rollout memory is time-major [T][E] on device.
+
+Vectorization: each iteration collects T = ceil(batch_size / E) steps of E lockstep envs
+(N = T*E transitions); envs keep running across iterations and the last step of every
+iteration is a truncation (end = 1, done = 0), so GAE bootstraps from V(s') there exactly as
+the reference does at a time-limit end.  With E = 1 whole episodes are collected until
+batch_size frames, as the reference does.
+"""
+import numpy as np
+import torch
+
+from . import config
+from ._lib import call, ptr, stream_handle
+from .onpolicy import OnPolicyNets
+from .ppo import calculate_gae
+from .sac_acm import SAC_AcM
+from .trainer import StatsLogger, SynthVecEnv
+
+
+class PPO_AcM:
+    def __init__(self, env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=2000,
+                 ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0, ppo_epsilon=0.2,
+                 gae_lambda=0.95, critic_num_target_updates=10, num_critic_updates_per_target=10, normalize_adv=True,
+                 custom_loss=0.1, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                 acm_epochs=5, acm_batch_size=64, acm_update_freq=3, acm_lr=3e-4, acm_update_batches=None,
+                 acm_pre_train_samples=100_000, acm_pre_train_epochs=5, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
+                 acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, iterations=1001,
+                 stats_freq=1, test_episodes=None, return_done=None, max_frames=None, n_envs=1, env=None,
+                 env_spec=None, device="cuda", seed=None, loop_seed=0, **unused):
+        ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
+        self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
+        self.device = torch.device(device)
+        self.gamma, self.gae_lambda = gamma, gae_lambda
+        self.batch_size, self.iterations, self.stats_freq = int(batch_size), int(iterations), int(stats_freq)
+        self.test_episodes, self.return_done, self.max_frames = test_episodes, return_done, max_frames
+        self.custom_loss, self.norm_closs = float(custom_loss), bool(norm_closs)
+        self.min_max_denormalize, self.denormalize_actor_out = bool(min_max_denormalize), bool(denormalize_actor_out)
+        self.acm_epochs, self.acm_update_freq, self.acm_update_batches = int(acm_epochs), acm_update_freq, \
+            acm_update_batches
+        self.actor_output_dim = ob
+        lim = 1.0 if self.min_max_denormalize else float(config.MAX_ABS_OBS_VALUE)  # acm.py:102-108
+        if env is None:
+            env = SynthVecEnv(n_envs, ob, ac, max_episode_steps=max_ep, ac_high=ac_high, seed=loop_seed,
+                              device=self.device)
+        self.env = env
+        self.n_envs = E = env.n
+        self.T = 1 if E == 1 else max(1, -(-self.batch_size // E))
+        Nmax = max(self.T * E, self.batch_size + (max_ep or 1000) if E == 1 else 0)
+        self.nets = OnPolicyNets(ob, ob, ac_lim=lim, actor_lr=actor_lr, critic_lr=critic_lr, ppo_epsilon=ppo_epsilon,
+                                 entropy_coef=entropy_coef, gamma=gamma, gae_lambda=gae_lambda,
+                                 critic_num_target_updates=critic_num_target_updates,
+                                 num_critic_updates_per_target=num_critic_updates_per_target,
+                                 max_ppo_epochs=max_ppo_epochs, ppo_batch_size=ppo_batch_size,
+                                 kl_div_threshold=kl_div_threshold, normalize_adv=normalize_adv,
+                                 max_batch=max(Nmax, ppo_batch_size), device=self.device, seed=seed)
+        # the AcM and its replay ring (acm.py:127-141: size = pre-train samples * 1.1)
+        ring = int(acm_pre_train_samples * 1.1)
+        self.acm = SAC_AcM(env_name=env_name, env_spec=(ob, ac, ac_high, max_ep), acm_lr=acm_lr, buffer_size=ring,
+                           max_batch=max(acm_batch_size, 64), min_max_denormalize=min_max_denormalize,
+                           denormalize_actor_out=denormalize_actor_out, device=self.device, seed=seed, env=env,
+                           acm_epochs=acm_epochs, acm_batch_size=acm_batch_size, acm_update_freq=1,
+                           acm_update_batches=acm_update_batches, acm_pre_train_samples=acm_pre_train_samples,
+                           acm_pre_train_epochs=acm_pre_train_epochs, acm_scheduler_step=acm_scheduler_step,
+                           acm_scheduler_gamma=acm_scheduler_gamma, acm_keep_pretrain=acm_keep_pretrain,
+                           loop_seed=loop_seed + 17)
+        self.replay_buffer = self.acm.replay_buffer
+        self.stats_logger = StatsLogger()
+        self.iteration = 0
+        self.loop_seed, self._ctr = int(loop_seed), 0
+        self.loss = {}
+        d = self.device
+        self._ep_ret = torch.zeros(E, device=d)
+        self._ret_sums = torch.zeros(2, dtype=torch.float64, device=d)
+        self._obs = None
+        self._prev_slots = None
+
+    # ---------------------------------------------------------------- helpers
+    def _randn(self, t):
+        self._ctr += 1
+        call("sppRandNormal", ptr(t), t.numel(), self.loop_seed, self._ctr, stream_handle())
+        return t
+
+    def normalize(self, x):
+        """MemoryAcM.normalize with the ring's statistics (memory.py:76-88)."""
+        rb = self.replay_buffer
+        if self.min_max_denormalize and not rb._have_minmax:
+            return x
+        return rb._norm(x, 0)
+
+    def denormalize(self, x):
+        return self.replay_buffer._norm(x, 1)
+
+    def process_action(self, action, norm_obs):
+        """on_policy.py:32-50: denormalise (if denormalize_actor_out) -> AcM(cat(obs, a)) -> env action."""
+        _, env_act = self.acm.act(norm_obs, eps=action, mode=3)
+        return env_act
+
+    # ---------------------------------------------------------------- RL.train / perform_iteration
+    def pre_train(self):
+        self.acm.pre_train()
+        self._obs = None
+
+    def train(self, iterations=None):
+        if iterations:
+            self.iterations += iterations
+        while self.iteration < self.iterations:
+            ret = self.perform_iteration()
+            running = self.stats_logger.calc_running_return(ret)
+            if self.return_done is not None and running is not None and running >= self.return_done:
+                break
+            if self.test_episodes and self.iteration % self.stats_freq == 0:
+                self.stats_logger.test_return = self.test()
+            self.iteration += 1
+            if self.max_frames is not None and self.max_frames < self.stats_logger.frames:
+                break
+        return self.stats_logger.running_return
+
+    def perform_iteration(self, sync=True):
+        """on_policy.py:52-75.  Returns the mean return of the episodes completed (None if none)."""
+        self._ret_sums.zero_()
+        mem = self.collect_batch()
+        self.update(mem)
+        if self.acm_update_freq and self.iteration % self.acm_update_freq == 0:
+            if self.acm_update_batches:
+                self.acm.update_acm_batches(self.acm_update_batches)
+            else:
+                self.acm.update_acm(self.acm_epochs)
+        if self.denormalize_actor_out:
+            self.acm.update_obs_stats()
+        if not sync:
+            return None
+        s = self._ret_sums.cpu().numpy()
+        return float(s[0] / s[1]) if s[1] > 0 else None
+
+    # ---------------------------------------------------------------- A2C.collect_batch
+    def _start(self):
+        self._obs = self.env.reset()
+        self._prev_slots = self.replay_buffer.add_obs_batch(self._obs)
+        self._ep_ret.zero_()
+        self._ep_len = np.zeros(self.n_envs, np.int64)
+
+    def collect_batch(self):
+        """Rollout memory, time-major [T][E]: normalised obs, actions, log-probs, rewards, done,
+        end, next obs (raw)."""
+        E = self.n_envs
+        if E == 1:  # whole episodes until batch_size frames (a2c.py:155-184)
+            steps = []
+            while sum(len(s) for s in steps) < self.batch_size:
+                self.stats_logger.rollouts += 1
+                self._start()
+                seg, end = [], False
+                while not end:
+                    step = self._step()
+                    end = bool(step[-1])
+                    seg.append(step[:-1])
+                steps.append(seg)
+            flat = [x for s in steps for x in s]
+        else:
+            if self._obs is None:
+                self._start()
+                self.stats_logger.rollouts += E
+            flat = [self._step()[:-1] for _ in range(self.T)]
+        T = len(flat)
+        cat = lambda k: torch.stack([f[k] for f in flat])  # noqa: E731
+        mem = {"obs": cat(0), "act": cat(1), "lp": cat(2), "rew": cat(3), "done": cat(4), "end": cat(5),
+               "next_obs": cat(6), "T": T}
+        if E > 1:
+            mem["end"][-1].fill_(1)  # segment truncation: GAE bootstraps from V(s') (ppo.py:136-148)
+        self.stats_logger.frames += T * E
+        return mem
+
+    def _step(self):
+        E, rb = self.n_envs, self.replay_buffer
+        norm_obs = self.normalize(self._obs)
+        eps = self._randn(torch.empty(E, self.actor_output_dim, device=self.device))
+        act, lp = self.nets.act(norm_obs, eps)
+        env_act = self.process_action(act, norm_obs)
+        nobs, rew, end, end_dev = self.env.step(env_act)
+        # a2c.py:168-171: end = env done; done = False when the episode hit max_ep_len (a time-limit end)
+        self._ep_len += 1
+        max_ep = getattr(self.env, "_max_episode_steps", None)
+        done_h = end & (self._ep_len != max_ep) if max_ep else end.copy()
+        self._ep_len[end] = 0
+        done = (torch.from_numpy(done_h.astype(np.uint8)).to(self.device) if done_h.any()
+                else torch.zeros(E, dtype=torch.uint8, device=self.device))
+        any_end = bool(end.any())
+        call("sppEpisodeAccum", ptr(rew), ptr(end_dev) if any_end else None, E, ptr(self._ep_ret),
+             ptr(self._ret_sums), stream_handle())
+        slots = rb.add_obs_batch(nobs)
+        rb.add_timestep_batch(self._prev_slots, slots, nobs, rew, done, end_dev, env_act)  # ReplayBufferAcM ring
+        self._prev_slots = slots
+        out = (norm_obs, act, lp, rew.clone(), done, end_dev.clone(), nobs.clone(), end.any() if E == 1 else False)
+        self._obs = nobs
+        if any_end and E > 1:
+            self.stats_logger.rollouts += int(end.sum())
+            self._obs = self.env.reset(end)
+            rs = rb.add_obs_batch(self._obs[torch.as_tensor(np.flatnonzero(end), device=self.device)])
+            self._prev_slots = self._prev_slots.copy()
+            self._prev_slots[np.flatnonzero(end)] = rs
+        return out
+
+    # ---------------------------------------------------------------- update (critic, GAE, actor)
+    def update(self, mem):
+        T, E, ob = mem["T"], self.n_envs, self.ob_dim
+        N = T * E
+        obs = mem["obs"].reshape(N, ob)
+        nobs = self.normalize(mem["next_obs"].reshape(N, ob))
+        rew, done = mem["rew"].reshape(N), mem["done"].reshape(N).float()
+        self.nets.update_critic(obs, nobs, rew, done)  # a2c.py:186-225
+        v = self.nets.value(obs).reshape(T, E)
+        v_next = self.nets.value(nobs).reshape(T, E)
+        _, adv = calculate_gae(mem["rew"].reshape(T, E), v, v_next, mem["done"].reshape(T, E),
+                               mem["end"].reshape(T, E), self.gamma, self.gae_lambda)
+        acts = mem["act"].reshape(N, ob)
+        nxt = nobs
+        if not self.norm_closs:  # on_policy.py:191-193
+            nxt, acts = self.denormalize(nobs), self.denormalize(acts)
+        self.nets.update_actor(adv.reshape(N), obs, acts, mem["lp"].reshape(N), nxt)
+        self.loss.update(self.nets.loss)
+        self.loss["acm"] = None
+
+    # ---------------------------------------------------------------- test (a2c.py test)
+    def test(self, episodes=None):
+        episodes = episodes or self.test_episodes or 1
+        env = self.env.spawn(episodes, seed=self.loop_seed + 99991)
+        obs = env.reset()
+        ret = torch.zeros(episodes, device=self.device)
+        sums = torch.zeros(2, dtype=torch.float64, device=self.device)
+        alive = np.ones(episodes, bool)
+        while alive.any():
+            n_obs = self.normalize(obs)
+            act, _ = self.nets.act(n_obs, None)  # deterministic mean
+            obs, rew, end, _ = env.step(self.process_action(act, n_obs))
+            m = torch.as_tensor((end & alive).astype(np.uint8), device=self.device)
+            call("sppEpisodeAccum", ptr(rew), ptr(m), episodes, ptr(ret), ptr(sums), stream_handle())
+            alive &= ~end
+            if end.any() and alive.any():
+                obs = env.reset(end)
+        s = sums.cpu().numpy()
+        return float(s[0] / s[1])
+
+    # ---------------------------------------------------------------- checkpoints (rl.py:263-301)
+    def collect_params_dict(self):
+        from .onpolicy import actor_layout, critic_layout
+        from . import nets as _nets
+
+        rb = self.replay_buffer
+        return {"actor": _nets.state_dict(self.nets.params[0], actor_layout(self.ob_dim, self.ob_dim)),
+                "critic": _nets.state_dict(self.nets.params[1], critic_layout(self.ob_dim)),
+                "acm": self.acm.net_state(5), "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
+                "min_obs": rb.min_obs.cpu() if rb._have_minmax else None,
+                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None}

@@ -182,17 +182,21 @@ class BufferAcMOffPolicy:
         self._have_minmax = True
 
     def normalize(self, obs, force=False):
+        """BufferAcMOffPolicy.normalize (replay_buffer.py:77-81) -> MemoryMeta.normalize (memory.py:76-88)."""
         if not (self.obs_norm or force):
             return obs
-        if self.min_max_denormalize:
-            if not self._have_minmax:
-                return obs
-            mean = (self.max_obs + self.min_obs) / 2
-            return (obs - mean) / (self.max_obs - mean + 1e-8)
-        return torch.clamp((obs - self.obs_mean) / (self.obs_std + 1e-8), -10, 10)
+        if self.min_max_denormalize and not self._have_minmax:
+            return obs
+        return self._norm(obs, 0)
 
     def denormalize(self, obs):
-        if self.min_max_denormalize:
-            mean = (self.max_obs + self.min_obs) / 2
-            return mean + obs * ((self.max_obs - self.min_obs) / 2)
-        return (self.obs_std + 1e-8) * obs + self.obs_mean
+        """MemoryMeta.denormalize (memory.py:90-127)."""
+        return self._norm(obs, 1)
+
+    def _norm(self, obs, inverse):
+        x = self._dev(obs)
+        out = torch.empty_like(x)
+        call("sppObsNormalize", ptr(x), x.numel() // self.obs_shape, self.obs_shape, ptr(self.min_obs),
+             ptr(self.max_obs), ptr(self.obs_mean), ptr(self.obs_std), int(self.min_max_denormalize), int(inverse),
+             ptr(out), stream_handle())
+        return out

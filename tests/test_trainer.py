@@ -214,3 +214,61 @@ def test_host_env_pool_pipelined_loop():
     for v in ag.loss.values():
         assert np.isfinite(v)
     assert np.isfinite(ag.stats_logger.test_return)
+
+
+@pytest.mark.gpu
+def test_ppo_acm_vectorized_loop_runs():
+    import spprl
+
+    ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", n_envs=64, batch_size=1024, iterations=3, ppo_batch_size=256,
+                       acm_pre_train_samples=2000, acm_pre_train_epochs=1, acm_update_freq=2, acm_epochs=1,
+                       acm_batch_size=64, custom_loss=0.1, device="cuda:0", seed=0, test_episodes=2,
+                       env_spec=(17, 6, 1.0, 40))
+    ag.pre_train()
+    ag.train()
+    torch.cuda.synchronize()
+    assert ag.T == 16 and ag.stats_logger.frames == 3 * 1024
+    assert np.isfinite(ag.loss["critic"]) and np.isfinite(ag.loss["actor"]) and np.isfinite(ag.loss["kl"])
+    assert ag.stats_logger.running_return is not None
+    assert np.isfinite(ag.stats_logger.test_return)
+
+
+@pytest.mark.gpu
+def test_ppo_acm_single_env_collects_whole_episodes():
+    import spprl
+
+    ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", n_envs=1, batch_size=100, iterations=1, ppo_batch_size=64,
+                       acm_pre_train_samples=300, acm_pre_train_epochs=1, acm_update_freq=1, acm_epochs=1,
+                       device="cuda:0", seed=0, env_spec=(17, 6, 1.0, 60))
+    ag.pre_train()
+    mem = ag.collect_batch()
+    assert mem["T"] == 120  # two 60-step episodes (a2c.py:155-184 finishes the episode in progress)
+    assert int(mem["end"].sum()) == 2 and int(mem["done"].sum()) == 0  # time-limit ends are not terminal
+    ag.update(mem)
+    torch.cuda.synchronize()
+    assert np.isfinite(ag.loss["critic"])
+
+
+@pytest.mark.gpu
+def test_acm_act_given_action_matches_oracle():
+    """sppPolicyAct mode 3 (on-policy process_action): env action = AcM(cat(obs, denorm(a)))."""
+    import spprl
+    from oracle import nets as onets
+
+    ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", min_max_denormalize=True, denormalize_actor_out=True,
+                       max_batch=256, buffer_size=64, device="cuda:0", seed=3)
+    rb = ag.replay_buffer
+    rng = np.random.RandomState(0)
+    lo, hi = -rng.uniform(0.5, 2, 17).astype(np.float32), rng.uniform(0.5, 2, 17).astype(np.float32)
+    rb.min_obs.copy_(torch.from_numpy(lo))
+    rb.max_obs.copy_(torch.from_numpy(hi))
+    rb._have_minmax = True
+    E = 77
+    obs = torch.from_numpy(rng.randn(E, 17).astype(np.float32))
+    a = torch.from_numpy(rng.uniform(-1.2, 1.2, (E, 17)).astype(np.float32))
+    tgt, env = ag.act(obs.cuda(), eps=a.cuda(), mode=3)
+    P = {n: torch.as_tensor(v) for n, v in ag.net_state(5).items()}
+    ad = torch.from_numpy(lo + (hi - lo) / 2) * 0 + (torch.from_numpy((hi + lo) / 2) + a * torch.from_numpy((hi - lo) / 2))
+    ref = onets.acm(P, torch.cat([obs, ad], 1), ag.ac_lim)
+    np.testing.assert_allclose(tgt.cpu().numpy(), ad.numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(env.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)

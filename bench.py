@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="sac_hopper", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="sac_hopper", choices=sorted(CONFIGS) + ["ppo_hcheetah"])
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -176,6 +176,73 @@ def cpu_baseline(cfg, seconds):
                       "torch-CPU restatement, 1 thread; %.1f s" % (n, cfg["env"], time.perf_counter() - start)}
 
 
+def bench_ppo(args, world, rank, dev):
+    """configs[3]: SPP-PPO HalfCheetah-v2, 16384 envs over 8 GPUs = 2048 per GPU (train/spp_ppo_hcheetah.py
+    hyper-parameters).  One step = one PPO_AcM iteration: T = 16 vector steps of rollout (actor sample,
+    AcM, env, ACM ring writes), 10 x 10 full-batch critic steps, GAE over [T][E], <= 10 clip-loss epochs of
+    512-sample minibatches with the KL stop, the ACM regression (5 epochs of 64-sample batches over the
+    1.1e5 ring every 3 iterations), ring obs statistics."""
+    import spprl
+    from spprl.dp import shard_seed
+
+    E = args.envs or 2048
+    T = 16
+    seed = shard_seed(1000, rank)
+    ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=T * E,
+                       ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
+                       custom_loss=0.1, norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True,
+                       acm_epochs=5, acm_batch_size=64, acm_update_freq=3, acm_lr=3e-4,
+                       acm_pre_train_samples=100_000, n_envs=E, device=dev, seed=0, loop_seed=seed)
+    rb = ag.replay_buffer
+    ob, ac = ag.ob_dim, ag.ac_dim
+    torch.manual_seed(seed)
+    fill = rb.size - 2 * E  # the ACM ring after pre-training (random env actions)
+    prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
+    slots = rb.add_obs_batch(torch.randn(fill, ob, device=dev))
+    prevs = np.concatenate([prev[-1:], slots[:-1]])
+    z = torch.zeros(fill, dtype=torch.uint8, device=dev)
+    rb.add_timestep_batch(prevs, slots, torch.randn(fill, ob, device=dev), torch.randn(fill, device=dev), z, z,
+                          torch.rand(fill, ac, device=dev) * 2 - 1)
+    ag.acm.update_obs_stats()
+    ag.iteration = 1
+
+    def iteration():
+        ag.perform_iteration(sync=False)
+        ag.iteration += 1  # ACM update every acm_update_freq iterations (on_policy.py:66-70)
+
+    for _ in range(args.warmup):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed = float(tmax.item())
+    value = world * T * E * args.steps / elapsed
+    res = {"metric": "env-steps/sec (rollout+update) SPP-PPO HalfCheetah-v2", "value": round(value, 1),
+           "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic: SynthEnv linear-tanh dynamics (HalfCheetah-v2 shapes ob=17, ac=6), random-init "
+                   "networks, ACM ring pre-filled with N(0,1) transitions",
+           "config": {"workload": "SPP-PPO HalfCheetah-v2, %d vectorized envs per GPU x %d steps per iteration "
+                                  "(BASELINE.json configs[3] per-GPU shape)" % (E, T), "envs_per_gpu": E,
+                      "steps_per_iteration": T, "acm_ring": rb.size, "parallelism": "dp%d" % world},
+           "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,6 +254,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    if args.config == "ppo_hcheetah":
+        return bench_ppo(args, world, rank, dev)
     import spprl
     from spprl import flops
     from spprl.dp import shard_seed

@@ -289,6 +289,12 @@ sppStatus sppPpoClipLoss(const float* lp_old, const float* lp_new, const float* 
 /* AdvantageDataset normalisation (algorithms/ppo/advantage_dataset.py:8-12):
  * out = (adv - mean) / (std(ddof=1) + 1.2e-7).  out may alias adv. */
 sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream);
+/* Data-parallel form: sppAdvSums writes the local fp64 {sum, sum of squares};
+ * the caller all-reduces them (and n) and sppAdvNormalizeGlobal normalises the local shard with
+ * the global moments (std ddof = 1, + 1.2e-7). */
+sppStatus sppAdvSums(const float* adv, int64_t n, double* sums2, void* stream);
+sppStatus sppAdvNormalizeGlobal(const float* adv, int64_t n_local, const double* sums2, int64_t n_global, float* out,
+                                void* stream);
 
 /* ------------------------------------------------------------------ on-policy nets (A2C / PPO)
  * The 64-wide tanh MLPs of rltoolkit/basic_model.py:7-76 used by A2C / PPO(_AcM):

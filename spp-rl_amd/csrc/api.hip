@@ -460,6 +460,32 @@ sppStatus sppAdvNormalize(const float* adv, int64_t n, float* out, void* stream)
   return SPP_OK;
 }
 
+sppStatus sppAdvSums(const float* adv, int64_t n, double* sums2, void* stream) {
+  SPP_REQUIRE(adv && sums2 && n >= 0, SPP_E_INVALID_ARG, "adv sums: bad args");
+  if (n == 0) {
+    SPP_CHECK_HIP(hipMemsetAsync(sums2, 0, sizeof(double) * 2, S(stream)));
+    return SPP_OK;
+  }
+  const int nblk = (int)std::min<int64_t>(cdiv(n, 256), 1024);
+  double* part = nullptr;
+  SPP_CHECK_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * nblk, S(stream)));
+  hipLaunchKernelGGL(k_adv_moments, dim3(nblk), dim3(256), 0, S(stream), adv, n, part);
+  hipLaunchKernelGGL(k_adv_sum2, dim3(1), dim3(64), 0, S(stream), (const double*)part, nblk, sums2);
+  SPP_CHECK_HIP(hipFreeAsync(part, S(stream)));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAdvNormalizeGlobal(const float* adv, int64_t n_local, const double* sums2, int64_t n_global, float* out,
+                                void* stream) {
+  SPP_REQUIRE(adv && out && sums2 && n_local >= 0 && n_global > 0, SPP_E_INVALID_ARG, "adv normalize dp: bad args");
+  if (n_local == 0) return SPP_OK;
+  hipLaunchKernelGGL(k_adv_norm_g, dim3((int)std::min<int64_t>(cdiv(n_local, 256), 1024)), dim3(256), 0, S(stream),
+                     adv, n_local, sums2, n_global, out);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
 sppStatus sppSynthEnvStep(const float* A, const float* obs, const float* action, int E, int ob, int ac,
                           float* next_obs, float* reward, void* stream) {
   SPP_REQUIRE(A && obs && action && next_obs && reward && E > 0, SPP_E_INVALID_ARG, "synth env: bad args");
@@ -818,9 +844,11 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
     for (int i = first; i < first + count; ++i) {
       DwJob& j = jobs[i];
       const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
-      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : cdiv(Bp, 2048);
+      // outputs that fit one 128x128 wave quadrant: the 4 waves split each item's samples
+      j.wsplit = (j.N <= 128 && j.K0 + j.K1 <= 128) ? 4 : 1;
+      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : cdiv(Bp, j.wsplit > 1 ? 1024 : 2048);
       ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
-      j.split_len = (int)round_up(cdiv(Bp, ns), 32);
+      j.split_len = (int)round_up(cdiv(Bp, ns), j.wsplit > 1 ? 128 : 32);
       j.nsplit = cdiv(Bp, j.split_len);
     }
   };
@@ -830,9 +858,9 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
   for (int ph = 0; ph < nph; ++ph) {
     size_t off = 0;
     for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-      if (jobs[j].nsplit > 1) {
+      if (jobs[j].nsplit * jobs[j].wsplit > 1) {
         jobs[j].slab = nullptr;
-        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+        off += (size_t)jobs[j].nsplit * jobs[j].wsplit * jobs[j].slab_stride;
       }
     }
     need = std::max(need, off);
@@ -846,9 +874,9 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
     size_t off = 0;
     std::vector<int> jj, ss;
     for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-      if (jobs[j].nsplit > 1) {
+      if (jobs[j].nsplit * jobs[j].wsplit > 1) {
         jobs[j].slab = D.slab.ptr + off;
-        off += (size_t)jobs[j].nsplit * jobs[j].slab_stride;
+        off += (size_t)jobs[j].nsplit * jobs[j].wsplit * jobs[j].slab_stride;
       }
     }
     // large-GEMM items first (they set the launch's critical path)

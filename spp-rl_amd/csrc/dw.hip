@@ -76,15 +76,21 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   const int split = item_split[item];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
   const int64_t ld = J.Bp;
-  const int b_begin = split * J.split_len;
-  const int b_end = min(b_begin + J.split_len, J.Bp);
-  const int nsteps = (b_end - b_begin) / 16;  // split_len and Bp are multiples of 32
+  const bool wsp = J.wsplit > 1;  // small output: every wave owns it, over a quarter of the samples
+  int b_begin = split * J.split_len;
+  int b_end = min(b_begin + J.split_len, J.Bp);
+  if (wsp) {  // quarters of whole 32-sample pairs of steps (dw_tile consumes steps in pairs)
+    const int q = (((b_end - b_begin + 3) / 4) + 31) & ~31;
+    b_begin = min(b_begin + w * q, b_end);
+    b_end = min(b_begin + q, b_end);
+  }
+  const int nsteps = (b_end - b_begin) / 16;  // even: ranges are multiples of 32 samples
   const int N = J.N, K = J.K0 + J.K1;
-  const int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1);
+  const int nb0 = wsp ? 0 : 4 * (w >> 1), kb0 = wsp ? 0 : 4 * (w & 1);
   const int ni = min(4, max(0, (N + 31) / 32 - nb0));
   const int nj = min(4, max(0, (K + 31) / 32 - kb0));
   if (ni == 0 || nj == 0) return;
-  const bool db = J.db != nullptr && (w & 1) == 0;
+  const bool db = J.db != nullptr && (wsp || (w & 1) == 0);
   // per-lane row pointers at this item's first sample; rows past N / K are
   // clamped to row 0 (their outputs are never stored)
   const float* ap[4];
@@ -117,8 +123,8 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   }
 #undef SPP_DW_CASE
   // partial (or final) result; rows >= nrow2 go to the second output (dW2/db2)
-  const bool direct = J.nsplit == 1;
-  float* slab = direct ? nullptr : J.slab + (int64_t)split * J.slab_stride;
+  const bool direct = J.nsplit * J.wsplit == 1;
+  float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + (wsp ? w : 0)) * J.slab_stride;
   auto out_w = [&](int n, int k, float v) {
     if (!direct) slab[(int64_t)n * K + k] = v;
     else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;
@@ -154,7 +160,8 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
 // elements of a job's [N*K | N] image, slabs summed in split order.
 __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const DwJob J = jobs[blockIdx.y];
-  if (J.nsplit == 1) return;
+  const int nslab = J.nsplit * J.wsplit;
+  if (nslab == 1) return;
   const int N = J.N, K = J.K0 + J.K1;
   const int64_t nw = (int64_t)N * K;
   const int64_t total = nw + (J.db ? N : 0);
@@ -164,7 +171,7 @@ __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const float* p = J.slab + e0;
   if (e0 + 4 <= total) {
     int sp = 0;
-    for (; sp + 4 <= J.nsplit; sp += 4) {
+    for (; sp + 4 <= nslab; sp += 4) {
       float4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(sp + u) * J.slab_stride);
@@ -173,12 +180,12 @@ __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
         s[0] += v[u].x; s[1] += v[u].y; s[2] += v[u].z; s[3] += v[u].w;
       }
     }
-    for (; sp < J.nsplit; ++sp) {
+    for (; sp < nslab; ++sp) {
       const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)sp * J.slab_stride);
       s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
     }
   } else {
-    for (int sp = 0; sp < J.nsplit; ++sp)
+    for (int sp = 0; sp < nslab; ++sp)
       for (int u = 0; e0 + u < total; ++u) s[u] += p[(int64_t)sp * J.slab_stride + u];
   }
 #pragma unroll

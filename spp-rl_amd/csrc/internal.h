@@ -14,10 +14,11 @@ struct DwJob {
   float* db;        // [nrow2] or null
   float* dW2;       // rows [nrow2, N) (second output, e.g. the log-std head), or null
   float* db2;
-  float* slab;      // split partials [nsplit][slab_stride]
+  float* slab;      // split partials [nsplit * wsplit][slab_stride]
   int64_t slab_stride;
   int N, K0, K1, Bp;
   int split_len, nsplit, nrow2;
+  int wsplit;       // 4: output <= 128x128, the 4 waves of an item split its samples (one slab each); else 1
 };
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)

@@ -216,4 +216,26 @@ __global__ void k_adv_norm(const float* __restrict__ a, int64_t n, const double*
     out[i] = fdiv_rn(fsub_rn(a[i], mean), den);
 }
 
+
+// Data-parallel AdvantageDataset normalisation: ranks all-reduce the
+// fp64 (sum, sum of squares) of k_adv_sum2 and normalise with the global n.
+__global__ void k_adv_sum2(const double* __restrict__ part, int nblk, double* __restrict__ sums) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0, s2 = 0.0;
+  for (int i = 0; i < nblk; ++i) {
+    s += part[2 * i];
+    s2 += part[2 * i + 1];
+  }
+  sums[0] = s;
+  sums[1] = s2;
+}
+__global__ void k_adv_norm_g(const float* __restrict__ a, int64_t n_local, const double* __restrict__ sums,
+                             int64_t n, float* __restrict__ out) {
+  const double mean = sums[0] / (double)n;
+  const double var = n > 1 ? fmax(0.0, (sums[1] - sums[0] * mean) / (double)(n - 1)) : 0.0;
+  const float m = (float)mean, den = fadd_rn((float)sqrt(var), 1.2e-7f);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_local; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = fdiv_rn(fsub_rn(a[i], m), den);
+}
+
 }  // namespace spp

@@ -71,6 +71,11 @@ class OnPolicyNets:
         lim = np.full(aout, float(ac_lim), np.float32) if np.ndim(ac_lim) == 0 else np.asarray(ac_lim, np.float32)
         call("sppOnpSetLimits", self._h, lim.ctypes.data_as(ctypes.c_void_p))
         self.loss = {}
+        # data parallel (one process per GPU, equal shards): gradient averaging and global sums
+        from .dp import make_allreduce, make_allreduce_sum
+
+        self.allreduce, self.allreduce_sum = make_allreduce(), make_allreduce_sum()
+        self.world = torch.distributed.get_world_size() if self.allreduce is not None else 1
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -96,6 +101,8 @@ class OnPolicyNets:
         x, q = self._dev(x), self._dev(q).reshape(-1)
         loss = torch.zeros(1, device=self.device)
         call("sppOnpCriticGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
+        if self.allreduce is not None:  # data parallel: average the critic gradient (RCCL)
+            self.allreduce(self.grads[1])
         call("sppOnpCriticApply", self._h, stream_handle())
         self._keep = (x, q)
         return loss
@@ -122,6 +129,9 @@ class OnPolicyNets:
         out = torch.zeros(4, device=self.device)
         call("sppOnpActorGrads", self._h, ptr(x), ptr(act), ptr(lp_old.reshape(-1)), ptr(adv.reshape(-1)), ptr(nxt),
              x.shape[0], ptr(out), stream_handle())
+        if self.allreduce is not None:  # average the actor gradient and the loss / KL partials
+            self.allreduce(self.grads[0])
+            self.allreduce(out)
         call("sppOnpActorApply", self._h, stream_handle())
         self._keep = (x, act, lp_old, adv, nxt)
         return out
@@ -131,7 +141,16 @@ class OnPolicyNets:
         random permutation per epoch like the reference's DataLoader(shuffle=True)."""
         adv = self._dev(advantages).reshape(-1)
         if self.normalize_adv:
-            adv = ppo.normalize_advantages(adv)
+            if self.allreduce_sum is not None:  # global moments over the ranks' shards (SURVEY §8e)
+                sums = torch.zeros(2, dtype=torch.float64, device=self.device)
+                call("sppAdvSums", ptr(adv), adv.numel(), ptr(sums), stream_handle())
+                self.allreduce_sum(sums)
+                out = torch.empty_like(adv)
+                call("sppAdvNormalizeGlobal", ptr(adv), adv.numel(), ptr(sums), adv.numel() * self.world, ptr(out),
+                     stream_handle())
+                adv = out
+            else:
+                adv = ppo.normalize_advantages(adv)
         obs, actions, logprobs = self._dev(obs), self._dev(actions), self._dev(logprobs).reshape(-1)
         nxt = self._dev(next_obs) if next_obs is not None else None
         N = obs.shape[0]
@@ -141,8 +160,9 @@ class OnPolicyNets:
             if kl >= self.kl_div_threshold:
                 break
             perm = torch.randperm(N, generator=generator).to(self.device)
-            for s in range(0, N, self.ppo_batch_size):
-                j = perm[s:s + self.ppo_batch_size]
+            mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
+            for s in range(0, N, mb):
+                j = perm[s:s + mb]
                 out = self.actor_step(obs[j], actions[j], logprobs[j], adv[j], nxt[j] if nxt is not None else None)
                 sums += out
             kl = float(out[1].item())  # KL of the epoch's last minibatch (ppo.py:188)

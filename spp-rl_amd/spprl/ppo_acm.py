@@ -40,7 +40,7 @@ class PPO_AcM:
     def __init__(self, env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=2000,
                  ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0, ppo_epsilon=0.2,
                  gae_lambda=0.95, critic_num_target_updates=10, num_critic_updates_per_target=10, normalize_adv=True,
-                 custom_loss=0.1, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                 custom_loss=0.1, norm_closs=config.NORM_CLOSS, min_max_denormalize=True, denormalize_actor_out=True,
                  acm_epochs=5, acm_batch_size=64, acm_update_freq=3, acm_lr=3e-4, acm_update_batches=None,
                  acm_pre_train_samples=100_000, acm_pre_train_epochs=5, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
                  acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, iterations=1001,

@@ -30,6 +30,7 @@
 #endif
 #endif
 #include "onp.hip"
+#include "sgd.hip"
 
 namespace spp {
 
@@ -1548,6 +1549,30 @@ sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
   SPP_REQUIRE(a && a->d_adam.ptr, SPP_E_STATE, "agent not ready");
   a->steps[3] += 1;
   launch_adam(a, 3, 1, a->net[SPP_NET_ACM].n, a->steps[3], a->cfg.acm_lr, 0.f, S(stream));
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAcmSgd(sppAgentHandle a, sppReplayHandle r, const int64_t* idx, int nsteps, int bs, float* loss_sum,
+                    void* stream) {
+  SPP_REQUIRE(a && r && idx && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
+  SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
+  SPP_REQUIRE(bs <= kSgdMaxBatch, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kSgdMaxBatch);
+  SPP_REQUIRE(r->d.ob == a->cfg.ob && r->d.ac == a->cfg.ac, SPP_E_SHAPE, "acm_sgd: replay dims differ");
+  sppStatus s = check_ready(a);
+  if (s) return s;
+  if (nsteps == 0) return SPP_OK;
+  const NetBufs& n = a->net[SPP_NET_ACM];
+  SPP_REQUIRE(n.p && n.m && n.v, SPP_E_STATE, "acm_sgd: ACM buffers not bound");
+  AcmSgdArgs g{r->d, idx, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout,
+               loss_sum};
+  const int ob = a->cfg.ob, ac = a->cfg.ac;
+  hipStream_t st = S(stream);
+  if (ob == 11 && ac == 3) hipLaunchKernelGGL((k_acm_sgd<22, 3>), dim3(1), dim3(kSgdThreads), 0, st, g);
+  else if (ob == 17 && ac == 6) hipLaunchKernelGGL((k_acm_sgd<34, 6>), dim3(1), dim3(kSgdThreads), 0, st, g);
+  else if (ob == 3 && ac == 1) hipLaunchKernelGGL((k_acm_sgd<6, 1>), dim3(1), dim3(kSgdThreads), 0, st, g);
+  else SPP_REQUIRE(false, SPP_E_SHAPE, "acm_sgd: no instantiation for ob=%d ac=%d", ob, ac);
+  a->steps[3] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

@@ -84,6 +84,7 @@ class DDPG_AcM(OffPolicyLoop):
         rb = self.replay_buffer
         call("sppAgentBindNormalizer", self._h, ptr(rb.min_obs), ptr(rb.max_obs), ptr(rb.obs_mean), ptr(rb.obs_std))
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
+        self.acm_kind = "basic"  # BasicAcM: per-step regression path
         self._init_loop(update_batch_size=update_batch_size, **unused)
 
     def __del__(self):

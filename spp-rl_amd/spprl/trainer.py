@@ -454,13 +454,26 @@ class OffPolicyLoop:
         call("sppAcmRegressApply", self._h, st)
         self._keep_acm_xy = (idx, x, y)
 
+    def _acm_sgd_ok(self, bs):
+        """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank."""
+        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 128
+                and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1)))
+
+    def _acm_sgd(self, idx, nsteps, bs):
+        call("sppAcmSgd", self._h, self.replay_buffer._h, ptr(idx), nsteps, bs, ptr(self._acm_loss_acc),
+             stream_handle())
+        self._keep_sgd = idx
+
     def update_acm_batches(self, n_batches):
         """acm.py:356-372: n batches of acm_batch_size uniform samples; loss = batch mean."""
         n = len(self.replay_buffer)
         self._acm_loss_acc.zero_()
-        for _ in range(n_batches):
-            self._acm_step_from_idx(self._rand_idx(self.acm_batch_size, n))
-            self._acm_loss_acc += self._acm_loss
+        if self._acm_sgd_ok(self.acm_batch_size):
+            self._acm_sgd(self._rand_idx(n_batches * self.acm_batch_size, n), n_batches, self.acm_batch_size)
+        else:
+            for _ in range(n_batches):
+                self._acm_step_from_idx(self._rand_idx(self.acm_batch_size, n))
+                self._acm_loss_acc += self._acm_loss
         self._acm_loss_acc /= n_batches
 
     def update_acm(self, epochs, pretrain=False):
@@ -475,11 +488,17 @@ class OffPolicyLoop:
             self._set_acm_lr(lr)
             perm = torch.randperm(n, generator=g).to(self.device)
             self._acm_loss_acc.zero_()
-            nb = 0
-            for s in range(0, n, self.acm_batch_size):
-                self._acm_step_from_idx(perm[s:s + self.acm_batch_size].contiguous())
-                self._acm_loss_acc += self._acm_loss
-                nb += 1
+            bs = self.acm_batch_size
+            nb = -(-n // bs)
+            if self._acm_sgd_ok(bs):  # one launch for the full batches, one for the ragged last batch
+                full = n // bs
+                self._acm_sgd(perm, full, bs)
+                if n % bs:
+                    self._acm_sgd(perm[full * bs:].contiguous(), 1, n % bs)
+            else:
+                for s in range(0, n, bs):
+                    self._acm_step_from_idx(perm[s:s + bs].contiguous())
+                    self._acm_loss_acc += self._acm_loss
             self._acm_loss_acc /= max(nb, 1)
             self._acm_sched_epochs += 1
         self._set_acm_lr(self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step))

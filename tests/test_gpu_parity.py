@@ -368,3 +368,32 @@ def test_obs_stats_data_parallel_protocol_matches_union(ob, ranks):
     allx = np.concatenate(data).astype(np.float64)
     np.testing.assert_array_equal(union.max_obs.cpu().numpy(), np.percentile(allx, 99, axis=0).astype(np.float32))
     np.testing.assert_array_equal(union.min_obs.cpu().numpy(), np.percentile(allx, 1, axis=0).astype(np.float32))
+
+
+@pytest.mark.parametrize("env_name,ob,ac,bs", [("Hopper-v2", 11, 3, 100), ("HalfCheetah-v2", 17, 6, 64)])
+def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
+    """sppAcmSgd (K sequential AcM regression steps in one launch, parameters in LDS) against
+    the oracle's AcMTrainer.batch_update sequence on the same replay batches (acm.py:246-264):
+    losses rtol 1e-4; parameters after K Adam steps within 1e-5 * max(1, |p|) except for a
+    few lr-sized flips of near-zero-moment coordinates."""
+    ag = _filled_agent(env_name, ob, ac, 2000, seed=4)
+    rb = ag.replay_buffer
+    params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}
+    o = OracleAcmTrainer(2 * ob, ac, lr=ag.acm_lr, ac_lim=ag.ac_lim.numpy(), params=params)
+    K = 6
+    idx = torch.from_numpy(np.random.RandomState(11).randint(0, 2000, K * bs)).to(DEV)
+    loss = torch.zeros(1, device=DEV)
+    _lib.call("sppAcmSgd", ag._h, rb._h, _lib.ptr(idx), K, bs, _lib.ptr(loss), _lib.stream_handle())
+    ol = 0.0
+    for k in range(K):
+        obs, nobs, _, _, _, acm = rb.gather(idx[k * bs:(k + 1) * bs])
+        ol += o.batch_update(torch.cat([obs, nobs], 1).cpu().numpy(), acm.cpu().numpy())
+    torch.cuda.synchronize()
+    assert float(loss.item()) == pytest.approx(ol, rel=1e-4)
+    got = ag.params[_lib.SPP_NET_ACM].cpu().numpy()
+    ref = o.flat()
+    d = np.abs(got - ref)
+    assert np.mean(d > 1e-5 * np.maximum(1, np.abs(ref))) < 5e-3 and d.max() < 4 * K * ag.acm_lr
+    steps = np.zeros(4, np.int64)
+    _lib.call("sppAgentGetSteps", ag._h, steps.ctypes.data_as(__import__("ctypes").c_void_p))
+    assert steps[3] == K

@@ -177,3 +177,69 @@ def test_dp_obs_stats_protocol_gloo():
         np.testing.assert_allclose(std, allx.std(0).astype(np.float32), rtol=1e-6)
     for a, b in zip(res[0], res[1]):
         np.testing.assert_array_equal(a, b)
+
+
+def _ppo_worker(rank, port, q):
+    """One data-parallel PPO_AcM actor step (OnPolicyNets.update_actor's exchange points):
+    global advantage moments (sppAdvSums -> all-reduce -> sppAdvNormalizeGlobal, oracle form),
+    per-rank half minibatch, gradient and loss/KL averaging with spprl.dp.make_allreduce."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from oracle import onpolicy as oo
+        from spprl.dp import make_allreduce, make_allreduce_sum
+
+        ob, aout, N = 17, 17, 512
+        x, act, lp_old, adv, flat = _ppo_case(ob, aout, N)
+        sl = slice(rank * N // WORLD, (rank + 1) * N // WORLD)
+        a = torch.from_numpy(adv[sl].astype(np.float64))
+        sums = torch.stack([a.sum(), (a * a).sum()])
+        make_allreduce_sum()(sums)
+        mean = sums[0] / N
+        std = torch.sqrt(torch.clamp((sums[1] - sums[0] * mean) / (N - 1), min=0.0))
+        an = ((a - mean) / (std.float() + 1.2e-7)).float().numpy()
+        out, g = oo.actor_step(flat, ob, aout, np.ones(aout, np.float32), x[sl], act[sl], lp_old[sl], an)
+        gt = torch.from_numpy(g)
+        ot = torch.tensor([out["actor"], out["kl"]])
+        ar = make_allreduce()
+        ar(gt)
+        ar(ot)
+        q.put((rank, an, gt.numpy(), ot.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _ppo_case(ob, aout, N):
+    from oracle import onpolicy as oo
+
+    rng = np.random.RandomState(6)
+    flat = oo.init_flat(oo.actor_layout(ob, aout), 3)
+    x = rng.randn(N, ob).astype(np.float32)
+    act, _ = oo.act(flat, ob, aout, np.ones(aout, np.float32), x, rng.randn(N, aout).astype(np.float32))
+    lp_old = (rng.randn(N) * 0.1 - 20).astype(np.float32)
+    adv = (rng.randn(N) * 3 + 1).astype(np.float32)
+    return x, act.astype(np.float32), lp_old, adv, flat
+
+
+def test_dp_ppo_actor_exchange_gloo():
+    from oracle import onpolicy as oo
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(60)
+    ob, aout, N = 17, 17, 512
+    x, act, lp_old, adv, flat = _ppo_case(ob, aout, N)
+    an = ((adv - adv.mean()) / (adv.std(ddof=1) + 1.2e-7)).astype(np.float32)  # AdvantageDataset
+    np.testing.assert_allclose(np.concatenate([res[0][0], res[1][0]]), an, rtol=1e-5, atol=1e-6)
+    out, g = oo.actor_step(flat, ob, aout, np.ones(aout, np.float32), x, act, lp_old, an)
+    for r in range(WORLD):
+        np.testing.assert_array_equal(res[r][1], res[0][1])  # replicas agree
+        assert np.abs(res[r][1] - g).max() <= 1e-5 * np.abs(g).max()
+        np.testing.assert_allclose(res[r][2], [out["actor"], out["kl"]], rtol=1e-5, atol=1e-6)

@@ -846,10 +846,13 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
       DwJob& j = jobs[i];
       const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
       // outputs that fit one 128x128 wave quadrant: the 4 waves split each item's samples
-      j.wsplit = (j.N <= 128 && j.K0 + j.K1 <= 128) ? 4 : 1;
-      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : cdiv(Bp, j.wsplit > 1 ? 1024 : 2048);
+      const bool thin_n = j.N <= 128, thin_k = j.K0 + j.K1 <= 128;
+      j.wsplit = thin_n && thin_k ? 4 : (thin_n != thin_k ? 2 : 1);
+      // small jobs: >= 2048 samples per item, and at most ~256 slabs (the fixed-order reduce is
+      // serial over slabs)
+      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
       ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
-      j.split_len = (int)round_up(cdiv(Bp, ns), j.wsplit > 1 ? 128 : 32);
+      j.split_len = (int)round_up(cdiv(Bp, ns), 32 * j.wsplit);
       j.nsplit = cdiv(Bp, j.split_len);
     }
   };

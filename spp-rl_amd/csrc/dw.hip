@@ -76,21 +76,36 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   const int split = item_split[item];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
   const int64_t ld = J.Bp;
-  const bool wsp = J.wsplit > 1;  // small output: every wave owns it, over a quarter of the samples
+  // Waves whose output quadrant would be empty take part of the samples instead:
+  //   wsplit 4 (N, K <= 128): all 4 waves on quadrant (0, 0), a quarter of the samples each;
+  //   wsplit 2 (one side <= 128): 2 quadrants along the wide side, 2 sample halves each.
+  const int N = J.N, K = J.K0 + J.K1;
+  const bool wsp = J.wsplit > 1;
+  int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1), part = 0;
+  if (J.wsplit == 4) {
+    nb0 = kb0 = 0;
+    part = w;
+  } else if (J.wsplit == 2) {
+    if (N <= 128) {
+      nb0 = 0;
+      part = w >> 1;
+    } else {
+      kb0 = 0;
+      part = w & 1;
+    }
+  }
   int b_begin = split * J.split_len;
   int b_end = min(b_begin + J.split_len, J.Bp);
-  if (wsp) {  // quarters of whole 32-sample pairs of steps (dw_tile consumes steps in pairs)
-    const int q = (((b_end - b_begin + 3) / 4) + 31) & ~31;
-    b_begin = min(b_begin + w * q, b_end);
+  if (wsp) {  // parts of whole 32-sample pairs of steps (dw_tile consumes steps in pairs)
+    const int q = (((b_end - b_begin + J.wsplit - 1) / J.wsplit) + 31) & ~31;
+    b_begin = min(b_begin + part * q, b_end);
     b_end = min(b_begin + q, b_end);
   }
   const int nsteps = (b_end - b_begin) / 16;  // even: ranges are multiples of 32 samples
-  const int N = J.N, K = J.K0 + J.K1;
-  const int nb0 = wsp ? 0 : 4 * (w >> 1), kb0 = wsp ? 0 : 4 * (w & 1);
   const int ni = min(4, max(0, (N + 31) / 32 - nb0));
   const int nj = min(4, max(0, (K + 31) / 32 - kb0));
   if (ni == 0 || nj == 0) return;
-  const bool db = J.db != nullptr && (wsp || (w & 1) == 0);
+  const bool db = J.db != nullptr && kb0 == 0;
   // per-lane row pointers at this item's first sample; rows past N / K are
   // clamped to row 0 (their outputs are never stored)
   const float* ap[4];
@@ -124,7 +139,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
 #undef SPP_DW_CASE
   // partial (or final) result; rows >= nrow2 go to the second output (dW2/db2)
   const bool direct = J.nsplit * J.wsplit == 1;
-  float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + (wsp ? w : 0)) * J.slab_stride;
+  float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + part) * J.slab_stride;
   auto out_w = [&](int n, int k, float v) {
     if (!direct) slab[(int64_t)n * K + k] = v;
     else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;

@@ -248,9 +248,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SPP_DIST_BACKEND=gloo (testing only): ranks may share one GPU; the default is RCCL ("nccl")
+    backend = os.environ.get("SPP_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -370,6 +377,12 @@ def main():
         "step_tflops": round(flop_step * args.steps / elapsed / 1e12, 2),
         "losses": {k: round(v, 5) for k, v in losses.items()},
     }
+    if world > 1:  # data-parallel replicas must stay bit-identical (same averaged grads, same Adam)
+        chk = torch.stack([p.double().sum() for p in ag.params.values()] +
+                          [p.double().abs().sum() for p in ag.params.values()])
+        allc = [torch.empty_like(chk) for _ in range(world)]
+        dist.all_gather(allc, chk)
+        result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:

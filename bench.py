@@ -36,6 +36,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA peak
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
@@ -54,6 +55,14 @@ CONFIGS = {
                    custom_loss=1.0, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
                    update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=500,
                    acm_update_batches=200, acm_batch_size=128)),
+    "sac_ant_bf16": dict(
+        algo="sac", env="Ant-v2", ob=111, ac=8, envs=4096, buffer=1_000_000, baseline_idx=4, bf16=True,
+        workload="SPP-SAC Ant (111-dim obs), %d vectorized envs per GPU, bf16 MFMA MLP + fp32 targets "
+                 "(BASELINE.json configs[4] per-GPU shape)",
+        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
+                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
+                   acm_update_batches=100, acm_batch_size=100, mlp_bf16=True)),
     "sac_ant": dict(
         algo="sac", env="Ant-v2", ob=111, ac=8, envs=4096, buffer=1_000_000, baseline_idx=4,
         workload="SPP-SAC Ant (111-dim obs), %d vectorized envs per GPU, fp32 MLP (BASELINE.json configs[4] "
@@ -349,6 +358,8 @@ def main():
         except Exception:
             traffic = None
     flop_step = 2.0 * (mac["update"] * B + mac["acm_reg"] * BA + mac["act"] * E)
+    bf16 = cfg.get("bf16", False)
+    peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     kname = "k_sac_critic_phase" if cfg["algo"] == "sac" else "k_ddpg_critic_phase"
     result = {
         "metric": "env-steps/sec (rollout+update) %s" % ("SPP-SAC " + cfg["env"] if cfg["algo"] == "sac"
@@ -362,14 +373,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16 MFMA MLP, fp32 accumulate / targets / optimizer" if bf16 else "fp32",
         "data": "synthetic: SynthEnv linear-tanh dynamics (%s shapes ob=%d, ac=%d), random-init networks, replay "
                 "pre-filled with N(0,1) transitions" % (cfg["env"], ob, ac),
         "config": {"workload": cfg["workload"] % E, "envs_per_gpu": E, "update_batch": B, "acm_batch": BA,
                    "rho": rho, "sigma": sigma, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world},
         "roofline": {"bound": "mfma", "kernel": "%s (critic targets + critic fwd/bwd)" % kname,
-                     "achieved": round(crit_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(crit_tf / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+                     "achieved": round(crit_tf, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(crit_tf / peak, 4), "traffic": traffic,
                      "flop_per_launch": 2.0 * mac["critic_phase"] * B, "avg_launch_ms": round(k_ms["critic_phase"], 3)},
         "kernels_ms_per_launch": {k: round(v, 3) for k, v in k_ms.items()},
         "kernels_tflops": {"critic_phase": round(crit_tf, 2), "actor_phase": round(act_tf, 2),

@@ -131,6 +131,8 @@ typedef struct {
   float actor_lr, critic_lr, alpha_lr, acm_lr;
   float target_entropy;     /* sac.py:104-106: -env ac_dim (Q4) */
   int max_batch;            /* workspace sizing (update batch B) */
+  int mlp_bf16;             /* 1: MLP layers on bf16 MFMA (v_mfma_f32_32x32x16_bf16), fp32 accumulation, epilogues,
+                               targets, losses and Adam (BASELINE configs[4]); SAC_AcM Hopper / Ant dims */
 } sppAgentConfig;
 
 typedef struct sppAgent* sppAgentHandle;

@@ -27,6 +27,7 @@
 #include "ks_sac_ant.hip"
 #include "ks_sac_small.hip"
 #include "ks_ddpg.hip"
+#include "ks_sac_bf16.hip"
 #endif
 #endif
 #include "onp.hip"
@@ -571,7 +572,14 @@ struct DwSet {
 
 // dims -> kernel instantiation: one translation unit per config family (ks_*.hip),
 // compiled in parallel by build.py and linked into libspprl.so.
-static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, KernelSet* ks) {
+static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, KernelSet* ks) {
+  if (bf16) {
+#ifndef SPP_ONLY_HOPPER
+    return algo == SPP_ALGO_SAC_ACM && kset_sac_bf16(ob, aout, ac, acmc, ks);
+#else
+    return false;
+#endif
+  }
   if (algo == SPP_ALGO_SAC_ACM) {
     if (kset_sac_hopper(ob, aout, ac, acmc, ks)) return true;
 #ifndef SPP_ONLY_HOPPER  // kernel-development builds: one instantiation, fast compile
@@ -688,7 +696,7 @@ static sppStatus build_packs(sppAgent* a) {
   // ib = 1: ib-major image for dense_lds (256-input layers)
   auto M = [&](std::vector<PackJob>* list, const float* W, const float* W2, int split, int ld, int trans, int coff,
                MapDesc out, MapDesc in, int NBO, int NBI, const float4** slot, int ib = 0) {
-    PackJob j{W, W2, split, ld, trans, coff, out, in, NBO, NBI, ib, nullptr};
+    PackJob j{W, W2, split, ld, trans, coff, out, in, NBO, NBI, ib, nullptr, a->cfg.mlp_bf16 ? 1 : 0};
     ms.push_back({list, j, slot});
   };
   // LDS table: each vector starts on a 32-float boundary, zero padded to a whole block
@@ -925,6 +933,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     j.nrow2 = nrow2 < 0 ? N : nrow2;
     j.dW2 = dW2; j.db2 = db2;
     j.slab_stride = round_up((int64_t)N * (K0 + K1) + N, 4);
+    j.bf16 = a->cfg.mlp_bf16 ? 1 : 0;
     jobs.push_back(j);
   };
   DwSet& D = a->dws[set];
@@ -1090,8 +1099,9 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
               "unsupported algo %d", cfg->algo);
   SPP_REQUIRE(cfg->max_batch > 0, SPP_E_INVALID_ARG, "max_batch must be > 0");
   KernelSet ks;
-  SPP_REQUIRE(find_kset(cfg->algo, cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, &ks), SPP_E_SHAPE,
-              "no kernel instantiation for algo %d (ob=%d, aout=%d, ac=%d)", cfg->algo, cfg->ob, cfg->aout, cfg->ac);
+  SPP_REQUIRE(find_kset(cfg->algo, cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, cfg->mlp_bf16 != 0, &ks),
+              SPP_E_SHAPE, "no kernel instantiation for algo %d (ob=%d, aout=%d, ac=%d, bf16=%d)", cfg->algo, cfg->ob,
+              cfg->aout, cfg->ac, cfg->mlp_bf16);
   SPP_CHECK_HIP(hipSetDevice(device));
   auto a = std::make_unique<sppAgent>();
   a->cfg = *cfg;

@@ -24,7 +24,16 @@ constexpr int kDwRing = 2;  // steps (16 samples each) in flight
 // One step = 16 samples: lane half h takes samples [16t + 8h, +8) of each of
 // its rows as two adjacent float4 (a full 64 B run per row and half), i.e. 8
 // MFMA k-steps per row pair.
-template <int NI, int NJ, bool DB>
+__device__ __forceinline__ bf16x8 pack8(const float4& a, const float4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
+  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
+  return r;
+}
+
+// BF: one v_mfma_f32_32x32x16_bf16 per (row block, column block) per 16-sample step: lane half
+// h's 8 samples are exactly the MFMA's k = 8h + j slots on both operands (bf16 agents, mlp_bf16).
+template <int NI, int NJ, bool DB, bool BF = false>
 __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
                                         f32x16 (&acc)[4][4], float (&bs)[4]) {
   float4 ra[kDwRing][NI][2], rx[kDwRing][NJ][2];
@@ -52,19 +61,30 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
       const int tn = t0 + u + kDwRing - 1;
       if (tn < nsteps) load(IC<sn>{}, tn);
       __builtin_amdgcn_sched_barrier(0);
-      static_for<0, NI>([&](auto I) {
-        static_for<0, 2>([&](auto P) {
-          const float4 av = ra[u][I][P];
-          if constexpr (DB) bs[I] += (av.x + av.y) + (av.z + av.w);
-          static_for<0, NJ>([&](auto J) {
-            const float4 xv = rx[u][J][P];
-            acc[I][J] = mfma(av.x, xv.x, acc[I][J]);
-            acc[I][J] = mfma(av.y, xv.y, acc[I][J]);
-            acc[I][J] = mfma(av.z, xv.z, acc[I][J]);
-            acc[I][J] = mfma(av.w, xv.w, acc[I][J]);
+      if constexpr (BF) {
+        static_for<0, NI>([&](auto I) {
+          if constexpr (DB) {
+            const float4 a0 = ra[u][I][0], a1 = ra[u][I][1];
+            bs[I] += ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
+          }
+          const bf16x8 av = pack8(ra[u][I][0], ra[u][I][1]);
+          static_for<0, NJ>([&](auto J) { acc[I][J] = mfma16(av, pack8(rx[u][J][0], rx[u][J][1]), acc[I][J]); });
+        });
+      } else {
+        static_for<0, NI>([&](auto I) {
+          static_for<0, 2>([&](auto P) {
+            const float4 av = ra[u][I][P];
+            if constexpr (DB) bs[I] += (av.x + av.y) + (av.z + av.w);
+            static_for<0, NJ>([&](auto J) {
+              const float4 xv = rx[u][J][P];
+              acc[I][J] = mfma(av.x, xv.x, acc[I][J]);
+              acc[I][J] = mfma(av.y, xv.y, acc[I][J]);
+              acc[I][J] = mfma(av.z, xv.z, acc[I][J]);
+              acc[I][J] = mfma(av.w, xv.w, acc[I][J]);
+            });
           });
         });
-      });
+      }
     });
   }
 }
@@ -125,10 +145,15 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
-#define SPP_DW_CASE(I, J_)                                             \
-  case (I) * 8 + (J_):                                                 \
-    if (db) dw_tile<I, J_, true>(ap, xp, nsteps, acc, bs);             \
-    else dw_tile<I, J_, false>(ap, xp, nsteps, acc, bs);               \
+#define SPP_DW_CASE(I, J_)                                                      \
+  case (I) * 8 + (J_):                                                          \
+    if (J.bf16) {                                                               \
+      if (db) dw_tile<I, J_, true, true>(ap, xp, nsteps, acc, bs);              \
+      else dw_tile<I, J_, false, true>(ap, xp, nsteps, acc, bs);                \
+    } else {                                                                    \
+      if (db) dw_tile<I, J_, true>(ap, xp, nsteps, acc, bs);                    \
+      else dw_tile<I, J_, false>(ap, xp, nsteps, acc, bs);                      \
+    }                                                                           \
     break;
   switch (ni * 8 + nj) {
     SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)

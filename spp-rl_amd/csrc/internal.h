@@ -19,6 +19,7 @@ struct DwJob {
   int N, K0, K1, Bp;
   int split_len, nsplit, nrow2;
   int wsplit;       // 4: output <= 128x128, the 4 waves of an item split its samples (one slab each); else 1
+  int bf16;         // 1: bf16 MFMA (operands rounded to bf16 in registers, fp32 accumulation)
 };
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)
@@ -32,6 +33,7 @@ struct PackJob {
   MapDesc out, in;
   int NBO, NBI, ibmajor;
   float4* dst;
+  int bf16;  // 1: bf16 image for v_mfma_f32_32x32x16_bf16 (2 fragments of 8 bf16 per block pair, mlp.h)
 };
 
 struct AdamJob {

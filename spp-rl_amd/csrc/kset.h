@@ -19,9 +19,9 @@ struct KernelSet {
   void (*dreg)(SacArgs, BAcmRegArgs);
 };
 
-template <int OB, int AOUT, int AC, bool ACMC>
+template <int OB, int AOUT, int AC, bool ACMC, bool BF = false>
 KernelSet make_kset() {
-  using C = Cfg<OB, AOUT, AC, ACMC>;
+  using C = Cfg<OB, AOUT, AC, ACMC, BF>;
   return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>,
           nullptr, nullptr, nullptr, nullptr};
 }
@@ -43,5 +43,6 @@ bool kset_sac_hcheetah(int ob, int aout, int ac, bool acmc, KernelSet* ks);  // 
 bool kset_sac_ant(int ob, int aout, int ac, bool acmc, KernelSet* ks);       // ks_sac_ant.hip
 bool kset_sac_small(int ob, int aout, int ac, bool acmc, KernelSet* ks);     // ks_sac_small.hip
 bool kset_ddpg(int ob, int aout, int ac, bool acmc, KernelSet* ks);          // ks_ddpg.hip
+bool kset_sac_bf16(int ob, int aout, int ac, bool acmc, KernelSet* ks);      // ks_sac_bf16.hip
 
 }  // namespace spp

@@ -267,16 +267,6 @@ __device__ __forceinline__ void dense_impl(const float4* __restrict__ Wf, int NB
   epi(NBO - 1, prev);
   SPP_TP(25);
 }
-template <int NBI, uint64_t RV, typename Epi>
-__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
-                                      const float* biasL, Epi&& epi) {
-  dense_impl<NBI, RV, true>(Wf, NBO, in, biasL, static_cast<Epi&&>(epi));
-}
-template <int NBI, uint64_t RV, typename Epi>
-__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI], decltype(nullptr),
-                                      Epi&& epi) {
-  dense_impl<NBI, RV, false>(Wf, NBO, in, nullptr, static_cast<Epi&&>(epi));
-}
 
 constexpr int cgcd(int a, int b) { return b ? cgcd(b, a % b) : a; }
 
@@ -363,15 +353,162 @@ __device__ __forceinline__ void dense_lds_impl(const float4* __restrict__ Wf, co
   epi(IC<NBO - 1>{}, acc[NBO - 1]);
   SPP_TP(22);
 }
-template <int NBO, typename Epi>
+
+// ---------------------------------------------------------------- bf16 MFMA layers
+// v_mfma_f32_32x32x16_bf16: lane (i = l&31, h = l>>5) holds A[i][k = 8h + j] and
+// B[k = 8h + j][i], j = 0..7; D layout as the f32 form.  The input tile's registers
+// 8s .. 8s+7 (s = 0, 1) of block ib, converted to bf16 (RNE), are k-step s of that block:
+// element j of lane half h is unit unit_of(8s + j, h) (the k order inside a step is the
+// D-layout row order).  Weight images hold the matching 8 bf16 per lane:
+//   Wf16[((ob*NBI + ib)*2 + s)*64 + lane] (ob-major) / [((ib*NBO + ob)*2 + s)*64 + lane]
+//   element j = bf16(W[out_map(ob, lane&31)][in_map(ib, 8s + j, lane>>5)])
+// (k_pack_matrix with PackJob::bf16).  Accumulation is fp32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 frag16(float4 v) { return __builtin_bit_cast(bf16x8, v); }
+template <int S>
+__device__ __forceinline__ bf16x8 to_bf16x8(const f32x16& t) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)t[8 * S + j];
+  return r;
+}
+// k-steps of block ib that carry a valid register quad
+constexpr int st_get(uint64_t RV, int ib) { return (rv_get(RV, ib) + 1) / 2; }
+constexpr int st_total(uint64_t RV, int nb) {
+  int t = 0;
+  for (int ib = 0; ib < nb; ++ib) t += st_get(RV, ib);
+  return t;
+}
+constexpr int st_ib(uint64_t RV, int NBI, int q) {
+  int base = 0;
+  for (int b = 0; b < NBI; ++b) {
+    if (q < base + st_get(RV, b)) return b;
+    base += st_get(RV, b);
+  }
+  return NBI - 1;
+}
+constexpr int st_s(uint64_t RV, int NBI, int q) {
+  int base = 0;
+  for (int b = 0; b < NBI; ++b) {
+    if (q < base + st_get(RV, b)) return q - base;
+    base += st_get(RV, b);
+  }
+  return 0;
+}
+
+// Register-input layer, bf16 MFMA: the inputs are converted once, every output block's
+// fragments (one 16-B buffer load per k-step) are fetched one block ahead, and block ob's
+// MFMA chain is issued before block ob-1's epilogue (as dense_impl).
+template <int NBI, uint64_t RV, bool BIAS, typename Epi>
+__device__ __forceinline__ void dense16_impl(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
+                                             const float* biasL, Epi&& epi) {
+  constexpr int NS = st_total(RV, NBI);
+  static_assert(NS > 0, "empty layer");
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const rsrc_t wr = rsrc(Wf);
+  const uint32_t l16 = 16u * lane;
+  constexpr int OBSTRIDE = NBI * 2 * 64 * 16;  // bytes per output block
+  bf16x8 bin[NS];
+  static_for<0, NS>([&](auto Q) {
+    constexpr int q = Q;
+    bin[q] = to_bf16x8<st_s(RV, NBI, q)>(in[st_ib(RV, NBI, q)]);
+  });
+  float4 cur[NS];
+  static_for<0, NS>([&](auto Q) {
+    constexpr int q = Q;
+    cur[q] = wfrag(wr, l16, (st_ib(RV, NBI, q) * 2 + st_s(RV, NBI, q)) * 1024);
+  });
+  auto chain = [&](int ob) {
+    f32x16 acc;
+    if constexpr (BIAS) acc = bias_tile(biasL, ob, h);
+    else acc = zero16();
+    const int wn = (ob + 1 < NBO ? ob + 1 : ob) * OBSTRIDE;
+    float4 nxt[NS];
+    static_for<0, NS>([&](auto Q) {
+      constexpr int q = Q;
+      nxt[q] = wfrag(wr, l16, wn + (st_ib(RV, NBI, q) * 2 + st_s(RV, NBI, q)) * 1024);
+    });
+    static_for<0, NS>([&](auto Q) { acc = mfma16(frag16(cur[(int)Q]), bin[(int)Q], acc); });
+#pragma unroll
+    for (int q = 0; q < NS; ++q) cur[q] = nxt[q];
+    return acc;
+  };
+  f32x16 prev = chain(0);
+#pragma unroll 1
+  for (int ob = 1; ob < NBO; ++ob) {
+    const f32x16 acc = chain(ob);
+    epi(ob - 1, prev);
+    prev = acc;
+  }
+  epi(NBO - 1, prev);
+}
+
+// 256-input layer from the LDS image, bf16 MFMA: all NBO output blocks accumulate at once;
+// input block ib's fragments (2 per output block) are double-buffered one block ahead.
+template <int NBO, bool BIAS, typename Epi>
+__device__ __forceinline__ void dense16_lds_impl(const float4* __restrict__ Wf, const float* img, const float* biasL,
+                                                 Epi&& epi) {
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const float* l = img + 4 * h * 32 + (lane & 31);
+  const rsrc_t wr = rsrc(Wf);
+  const uint32_t l16 = 16u * lane;
+  f32x16 acc[NBO];
+  static_for<0, NBO>([&](auto O) {
+    if constexpr (BIAS) acc[O] = bias_tile(biasL, O, h);
+    else acc[O] = zero16();
+  });
+  float4 fr[2][2 * NBO];
+  static_for<0, 2 * NBO>([&](auto J) { fr[0][J] = wfrag(wr, l16, (int)J * 1024); });
+  static_for<0, 8>([&](auto IB) {
+    constexpr int ib = IB;
+    f32x16 x;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = l[(32 * ib + ru(r)) * 32];
+    const bf16x8 b0 = to_bf16x8<0>(x), b1 = to_bf16x8<1>(x);
+    if constexpr (ib + 1 < 8) {
+      static_for<0, 2 * NBO>([&](auto J) {
+        fr[(ib + 1) & 1][J] = wfrag(wr, l16, ((ib + 1) * NBO * 2 + (int)J) * 1024);
+      });
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, NBO>([&](auto O) {
+      constexpr int ob = O;
+      acc[ob] = mfma16(frag16(fr[ib & 1][2 * ob]), b0, acc[ob]);
+      acc[ob] = mfma16(frag16(fr[ib & 1][2 * ob + 1]), b1, acc[ob]);
+    });
+  });
+  static_for<0, NBO>([&](auto O) { epi(IC<(int)O>{}, acc[O]); });
+}
+
+// Front ends: BF selects the bf16 MFMA form (the weight images must be bf16 images).
+template <int NBI, uint64_t RV, bool BF = false, typename Epi>
+__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI],
+                                      const float* biasL, Epi&& epi) {
+  if constexpr (BF) dense16_impl<NBI, RV, true>(Wf, NBO, in, biasL, static_cast<Epi&&>(epi));
+  else dense_impl<NBI, RV, true>(Wf, NBO, in, biasL, static_cast<Epi&&>(epi));
+}
+template <int NBI, uint64_t RV, bool BF = false, typename Epi>
+__device__ __forceinline__ void dense(const float4* __restrict__ Wf, int NBO, const f32x16 (&in)[NBI], decltype(nullptr),
+                                      Epi&& epi) {
+  if constexpr (BF) dense16_impl<NBI, RV, false>(Wf, NBO, in, nullptr, static_cast<Epi&&>(epi));
+  else dense_impl<NBI, RV, false>(Wf, NBO, in, nullptr, static_cast<Epi&&>(epi));
+}
+template <int NBO, bool BF = false, typename Epi>
 __device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, const float* biasL,
                                           Epi&& epi) {
-  dense_lds_impl<NBO, true>(Wf, img, biasL, static_cast<Epi&&>(epi));
+  if constexpr (BF) dense16_lds_impl<NBO, true>(Wf, img, biasL, static_cast<Epi&&>(epi));
+  else dense_lds_impl<NBO, true>(Wf, img, biasL, static_cast<Epi&&>(epi));
 }
-template <int NBO, typename Epi>
+template <int NBO, bool BF = false, typename Epi>
 __device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const float* img, decltype(nullptr),
                                           Epi&& epi) {
-  dense_lds_impl<NBO, false>(Wf, img, nullptr, static_cast<Epi&&>(epi));
+  if constexpr (BF) dense16_lds_impl<NBO, false>(Wf, img, nullptr, static_cast<Epi&&>(epi));
+  else dense_lds_impl<NBO, false>(Wf, img, nullptr, static_cast<Epi&&>(epi));
 }
 
 // ---------------------------------------------------------------- loaders / stores

@@ -7,8 +7,41 @@
 
 namespace spp {
 
+__device__ __forceinline__ float pack_src(const PackJob& J, int n, int k) {
+  if (n < 0 || k < 0) return 0.f;
+  const int row = J.trans ? k : n;
+  const int col = J.coff + (J.trans ? n : k);
+  const float* base = row < J.split ? J.W + (int64_t)row * J.ld : J.W2 + (int64_t)(row - J.split) * J.ld;
+  return base[col];
+}
+
+// bf16 image: element (ob, ib, s, lane) = 8 bf16 W[out(ob, lane&31)][in(ib, 8s + j, lane>>5)], RNE
+__device__ void pack_bf16(const PackJob& J) {
+  const int64_t total = (int64_t)J.NBO * J.NBI * 2 * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    int64_t rest = i >> 6;
+    const int s = (int)(rest & 1);
+    rest >>= 1;
+    const int ib = J.ibmajor ? (int)(rest / J.NBO) : (int)(rest % J.NBI);
+    const int ob = J.ibmajor ? (int)(rest % J.NBO) : (int)(rest / J.NBI);
+    int q, hh;
+    row_to_pos(lane & 31, q, hh);
+    const int n = map_index(J.out, ob, q, hh);
+    typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)pack_src(J, n, map_index(J.in, ib, 8 * s + j, lane >> 5));
+    J.dst[i] = __builtin_bit_cast(float4, v);
+  }
+}
+
 __global__ void k_pack_matrix(const PackJob* __restrict__ jobs) {
   const PackJob J = jobs[blockIdx.y];
+  if (J.bf16) {
+    pack_bf16(J);
+    return;
+  }
   const int64_t total = (int64_t)J.NBO * J.NBI * 4 * 64;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(i & 63);

@@ -18,10 +18,11 @@ namespace spp {
 constexpr float kLog2 = 0.69314718055994530942f;
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // math.log(math.sqrt(2*pi))
 
-template <int OB_, int AOUT_, int AC_, bool ACMC_>
+template <int OB_, int AOUT_, int AC_, bool ACMC_, bool BF_ = false>
 struct Cfg {
   static constexpr int OB = OB_, AOUT = AOUT_, AC = AC_;
   static constexpr bool ACMC = ACMC_;
+  static constexpr bool BF = BF_;  // bf16 MFMA MLP layers (fp32 accumulation, epilogues and targets)
   static constexpr int NB_OB = blocks_of(OB);
   static constexpr int NB_AOUT = blocks_of(AOUT);
   static constexpr int NB_H2 = blocks_of(2 * AOUT);      // heads output blocks (natural rows mu | logsig)
@@ -185,7 +186,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
     f32x16 x[C::NB_OB];
     gm_load<C::NB_OB>(x, X, xbytes, C::OB, L.ld4, L.vo);
     const rsrc_t hr = rsrc(H1g);
-    dense<C::NB_OB, C::RV_X>(A.W1, 8, x, L.tbl + A.tb1, [&](int ob, const f32x16& acc) {
+    dense<C::NB_OB, C::RV_X, C::BF>(A.W1, 8, x, L.tbl + A.tb1, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -201,7 +202,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
   SPP_TP(1);
   {
     const rsrc_t hr = rsrc(H2g);
-    dense_lds<8>(A.W2, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
+    dense_lds<8, C::BF>(A.W2, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -216,7 +217,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
   }
   SPP_TP(2);
   {
-    dense_lds<NBH>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
+    dense_lds<NBH, C::BF>(A.Wh, L.img, L.tbl + A.tbh, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
@@ -234,7 +235,7 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
                                             float* Z1g, float* Z2g, float* T3g) {
   float* small = L.sl - L.h4 * 32 - L.s;
   const rsrc_t z1r = rsrc(Z1g), z2r = rsrc(Z2g), t3r = rsrc(T3g);
-  dense<C::NB_ACMIN, C::RV_ACMIN>(p.acm.W1, 2, xin, L.tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
+  dense<C::NB_ACMIN, C::RV_ACMIN, C::BF>(p.acm.W1, 2, xin, L.tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ur = 32 * ob + ru(q);
@@ -245,7 +246,7 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
   });
   f32x16 z1[2];
   lds_load<2>(z1, small);
-  dense<2, C::RV_Z1>(p.acm.W2, 1, z1, L.tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
+  dense<2, C::RV_Z1, C::BF>(p.acm.W2, 1, z1, L.tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = tanhf(acc[q]);
@@ -255,7 +256,7 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
   });
   f32x16 z2[1];
   lds_load<1>(z2, small);
-  dense<1, C::RV_Z2>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
+  dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int u = ru(q) + L.h4;
@@ -275,7 +276,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
                                                 float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
                                                 uint64_t& m2lo, uint64_t& m2hi) {
   const rsrc_t h1r = rsrc(H1g), h2r = rsrc(H2g);
-  dense<C::NB_CIN, C::RV_CIN>(Q.W1, 8, xin, L.tbl + Q.tb1, [&](int ob, const f32x16& acc) {
+  dense<C::NB_CIN, C::RV_CIN, C::BF>(Q.W1, 8, xin, L.tbl + Q.tb1, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -290,7 +291,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
   SPP_TP(R);
   float qp = 0.f;
   const float* w3 = L.tbl + Q.tw3;
-  dense_lds<8>(Q.W2, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
+  dense_lds<8, C::BF>(Q.W2, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       SPP_TP(13);
       // delta1 = (W2^T delta2) * relu'(h1)
       const rsrc_t d1r = rsrc(p.D1[i]);
-      dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<8, C::BF>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2)
           fm_st(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
@@ -505,11 +506,11 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         for (int q = 0; q < 16; ++q)
           L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tval(w3, ob, q, L.h4) : 0.f;
       }
-      dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<8, C::BF>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
       });
-      dense_lds<C::NB_CA>(Q.W1Ta, big, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<C::NB_CA, C::BF>(Q.W1Ta, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int ib = 0; ib < C::NB_CA; ++ib)
           if (ib == ob) dca[ib] += acc;
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         }
         dp3[0][q] = v;
       }
-      dense<1, C::RV_AC>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
+      dense<1, C::RV_AC, C::BF>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const float zz = fm_ld(rsrc(z.Z2), ru(q), L.ld4, L.vo);
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       });
       f32x16 dp2[1];
       lds_load<1>(dp2, small);
-      dense<1, C::RV_Z2>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
+      dense<1, C::RV_Z2, C::BF>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int ur = 32 * ob + ru(q);
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       });
       f32x16 dp1[2];
       lds_load<2>(dp1, small);
-      dense<2, C::RV_Z1>(p.acm.W1Ta, C::NB_AOUT, dp1, nullptr, [&](int ob, const f32x16& acc) {
+      dense<2, C::RV_Z1, C::BF>(p.acm.W1Ta, C::NB_AOUT, dp1, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int ur = 32 * ob + ru(q);
@@ -614,7 +615,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         hd[ib][r + 8] = gls;
       }
     // ---- dh2 = Wh^T dheads * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
-    dense<C::NB_PAIR, C::RV_PAIR>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
+    dense<C::NB_PAIR, C::RV_PAIR, C::BF>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       }
     });
     {
-      dense_lds<8>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds<8, C::BF>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q)
           fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
@@ -748,7 +749,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
         xin[ib][r] = v;
         if (u < IN) fm_st(rsrc(g.XT), ur, L.ld4, L.vo, v);
       }
-    dense<NB_IN, RV_IN>(p.acm.W1, 2, xin, tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
+    dense<NB_IN, RV_IN, C::BF>(p.acm.W1, 2, xin, tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
@@ -759,7 +760,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     });
     f32x16 z1[2];
     lds_load<2>(z1, small);
-    dense<2, C::RV_Z1>(p.acm.W2, 1, z1, tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
+    dense<2, C::RV_Z1, C::BF>(p.acm.W2, 1, z1, tbl + p.acm.tb2, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float v = tanhf(acc[q]);
@@ -772,7 +773,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     float lsum = 0.f;
     f32x16 p3[1];
     const float sc = 2.f / ((float)g.B * (float)C::AC);
-    dense<1, C::RV_Z2>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
+    dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int u = ru(q) + L.h4;
@@ -788,7 +789,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
         if (u < C::AC) fm_st(rsrc(g.P3), ru(q), L.ld4, L.vo, v);
       }
     });
-    dense<1, C::RV_AC>(p.acm.W3T, 1, p3, nullptr, [&](int ob, const f32x16& acc) {
+    dense<1, C::RV_AC, C::BF>(p.acm.W3T, 1, p3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float zz = z2[0][q];
@@ -799,7 +800,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     });
     f32x16 p2[1];
     lds_load<1>(p2, small);
-    dense<1, C::RV_Z2>(p.acm.W2T, 2, p2, nullptr, [&](int ob, const f32x16& acc) {
+    dense<1, C::RV_Z2, C::BF>(p.acm.W2T, 2, p2, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);

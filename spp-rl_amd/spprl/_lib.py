@@ -30,7 +30,8 @@ class AgentConfig(ctypes.Structure):
     _fields_ = [("algo", c_int), ("ob", c_int), ("aout", c_int), ("ac", c_int), ("acm_critic", c_int),
                 ("min_max_denormalize", c_int), ("norm_closs", c_int), ("custom_loss", c_float),
                 ("gamma", c_float), ("tau", c_float), ("actor_lr", c_float), ("critic_lr", c_float),
-                ("alpha_lr", c_float), ("acm_lr", c_float), ("target_entropy", c_float), ("max_batch", c_int)]
+                ("alpha_lr", c_float), ("acm_lr", c_float), ("target_entropy", c_float), ("max_batch", c_int),
+                ("mlp_bf16", c_int)]
 
 
 class OnPolicyConfig(ctypes.Structure):

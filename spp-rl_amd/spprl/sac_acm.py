@@ -31,7 +31,7 @@ class SAC_AcM(OffPolicyLoop):
                  acm_lr=config.ACM_LR, acm_critic=config.ACM_CRITIC, custom_loss=0.0, norm_closs=config.NORM_CLOSS,
                  min_max_denormalize=config.MIN_MAX_DENORMALIZE, denormalize_actor_out=config.DENORMALIZE_ACTOR_OUT,
                  acm_ob_idx=None, obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None,
-                 seed=None, **unused):
+                 seed=None, mlp_bf16=False, **unused):
         _lib.load()
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
         self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
@@ -66,7 +66,8 @@ class SAC_AcM(OffPolicyLoop):
                         _lib.SPP_NET_CRITIC2_TARG: nets.critic_layout(cin), _lib.SPP_NET_ACM: nets.acm_layout(2 * ob, ac)}
         cfg = _lib.AgentConfig(_lib.SPP_ALGO_SAC_ACM, ob, aout, ac, int(self.acm_critic), int(self.min_max_denormalize),
                                int(self.norm_closs), self.custom_loss, gamma, self.tau, actor_lr, critic_lr, alpha_lr,
-                               acm_lr, self.target_entropy, self.max_batch)
+                               acm_lr, self.target_entropy, self.max_batch, int(bool(mlp_bf16)))
+        self.mlp_bf16 = bool(mlp_bf16)  # bf16 MFMA MLP layers, fp32 everything else (BASELINE configs[4])
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = ctypes.c_void_p()
         call("sppAgentCreate", ctypes.byref(h), ctypes.byref(cfg), dev)

@@ -397,3 +397,43 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     steps = np.zeros(4, np.int64)
     _lib.call("sppAgentGetSteps", ag._h, steps.ctypes.data_as(__import__("ctypes").c_void_p))
     assert steps[3] == K
+
+
+@pytest.mark.parametrize("env_name,ob,ac", [("Hopper-v2", 11, 3), ("Ant-v2", 111, 8)])
+def test_sac_acm_update_bf16_mlp_within_bf16_tolerance(env_name, ob, ac):
+    """mlp_bf16 (BASELINE configs[4]: bf16 MFMA MLP + fp32 targets): one SAC_AcM update against the
+    fp32 oracle.  Tolerance stated for bf16 operands (8-bit mantissa, fp32 accumulation): losses
+    rtol 3e-2, per-network gradient relative error < 6e-2; a wrong operand layout gives O(1)."""
+    from oracle.nets import Norm
+
+    B = 512
+    rng = np.random.RandomState(1)
+    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
+                       denormalize_actor_out=True, gamma=0.99, max_batch=B, buffer_size=128, device=DEV, seed=0,
+                       mlp_bf16=True)
+    names = {"actor": _lib.SPP_NET_ACTOR, "critic_1": _lib.SPP_NET_CRITIC1, "critic_2": _lib.SPP_NET_CRITIC2,
+             "critic_1_targ": _lib.SPP_NET_CRITIC1_TARG, "critic_2_targ": _lib.SPP_NET_CRITIC2_TARG,
+             "acm": _lib.SPP_NET_ACM}
+    params = {k: {n: v.numpy() for n, v in ag.net_state(net).items()} for k, net in names.items()}
+    lo = -rng.uniform(0.5, 2, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2, ob).astype(np.float32)
+    rb = ag.replay_buffer
+    rb.min_obs.copy_(torch.from_numpy(lo))
+    rb.max_obs.copy_(torch.from_numpy(hi))
+    rb._have_minmax = True
+    batch = (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
+             rng.uniform(-1, 1, (B, ob)).astype(np.float32), rng.randn(B).astype(np.float32),
+             (rng.rand(B) < 0.1).astype(np.int8), rng.uniform(-1, 1, (B, ac)).astype(np.float32))
+    e1, e2 = rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32)
+    ag.update(*batch, eps_next=e1, eps_cur=e2)
+    torch.cuda.synchronize()
+    norm = Norm(True, torch.from_numpy(lo), torch.from_numpy(hi))
+    o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm, actor_lim=1.0,
+                     acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params)
+    ol = o.update(*batch, e1, e2)
+    for k in ("critic_1", "critic_2", "actor"):
+        err = relerr(ag.grads[names[k]].cpu().numpy(), o.last["grads"][k])
+        assert err < 6e-2, (k, err)
+    gl = ag.loss
+    for k in ("critic_1", "critic_2", "actor"):
+        assert abs(gl[k] - ol[k]) <= 3e-2 * abs(ol[k]) + 1e-3, (k, gl[k], ol[k])

@@ -319,29 +319,22 @@ static void stats_pass1(sppReplayHandle h, uint32_t* hist, const float* pivot, h
   hipLaunchKernelGGL(k_stats_p1, dim3(kStatsBlocks), dim3(256), lds1, st, h->d, h->len, hist, h->st_part, pivot);
 }
 
-// byte pass p (0-based) of the per-group radix select: (group col0, shift)
-static void stats_pass_coords(int ob, int p, int* col0, int* nc, int* shift) {
-  const int G = std::min(ob, 32);
-  *col0 = (p / 3) * G;
-  *nc = std::min(G, ob - *col0);
-  *shift = 16 - 8 * (p % 3);
-}
+// digit pass p (0-based) after the top byte: 6-bit digits at bits 18, 12, 6, 0, all columns
+constexpr int kStatsPasses = 24 / kStatsDigit;
+static int stats_shift(int p) { return 24 - kStatsDigit * (p + 1); }
 
 static void stats_pk(sppReplayHandle h, int p, uint32_t* hist, hipStream_t st) {
-  int col0, nc, shift;
-  stats_pass_coords(h->d.ob, p, &col0, &nc, &shift);
-  const size_t ldsk = sizeof(uint32_t) * nc * 4 * 256;
-  const int resident = std::max(1, std::min(8, (int)((160 * 1024) / ldsk)));  // blocks per CU by LDS
-  hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(256), ldsk, st, h->d, h->len, col0, nc, shift,
-                     (const uint32_t*)h->st_state, hist);
+  const size_t ldsk = sizeof(uint32_t) * h->d.ob * 4 * kStatsBins;
+  const int resident = std::max(1, std::min(2, (int)((160 * 1024) / ldsk)));  // 1024-thread blocks per CU
+  hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(kStatsPkThreads), ldsk, st, h->d, h->len,
+                     stats_shift(p), (const uint32_t*)h->st_state, hist);
 }
 
 static void stats_sel(sppReplayHandle h, int p, uint32_t* hist, int64_t n, float* max_obs, float* min_obs,
                       int first_update, hipStream_t st) {
-  int col0, nc, shift;
-  stats_pass_coords(h->d.ob, p, &col0, &nc, &shift);
-  hipLaunchKernelGGL(k_stats_sel, dim3(nc), dim3(256), 0, st, hist, kStatsBlocks, h->d.ob, col0, nc, shift, 0,
-                     (const double*)nullptr, n, h->st_state, h->st_mean, max_obs, min_obs, first_update);
+  hipLaunchKernelGGL(k_stats_sel, dim3(h->d.ob), dim3(256), 0, st, hist, kStatsBlocks, h->d.ob, 0, h->d.ob,
+                     stats_shift(p), 0, (const double*)nullptr, n, h->st_state, h->st_mean, max_obs, min_obs,
+                     first_update);
 }
 
 sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
@@ -360,7 +353,7 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
                      (const double*)h->st_part, len, h->st_state, h->st_mean, max_obs, min_obs, first_update);
   hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std,
                      (const float*)nullptr);
-  const int npass = 3 * ((ob + std::min(ob, 32) - 1) / std::min(ob, 32));
+  const int npass = kStatsPasses;
   for (int p = 0; p < npass; ++p) {
     stats_pk(h, p, h->st_hist, st);
     stats_sel(h, p, h->st_hist, len, max_obs, min_obs, first_update, st);
@@ -387,7 +380,7 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot, d
   sppStatus s = stats_alloc(h);
   if (s) return s;
   hipStream_t st = S(stream);
-  const int npass = 3 * ((ob + std::min(ob, 32) - 1) / std::min(ob, 32));
+  const int npass = kStatsPasses;
   SPP_REQUIRE(step <= npass + 1, SPP_E_INVALID_ARG, "obs_stats_dp: step %d > %d", step, npass + 1);
   *done = 0;
   if (step == 0) {  // local pass 1 -> sums [ob][2] about the shared pivot, top-byte histogram

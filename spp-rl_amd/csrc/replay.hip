@@ -225,46 +225,53 @@ __global__ __launch_bounds__(256) void k_stats_p1(ReplayDev r, int64_t len, uint
   }
 }
 
-// Passes 2-4 for columns [col0, col0 + ncols): per-rank histograms of byte `shift`.
-__global__ __launch_bounds__(256) void k_stats_pk(ReplayDev r, int64_t len, int col0, int ncols, int shift,
-                                                  const uint32_t* __restrict__ state, uint32_t* __restrict__ ghist) {
-  extern __shared__ uint32_t shk[];  // [ncols][4][256]
+// Passes 2-5 (k_stats_pk): per-rank histograms of the next 6-bit digit (bits
+// [shift, shift+6), shift = 18, 12, 6, 0) among the rows matching each rank's prefix,
+// all columns in one read of the data: LDS [ob][4][64] (<= 128 KiB for ob <= 128).
+// 1024 threads (64 row lanes x 16 column lanes) keep enough loads in flight per CU.
+constexpr int kStatsDigit = 6;
+constexpr int kStatsBins = 1 << kStatsDigit;
+constexpr int kStatsPkThreads = 1024;
+__global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64_t len, int shift,
+                                                              const uint32_t* __restrict__ state,
+                                                              uint32_t* __restrict__ ghist) {
+  extern __shared__ uint32_t shk[];  // [ob][4][kStatsBins]
   const int ob = r.ob;
-  const int nb = ncols * 4 * 256;
+  const int nb = ob * 4 * kStatsBins;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) shk[i] = 0;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4, nty = blockDim.x >> 4;
   uint32_t pre[kStatsColsPerThread][4], msk[kStatsColsPerThread][4];
 #pragma unroll
   for (int j = 0; j < kStatsColsPerThread; ++j)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = tx + 16 * j;
-      pre[j][q] = c < ncols ? state[((col0 + c) * 4 + q) * 3 + 0] : 0u;
-      msk[j][q] = c < ncols ? state[((col0 + c) * 4 + q) * 3 + 1] : 0u;
+      pre[j][q] = c < ob ? state[(c * 4 + q) * 3 + 0] : 0u;
+      msk[j][q] = c < ob ? state[(c * 4 + q) * 3 + 1] : 0u;
     }
   __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * 16;
-  for (int64_t i0 = (int64_t)blockIdx.x * 16 + ty; i0 < len; i0 += stride * kStatsRowsK) {
-    int64_t base[kStatsRowsK];
+  const int64_t stride = (int64_t)gridDim.x * nty;
+  for (int64_t i0 = (int64_t)blockIdx.x * nty + ty; i0 < len; i0 += stride * kStatsRows) {
+    int64_t base[kStatsRows];
 #pragma unroll
-    for (int k = 0; k < kStatsRowsK; ++k) {
+    for (int k = 0; k < kStatsRows; ++k) {
       const int64_t i = i0 + k * stride;
-      base[k] = i < len ? r.obs_idx[i] * ob + col0 : -1;
+      base[k] = i < len ? r.obs_idx[i] * ob : -1;
     }
 #pragma unroll
     for (int j = 0; j < kStatsColsPerThread; ++j) {
       const int c = tx + 16 * j;
-      if (c >= ncols) break;
-      uint32_t kk[kStatsRowsK];
+      if (c >= ob) break;
+      uint32_t kk[kStatsRows];
 #pragma unroll
-      for (int k = 0; k < kStatsRowsK; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
+      for (int k = 0; k < kStatsRows; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
 #pragma unroll
-      for (int k = 0; k < kStatsRowsK; ++k)
+      for (int k = 0; k < kStatsRows; ++k)
         if (base[k] >= 0)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             if ((kk[k] & msk[j][q]) == pre[j][q])
-              atomicAdd(&shk[(c * 4 + q) * 256 + ((kk[k] >> shift) & 255)], 1u);
+              atomicAdd(&shk[(c * 4 + q) * kStatsBins + ((kk[k] >> shift) & (kStatsBins - 1))], 1u);
     }
   }
   __syncthreads();
@@ -281,8 +288,10 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
   __shared__ uint32_t cnt[4][256];
   __shared__ double rd[2][256];
   const int c = col0 + blockIdx.x, t = threadIdx.x;
+  const int nbins = first ? 256 : kStatsBins;  // pass 1: top byte; later passes: 6-bit digits
   for (int q = 0; q < (first ? 1 : 4); ++q) {
-    const int64_t off = first ? (int64_t)c * 256 + t : ((int64_t)blockIdx.x * 4 + q) * 256 + t;
+    if (t >= nbins) break;
+    const int64_t off = first ? (int64_t)c * 256 + t : ((int64_t)blockIdx.x * 4 + q) * nbins + t;
     cnt[q][t] = ghist[off];
     ghist[off] = 0;
   }
@@ -321,8 +330,8 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
     }
     const uint32_t* h = cnt[first ? 0 : q];
     uint32_t acc = 0;
-    int bin = 255;
-    for (int d = 0; d < 256; ++d) {
+    int bin = nbins - 1;
+    for (int d = 0; d < nbins; ++d) {
       if (acc + h[d] > rank) {
         bin = d;
         break;
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
       acc += h[d];
     }
     st[0] |= (uint32_t)bin << shift;
-    st[1] |= 255u << shift;
+    st[1] |= (uint32_t)(nbins - 1) << shift;
     st[2] = rank - acc;
   }
   if (first && t == 0) {

@@ -471,6 +471,21 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     f32x16 hd[C::NB_PAIR];
     load_pair<C>(hd, big);
     const float lp = squash_write<C>(p, hd, p.EPS2, L);  // a_d -> big rows [0, AOUT)
+    // Wide heads (Ant): park mu / raw log-std in the ADH rows the heads backward overwrites
+    // (same lane, same element), instead of keeping NB_PAIR tiles live through the critics.
+    constexpr bool kParkHeads = C::NB_PAIR > 2;
+    if constexpr (kParkHeads) {
+#pragma unroll
+      for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int j0 = 16 * ib + r;
+          if (j0 + 8 * L.h < C::AOUT) {
+            fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, hd[ib][r]);
+            fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, hd[ib][r + 8]);
+          }
+        }
+    }
     // ---- critic input [s | ACM(s, a_d)] or [s | a_d]  (:67-72)
     f32x16 cin[C::NB_CIN];
     if constexpr (C::ACMC) {
@@ -577,8 +592,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         const int j = j0 + h8;
         float gmu = 0.f, gls = 0.f;
         if (j < C::AOUT) {
-          const float mu = hd[ib][r];
-          const float lsr = hd[ib][r + 8];
+          const float mu = kParkHeads ? fm_ld(rsrc(p.ADH), j0, L.ld4, L.vp) : hd[ib][r];
+          const float lsr = kParkHeads ? fm_ld(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp) : hd[ib][r + 8];
           const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
           const float sc = expf(ls);
           const float e = fm_ld(rsrc(p.EPS2), j0, L.ld4, L.vp);

@@ -225,10 +225,11 @@ sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
 /* ACM regression batch straight from the ring (rbuffer_sample_acm, replay_buffer.py:404-430 +
  * acm_cat, acm.py:260-264): x = [obs | next_obs] [B][2ob], y = acm action [B][ac]. */
 /* nsteps sequential AcM regression steps (acm.py:246-258 each: MSE + Adam at acm_lr) in ONE
- * launch: batch k = replay rows idx[k*bs .. k*bs+bs) (acm_cat of obs / next_obs, target = acm
- * action), bs <= 128.  Parameters stay in LDS, moments in registers (update_acm epochs,
- * update_acm_batches).  loss_sum += sum of the steps' batch losses.  AcM agents (SAC_AcM) only. */
-sppStatus sppAcmSgd(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int nsteps, int bs, float* loss_sum,
+ * launch: step k's batch = rows [k*bs, k*bs + bs) of x [nsteps*bs][2ob] / y [nsteps*bs][ac]
+ * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 128.  Parameters stay in
+ * LDS, moments in registers (update_acm epochs, update_acm_batches).  loss_sum += sum of the
+ * steps' batch losses.  AcM agents (SAC_AcM) only. */
+sppStatus sppAcmSgd(sppAgentHandle h, const float* x_dev, const float* y_dev, int nsteps, int bs, float* loss_sum,
                     void* stream);
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
 

@@ -1559,19 +1559,17 @@ sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
   return SPP_OK;
 }
 
-sppStatus sppAcmSgd(sppAgentHandle a, sppReplayHandle r, const int64_t* idx, int nsteps, int bs, float* loss_sum,
+sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps, int bs, float* loss_sum,
                     void* stream) {
-  SPP_REQUIRE(a && r && idx && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
+  SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
   SPP_REQUIRE(bs <= kSgdMaxBatch, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kSgdMaxBatch);
-  SPP_REQUIRE(r->d.ob == a->cfg.ob && r->d.ac == a->cfg.ac, SPP_E_SHAPE, "acm_sgd: replay dims differ");
   sppStatus s = check_ready(a);
   if (s) return s;
   if (nsteps == 0) return SPP_OK;
   const NetBufs& n = a->net[SPP_NET_ACM];
   SPP_REQUIRE(n.p && n.m && n.v, SPP_E_STATE, "acm_sgd: ACM buffers not bound");
-  AcmSgdArgs g{r->d, idx, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout,
-               loss_sum};
+  AcmSgdArgs g{x, y, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout, loss_sum};
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
   if (ob == 11 && ac == 3) hipLaunchKernelGGL((k_acm_sgd<22, 3>), dim3(1), dim3(kSgdThreads), 0, st, g);

@@ -130,7 +130,7 @@ _SIGS = {
                                 c_void_p, c_void_p]),
     "sppAdvSums": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAdvNormalizeGlobal": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
-    "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, n, bs
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -460,9 +460,14 @@ class OffPolicyLoop:
                 and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1)))
 
     def _acm_sgd(self, idx, nsteps, bs):
-        call("sppAcmSgd", self._h, self.replay_buffer._h, ptr(idx), nsteps, bs, ptr(self._acm_loss_acc),
-             stream_handle())
-        self._keep_sgd = idx
+        """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd)."""
+        n = nsteps * bs
+        st = stream_handle()
+        x = torch.empty(n, 2 * self.ob_dim, device=self.device)
+        y = torch.empty(n, self.ac_dim, device=self.device)
+        call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), n, ptr(x), ptr(y), st)
+        call("sppAcmSgd", self._h, ptr(x), ptr(y), nsteps, bs, ptr(self._acm_loss_acc), st)
+        self._keep_sgd = (idx, x, y)
 
     def update_acm_batches(self, n_batches):
         """acm.py:356-372: n batches of acm_batch_size uniform samples; loss = batch mean."""
@@ -492,7 +497,7 @@ class OffPolicyLoop:
             nb = -(-n // bs)
             if self._acm_sgd_ok(bs):  # one launch for the full batches, one for the ragged last batch
                 full = n // bs
-                self._acm_sgd(perm, full, bs)
+                self._acm_sgd(perm[:full * bs].contiguous(), full, bs)
                 if n % bs:
                     self._acm_sgd(perm[full * bs:].contiguous(), 1, n % bs)
             else:

@@ -383,7 +383,10 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     K = 6
     idx = torch.from_numpy(np.random.RandomState(11).randint(0, 2000, K * bs)).to(DEV)
     loss = torch.zeros(1, device=DEV)
-    _lib.call("sppAcmSgd", ag._h, rb._h, _lib.ptr(idx), K, bs, _lib.ptr(loss), _lib.stream_handle())
+    xg = torch.empty(K * bs, 2 * ob, device=DEV)
+    yg = torch.empty(K * bs, ac, device=DEV)
+    _lib.call("sppReplayGatherAcm", rb._h, _lib.ptr(idx), K * bs, _lib.ptr(xg), _lib.ptr(yg), _lib.stream_handle())
+    _lib.call("sppAcmSgd", ag._h, _lib.ptr(xg), _lib.ptr(yg), K, bs, _lib.ptr(loss), _lib.stream_handle())
     ol = 0.0
     for k in range(K):
         obs, nobs, _, _, _, acm = rb.gather(idx[k * bs:(k + 1) * bs])

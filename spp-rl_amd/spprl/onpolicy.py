@@ -161,9 +161,12 @@ class OnPolicyNets:
                 break
             perm = torch.randperm(N, generator=generator).to(self.device)
             mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
+            # one permuted copy per epoch: every minibatch is then a contiguous slice
+            o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]
+            n_p = nxt[perm] if nxt is not None else None
             for s in range(0, N, mb):
-                j = perm[s:s + mb]
-                out = self.actor_step(obs[j], actions[j], logprobs[j], adv[j], nxt[j] if nxt is not None else None)
+                e = s + mb
+                out = self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None)
                 sums += out
             kl = float(out[1].item())  # KL of the epoch's last minibatch (ppo.py:188)
         self.loss.update(actor=float(sums[0]) / (i + 1), entropy=float(sums[3]) / (i + 1), kl=kl)

@@ -313,7 +313,15 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
                                               const float* __restrict__ EPS, const Lane& L) {
   float lp = 0.f, corr = 0.f;
   const int h8 = 8 * L.h;
-  const rsrc_t er = rsrc(EPS);
+  // all eps reads first (one latency for the block, not one per output).  The loads may be
+  // issued for every lane, so they go through a resource bounded to the [AOUT][Bp] array:
+  // the pairing layout's unused slots (j >= AOUT) read 0 instead of past the array.
+  const rsrc_t er = rsrc_n(EPS, C::AOUT * L.ld4);
+  float ev[C::NB_PAIR][8];
+#pragma unroll
+  for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) ev[ib][r] = fm_ldb(er, 16 * ib + r, L.ld4, L.vp);
 #pragma unroll
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
@@ -324,7 +332,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         const float mu = hd[ib][r];
         const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
         const float sc = expf(ls);
-        const float e = fm_ld(er, j0, L.ld4, L.vp);
+        const float e = ev[ib][r];
         const float u = fadd_rn(mu, fmul_rn(e, sc));
         const float d = fsub_rn(u, mu);
         const float var = fmul_rn(sc, sc);

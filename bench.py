@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="concurrent 1-thread oracle processes for the CPU baseline (reference N_CORES)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -252,6 +254,28 @@ def bench_ppo(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def _cpu_worker(args):
+    name, seconds = args
+    return cpu_baseline(CONFIGS[name], seconds)
+
+
+def cpu_baseline_pool(name, seconds, procs):
+    """The reference's N_CORES layout (train/spp_*.py: a multiprocessing pool of independent
+    1-thread runs, evals.py:22-26): `procs` concurrent oracle runs on the host cores; the
+    aggregate is the sum of the per-process env-steps/s."""
+    import multiprocessing as mp
+
+    if procs <= 1:
+        return cpu_baseline(CONFIGS[name], seconds)
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(name, seconds)] * procs)
+    vals = [r["value"] for r in res]
+    out = dict(res[0])
+    out.update(value=round(sum(vals), 2), cores=procs, per_core=round(sum(vals) / procs, 2),
+               sample="%d concurrent 1-thread processes, each: %s" % (procs, res[0]["sample"]))
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -395,7 +419,7 @@ def main():
         dist.all_gather(allc, chk)
         result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline_pool(args.config, args.cpu_seconds, args.cpu_procs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

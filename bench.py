@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+    ap.add_argument("--cpu-procs", type=int, default=min(8, os.cpu_count() or 1),
                     help="concurrent 1-thread oracle processes for the CPU baseline (reference N_CORES)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -267,8 +267,20 @@ def cpu_baseline_pool(name, seconds, procs):
 
     if procs <= 1:
         return cpu_baseline(CONFIGS[name], seconds)
-    with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(name, seconds)] * procs)
+    # the workers are CPU-only: hide the GPUs from them (a process that loads the HIP runtime
+    # may count as a GPU user; the box allows 16 per job)
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    for k in saved:
+        os.environ[k] = "-1"
+    try:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, [(name, seconds)] * procs)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     vals = [r["value"] for r in res]
     out = dict(res[0])
     out.update(value=round(sum(vals), 2), cores=procs, per_core=round(sum(vals) / procs, 2),

@@ -68,10 +68,11 @@ def _compile(src, verbose):
     return obj
 
 
-def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None):
+def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, nodense=False):
     if prof:  # region-timing variant (never the default library): single TU
         out = os.path.join(HERE, "spprl", "libspprl_prof.so")
-        extra = ["-DSPP_ONLY_HOPPER"] if hopper_only else []
+        extra = (["-DSPP_ONLY_HOPPER"] if hopper_only else []) + (["-DSPP_PROF_NODENSE"] if nodense else []) + (
+            ["-DSPP_PROF_DRAIN"] if "--drain" in sys.argv else [])
         cmd = [HIPCC] + FLAGS + ["-shared", "-DSPP_PROF", "-DSPP_SINGLE_TU"] + extra + [
             "-o", out, os.path.join(CSRC, "api.hip")]
         subprocess.check_call(cmd)
@@ -98,4 +99,5 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, prof="--prof" in sys.argv, hopper_only="--hopper-only" in sys.argv)
+    build(force="--force" in sys.argv, prof="--prof" in sys.argv, hopper_only="--hopper-only" in sys.argv,
+          nodense="--nodense" in sys.argv)

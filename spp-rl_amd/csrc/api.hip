@@ -1630,7 +1630,14 @@ sppStatus sppDebugDense(const float* x, const float* W, const float* b, float* y
   SPP_CHECK_HIP(hipMemcpy(dj, &pj, sizeof(pj), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_pack_matrix, dim3(16, 1), dim3(256), 0, st, (const PackJob*)dj);
   const dim3 grid(cdiv(B, 32));
-  if (NBI < 8) {
+  const int kq = regs_valid(K, 0) / 4;  // quads of block 0 that carry units
+  if (NBI == 1 && kq < 4) {
+    switch (kq) {
+#define SPP_DD(n) case n: hipLaunchKernelGGL((k_debug_dense<1, 1, n>), grid, dim3(64), 0, st, (const float4*)wf, b, x, y, B, K, N, act); break;
+      SPP_DD(1) SPP_DD(2) SPP_DD(3)
+#undef SPP_DD
+    }
+  } else if (NBI < 8) {
     switch (NBI) {
 #define SPP_DD(n) case n: hipLaunchKernelGGL((k_debug_dense<n, 1>), grid, dim3(64), 0, st, (const float4*)wf, b, x, y, B, K, N, act); break;
       SPP_DD(1) SPP_DD(2) SPP_DD(3) SPP_DD(4) SPP_DD(5) SPP_DD(6) SPP_DD(7)

@@ -11,7 +11,7 @@
 // consecutive MFMA k-steps for both A and X (same sample<->k map on both
 // sides).  Each lane streams its 4 A rows and 4 X rows straight from HBM
 // through an R-deep register ring (loads for step t+R-1 issued before step
-// t's MFMAs).  Partial slabs are summed in a fixed order by k_dw_reduce
+// t's MFMAs; R from dw_ring, deeper for thin tile sets).  Partial slabs are summed in a fixed order by k_dw_reduce
 // (deterministic, no atomics).
 #include "common.h"
 #include "internal.h"
@@ -19,7 +19,18 @@
 namespace spp {
 
 constexpr int kDwThreads = 256;
-constexpr int kDwRing = 2;  // steps (16 samples each) in flight
+
+// Steps (16 samples each) in flight for an NI x NJ tile set: the R-1 steps ahead carry
+// NI*NJ*8 MFMAs (64 cycles) each, enough to cover >= ~8K cycles of HBM latency, within
+// ~200 VGPRs of operand ring.  4x4: 2 (one 8K-cycle step ahead); thin tiles go deeper.
+template <int NI, int NJ>
+constexpr int dw_ring() {
+  constexpr int mf = NI * NJ * 8;
+  constexpr int want = 1 + (128 + mf - 1) / mf;
+  constexpr int cap = 200 / ((NI + NJ) * 8);
+  constexpr int r = want < cap ? want : cap;
+  return r < 2 ? 2 : (r > 8 ? 8 : r);
+}
 
 // One step = 16 samples: lane half h takes samples [16t + 8h, +8) of each of
 // its rows as two adjacent float4 (a full 64 B run per row and half), i.e. 8
@@ -36,7 +47,8 @@ __device__ __forceinline__ bf16x8 pack8(const float4& a, const float4& b) {
 template <int NI, int NJ, bool DB, bool BF = false>
 __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
                                         f32x16 (&acc)[4][4], float (&bs)[4]) {
-  float4 ra[kDwRing][NI][2], rx[kDwRing][NJ][2];
+  constexpr int R = dw_ring<NI, NJ>();
+  float4 ra[R][NI][2], rx[R][NJ][2];
   const float* a0[NI];
   const float* x0[NJ];
   static_for<0, NI>([&](auto I) { a0[I] = ap[I]; });
@@ -52,13 +64,16 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
       rx[sl][J][1] = *reinterpret_cast<const float4*>(x0[J] + 16 * t + 4);
     });
   };
-  static_for<0, kDwRing - 1>([&](auto S) { load(S, (int)S); });
+  static_for<0, R - 1>([&](auto S) {
+    if ((int)S < nsteps) load(S, (int)S);
+  });
 #pragma unroll 1
-  for (int t0 = 0; t0 < nsteps; t0 += kDwRing) {
-    static_for<0, kDwRing>([&](auto U) {
+  for (int t0 = 0; t0 < nsteps; t0 += R) {
+    static_for<0, R>([&](auto U) {
       constexpr int u = U;
-      constexpr int sn = (u + kDwRing - 1) % kDwRing;
-      const int tn = t0 + u + kDwRing - 1;
+      constexpr int sn = (u + R - 1) % R;
+      if (t0 + u >= nsteps) return;
+      const int tn = t0 + u + R - 1;
       if (tn < nsteps) load(IC<sn>{}, tn);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (BF) {
@@ -116,12 +131,12 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   }
   int b_begin = split * J.split_len;
   int b_end = min(b_begin + J.split_len, J.Bp);
-  if (wsp) {  // parts of whole 32-sample pairs of steps (dw_tile consumes steps in pairs)
+  if (wsp) {  // parts of whole 32-sample units
     const int q = (((b_end - b_begin + J.wsplit - 1) / J.wsplit) + 31) & ~31;
     b_begin = min(b_begin + part * q, b_end);
     b_end = min(b_begin + q, b_end);
   }
-  const int nsteps = (b_end - b_begin) / 16;  // even: ranges are multiples of 32 samples
+  const int nsteps = (b_end - b_begin) / 16;  // ranges are multiples of 32 samples
   const int ni = min(4, max(0, (N + 31) / 32 - nb0));
   const int nj = min(4, max(0, (K + 31) / 32 - kb0));
   if (ni == 0 || nj == 0) return;

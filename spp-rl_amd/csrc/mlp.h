@@ -19,10 +19,16 @@ namespace spp {
 
 // Region timing of the phase kernels (profiling builds only, -DSPP_PROF): each
 // wave accumulates s_memtime deltas per region in LDS, flushed to g_tprof.
+// sched_barrier keeps the scheduler from moving a region's code across its marker.
 #ifdef SPP_PROF
 __device__ unsigned long long g_tprof[64];
 __shared__ unsigned long long s_tprof[4][32];
 __shared__ unsigned long long s_tlast[4];
+#ifdef SPP_PROF_DRAIN  // charge each region with the memory traffic it left in flight
+#define SPP_TP_DRAIN() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else
+#define SPP_TP_DRAIN()
+#endif
 #define SPP_TP_INIT()                                                            \
   {                                                                              \
     const int w_ = threadIdx.x >> 6;                                             \
@@ -31,7 +37,10 @@ __shared__ unsigned long long s_tlast[4];
   }
 #define SPP_TP(k)                                                                \
   {                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    SPP_TP_DRAIN();                                                              \
     const unsigned long long t_ = clock64();                                     \
+    __builtin_amdgcn_sched_barrier(0);                                           \
     const int w_ = threadIdx.x >> 6;                                             \
     if ((threadIdx.x & 63) == 0 && w_ < 4) {                                     \
       s_tprof[w_][k] += t_ - s_tlast[w_];                                        \
@@ -47,6 +56,13 @@ __shared__ unsigned long long s_tlast[4];
 #define SPP_TP_INIT()
 #define SPP_TP(k)
 #define SPP_TP_FLUSH()
+#endif
+// markers inside the dense layers (off with -DSPP_PROF_NODENSE: then a kernel's
+// top-level regions include their layers)
+#if defined(SPP_PROF) && !defined(SPP_PROF_NODENSE)
+#define SPP_TPD(k) SPP_TP(k)
+#else
+#define SPP_TPD(k)
 #endif
 
 // ---------------------------------------------------------------- layout maps
@@ -255,7 +271,7 @@ __device__ __forceinline__ void dense_impl(const float4* __restrict__ Wf, int NB
     });
     return acc;
   };
-  SPP_TP(23);
+  SPP_TPD(23);
   f32x16 prev = chain(0);
 #pragma unroll 1
   for (int ob = 1; ob < NBO; ++ob) {
@@ -263,9 +279,9 @@ __device__ __forceinline__ void dense_impl(const float4* __restrict__ Wf, int NB
     epi(ob - 1, prev);
     prev = acc;
   }
-  SPP_TP(24);
+  SPP_TPD(24);
   epi(NBO - 1, prev);
-  SPP_TP(25);
+  SPP_TPD(25);
 }
 
 constexpr int cgcd(int a, int b) { return b ? cgcd(b, a % b) : a; }
@@ -333,7 +349,7 @@ __device__ __forceinline__ void dense_lds_impl(const float4* __restrict__ Wf, co
       acc[ob] = mfma(ring[s][J].w, xin[kb][4 * rq + 3], acc[ob]);
     });
   };
-  SPP_TP(20);
+  SPP_TPD(20);
 #pragma unroll 1
   for (int it = 0; it < NIT - 1; ++it) {
     f32x16 xnx[IBU];
@@ -349,9 +365,9 @@ __device__ __forceinline__ void dense_lds_impl(const float4* __restrict__ Wf, co
     constexpr int u = UC;
     if constexpr (u / NCI == IBU - 1 && u % NCI >= 1) epi(IC<u % NCI - 1>{}, acc[u % NCI - 1]);
   });
-  SPP_TP(21);
+  SPP_TPD(21);
   epi(IC<NBO - 1>{}, acc[NBO - 1]);
-  SPP_TP(22);
+  SPP_TPD(22);
 }
 
 // ---------------------------------------------------------------- bf16 MFMA layers

@@ -461,6 +461,7 @@ template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratch z) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  SPP_TP_INIT();
   load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
@@ -475,10 +476,13 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
     // ---- a, logpi = actor(s)  (sac_acm.py:137)
     uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
+    SPP_TP(26);
     actor_trunk<C, true>(p.actor, p.S, C::OB * L.ld4, L, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
+    SPP_TP(27);  // actor trunk
     f32x16 hd[C::NB_PAIR];
     load_pair<C>(hd, big);
     const float lp = squash_write<C>(p, hd, p.EPS2, L);  // a_d -> big rows [0, AOUT)
+    SPP_TP(28);  // squash
     // Wide heads (Ant): park mu / raw log-std in the ADH rows the heads backward overwrites
     // (same lane, same element), instead of keeping NB_PAIR tiles live through the critics.
     constexpr bool kParkHeads = C::NB_PAIR > 2;
@@ -504,6 +508,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     } else {
       load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
     }
+    SPP_TP(29);  // ACM forward
     // ---- q = min(Q1, Q2)(s, c)  (:73-75), masks kept for the backward
     uint64_t ma0 = 0, ma1 = 0, ma2 = 0, ma3 = 0, mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0;
     const float q1 = critic_forward<C, false>(p.critic[0], cin, L, nullptr, nullptr, ma0, ma1, ma2, ma3);
@@ -513,6 +518,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     const float gq = valid ? -p.inv_B : 0.f;
     const float dqa = q1 < q2 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
     const float dqb = q2 < q1 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
+    SPP_TP(19);  // q min (the critic layers themselves: slots 30, 31)
     // ---- back through both critics to their action input
     f32x16 dca[C::NB_CA];
 #pragma unroll
@@ -529,16 +535,26 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         for (int q = 0; q < 16; ++q)
           L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tval(w3, ob, q, L.h4) : 0.f;
       }
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(20);  // delta staging
+#endif
       dense_lds<8, C::BF>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
       });
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(21);  // W2T
+#endif
       dense_lds<C::NB_CA, C::BF>(Q.W1Ta, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int ib = 0; ib < C::NB_CA; ++ib)
           if (ib == ob) dca[ib] += acc;
       });
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(22);  // W1Ta
+#endif
     }
+    SPP_TP(31);  // critics backward
     // ---- through the frozen ACM to d a_d  (basic_model.py:118-126 backward)
     if constexpr (C::ACMC) {
       f32x16 dp3[1];
@@ -552,6 +568,9 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         }
         dp3[0][q] = v;
       }
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(23);  // ACM bwd input
+#endif
       dense<1, C::RV_AC, C::BF>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -559,6 +578,9 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           L.sl[ru(q) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(24);  // ACM W3T
+#endif
       f32x16 dp2[1];
       lds_load<1>(dp2, small);
       dense<1, C::RV_Z2, C::BF>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
@@ -569,6 +591,9 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           L.sl[ur * 32] = acc[q] * (1.f - zz * zz);
         }
       });
+#ifdef SPP_PROF_NODENSE
+      SPP_TP(25);  // ACM W2T
+#endif
       f32x16 dp1[2];
       lds_load<2>(dp1, small);
       dense<2, C::RV_Z1, C::BF>(p.acm.W1Ta, C::NB_AOUT, dp1, nullptr, [&](int ob, const f32x16& acc) {
@@ -587,6 +612,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           if (ur + L.h4 < C::AOUT) L.bl[ur * 32] = dca[ib][q];
         }
     }
+    SPP_TP(16);  // ACM backward
     // ---- heads backward in the pairing layout (squash, denorm, custom loss, logpi)
     float sac_part = (valid && L.h == 0) ? fsub_rn(alpha * lp, qmin) : 0.f;
     float dist_part = 0.f;
@@ -637,6 +663,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         hd[ib][r] = gmu;
         hd[ib][r + 8] = gls;
       }
+    SPP_TP(17);  // heads backward
     // ---- dh2 = Wh^T dheads * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
     dense<C::NB_PAIR, C::RV_PAIR, C::BF>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
@@ -654,6 +681,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
       });
     }
+    SPP_TP(18);  // trunk backward
     const float ps = wave_sum(sac_part);
     const float pd = wave_sum(dist_part);
     const float pl = wave_sum((valid && L.h == 0) ? lp : 0.f);
@@ -663,6 +691,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       p.part[tile * kParts + 4] = pl;
     }
   }
+  SPP_TP_FLUSH();
 }
 
 // ============================================================================ rollout action
@@ -892,8 +921,9 @@ __global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint6
 // ============================================================================ debug dense
 // One layer on a [B][K] row-major batch with a natural bias b (NULL -> 0).
 // K <= 224: register-input dense (ob-major image); K == 256: dense_lds from the
-// LDS image (ib-major image), NBO compile-time.
-template <int NBI, int NBO>
+// LDS image (ib-major image), NBO compile-time.  KQ > 0 (NBI == 1): only the first
+// KQ register quads of the input block carry units, as in the 3..24-wide first layers.
+template <int NBI, int NBO, int KQ = 0>
 __global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const float* bias, const float* x, float* y,
                                                     int B, int K, int N, int act) {
   __shared__ float img[256 * 32];
@@ -924,7 +954,7 @@ __global__ __launch_bounds__(64) void k_debug_dense(const float4* Wf, const floa
   if constexpr (NBI == 8)
     dense_lds<NBO>(Wf, img, tb, epi);  // tb holds zeros without a bias
   else
-    dense<NBI, rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, tb, epi);
+    dense<NBI, KQ ? (uint64_t)KQ : rv_nat(32 * NBI, NBI)>(Wf, (N + 31) / 32, in, tb, epi);
 }
 
 }  // namespace spp

@@ -31,7 +31,7 @@ def relerr(a, b):
 
 
 # ------------------------------------------------------------------ MFMA tile layout
-@pytest.mark.parametrize("K,N,act", [(11, 256, 1), (14, 256, 1), (22, 64, 2), (256, 256, 1), (256, 22, 0),
+@pytest.mark.parametrize("K,N,act", [(11, 256, 1), (14, 256, 1), (22, 64, 2), (3, 256, 1), (3, 22, 0), (8, 64, 2), (17, 96, 1), (256, 256, 1), (256, 22, 0),
                                      (256, 1, 0), (64, 32, 2), (32, 3, 2), (111, 256, 1), (222, 64, 0)])
 def test_dense_tile_matches_torch(K, N, act):
     torch.manual_seed(K * 1000 + N)

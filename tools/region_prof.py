@@ -16,8 +16,12 @@ from spprl import _lib  # noqa: E402
 NAMES = {0: "tile start", 1: "actor L1", 2: "actor L2", 3: "actor heads", 4: "squash", 5: "ACM + target input",
          6: "targ1 L1", 7: "targ1 L2", 8: "targ2 L1", 9: "targ2 L2", 10: "y + critic input", 11: "critic L1",
          12: "critic L2", 13: "delta2 staging", 14: "critic W2T", 15: "tile end",
-         20: "dense_lds prologue", 21: "dense_lds loop", 22: "dense_lds epilogue",
-         23: "dense prologue", 24: "dense mfma", 25: "dense epilogue"}
+         20: "dense_lds prologue | A: delta staging (nodense)", 21: "dense_lds loop | A: W2T (nodense)",
+         22: "dense_lds epilogue | A: W1Ta (nodense)",
+         23: "dense prologue | A: ACM bwd input (nodense)", 24: "dense mfma | A: ACM W3T (nodense)",
+         25: "dense epilogue | A: ACM W2T (nodense)",
+         26: "A: tile start", 27: "A: actor trunk", 28: "A: squash", 29: "A: ACM fwd", 30: "A: critics fwd",
+         31: "A: critics bwd", 16: "A: ACM bwd", 17: "A: heads bwd", 18: "A: trunk bwd"}
 
 
 def main():
@@ -44,7 +48,7 @@ def main():
     t = np.array(buf[:32], np.float64)
     tiles = 3 * (B // 32)
     tot = t.sum()
-    print("critic phase, cycles per tile (%d tiles): total %.0f" % (tiles, tot / tiles))
+    print("both phases, cycles per tile (%d tiles per phase): total %.0f" % (tiles, tot / tiles))
     for k in [k for k in NAMES if t[k] > 0]:
         print("  %2d %-20s %9.0f  %5.1f%%" % (k, NAMES[k], t[k] / tiles, 100 * t[k] / tot))
 

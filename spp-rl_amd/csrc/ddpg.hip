@@ -88,36 +88,48 @@ __device__ __forceinline__ void bacm_backward(const SacArgs& p, const f32x16& dc
   float* bimg = L.img + kBacmRow * 32;
   float* bl = L.bl + kBacmRow * 32;
   const float t = *B.t;
-  const rsrc_t hr = rsrc(z.H), h1r = rsrc(z.H1), r3r = rsrc(z.R3);
+  const rsrc_t hr = rsrc(z.H), h1r = rsrc(z.H1), r3r = rsrc_n(z.R3, C::AC * L.ld4);
+  // All scratch values requested up front: a buffer load issued inside an epilogue is ordered
+  // behind the epilogue's stores (no alias proof against LDS), i.e. one round trip per element.
+  float r3v[16], t1v[16], h1v[2][16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int u = ru(q) + L.h4;
+    r3v[q] = fm_ldb(r3r, ru(q), L.ld4, L.vo);  // rows >= AC read 0
+    t1v[q] = B.t1[u < C::AC ? u : 0];
+  }
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) h1v[ob][q] = fm_ld(h1r, 32 * ob + ru(q), L.ld4, L.vo);
   f32x16 du3[1];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int u = ru(q) + L.h4;
-    float v = 0.f;
-    if (u < C::AC) {
-      const float r = fm_ld(r3r, ru(q), L.ld4, L.vo);
-      v = dc[q] * B.t1[u] * (1.f - r * r);
-    }
-    du3[0][q] = v;
+    const float r = r3v[q];
+    du3[0][q] = u < C::AC ? dc[q] * t1v[q] * (1.f - r * r) : 0.f;
   }
   // dz = (W3^T du3) * (1 - h1^2) -> BasicAcM rows
   dense<1, C::RV_AC>(B.W3T, 2, du3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int ur = 32 * ob + ru(q);
-      const float h1 = fm_ld(h1r, ur, L.ld4, L.vo);
-      bl[ur * 32] = acc[q] * (1.f - h1 * h1);
+      const float h1 = ob ? h1v[1][q] : h1v[0][q];
+      bl[(32 * ob + ru(q)) * 32] = acc[q] * (1.f - h1 * h1);
     }
   });
+  float hv[4][16];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) hv[ob][q] = fm_ld(hr, 32 * ob + ru(q), L.ld4, L.vo);
   f32x16 dz[2];
   lds_load<2>(dz, bimg);
   // du1 = (W2^T dz) * (1 - h^2) -> BIG rows [0, 128)
   dense<2, C::RV_B50>(B.W2T, 4, dz, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int ur = 32 * ob + ru(q);
-      const float h = fm_ld(hr, ur, L.ld4, L.vo);
-      L.bl[ur * 32] = acc[q] * (1.f - h * h);
+      const float h = ob == 0 ? hv[0][q] : (ob == 1 ? hv[1][q] : (ob == 2 ? hv[2][q] : hv[3][q]));
+      L.bl[(32 * ob + ru(q)) * 32] = acc[q] * (1.f - h * h);
     }
   });
   f32x16 du1[4];
@@ -299,36 +311,43 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
     float ddpg_part = (valid && L.h == 0) ? -q : 0.f;
     float dist_part = 0.f;
     const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
-    const rsrc_t s2r = rsrc(p.S2), adhr = rsrc(p.ADH);
+    // Branch-free over the units, loads through array-bounded resources (rows >= AOUT read 0),
+    // stores after the loop: per-unit branches or interleaved stores cost a round trip per unit.
+    const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4), adhr = rsrc(p.ADH);
+    const bool closs = p.custom_loss != 0.f;
 #pragma unroll
     for (int ib = 0; ib < C::NB_AOUT; ++ib)
 #pragma unroll
       for (int q2 = 0; q2 < 16; ++q2) {
         const int ur = 32 * ib + ru(q2), j = ur + L.h4;
-        float gu = 0.f;
-        if (j < C::AOUT) {
-          const float t = tanhf(u[ib][q2]);
-          const float lim = p.actor_lim[j];
-          const float a = fmul_rn(t, lim);
-          float g_ad = L.bl[ur * 32];
-          float g_a = 0.f;
-          if (p.custom_loss != 0.f) {
-            const float s2 = fm_ld(s2r, ur, L.ld4, L.vo);
-            if (p.norm_closs) {
-              const float df = fsub_rn(a, normalize(p, j, s2));
-              g_a += cl_scale * df;
-              dist_part += valid ? df * df : 0.f;
-            } else {
-              const float df = fsub_rn(denorm(p, j, a), s2);
-              g_ad += cl_scale * df;
-              dist_part += valid ? df * df : 0.f;
-            }
+        const bool ok = j < C::AOUT;
+        const int jj = ok ? j : 0;
+        const float s2 = closs ? fm_ldb(s2r, ur, L.ld4, L.vo) : 0.f;
+        const float t = tanhf(u[ib][q2]);
+        const float lim = p.actor_lim[jj];
+        const float a = fmul_rn(t, lim);
+        float g_ad = L.bl[ur * 32];
+        float g_a = 0.f;
+        if (closs) {
+          if (p.norm_closs) {
+            const float df = fsub_rn(a, normalize(p, jj, s2));
+            g_a += cl_scale * df;
+            dist_part += (valid && ok) ? df * df : 0.f;
+          } else {
+            const float df = fsub_rn(denorm(p, jj, a), s2);
+            g_ad += cl_scale * df;
+            dist_part += (valid && ok) ? df * df : 0.f;
           }
-          g_a += g_ad * denorm_scale(p, j);
-          gu = g_a * lim * (1.f - t * t);
-          fm_st(adhr, ur, L.ld4, L.vo, gu);
         }
-        u[ib][q2] = gu;
+        g_a += g_ad * denorm_scale(p, jj);
+        u[ib][q2] = ok ? g_a * lim * (1.f - t * t) : 0.f;
+      }
+#pragma unroll
+    for (int ib = 0; ib < C::NB_AOUT; ++ib)
+#pragma unroll
+      for (int q2 = 0; q2 < 16; ++q2) {
+        const int ur = 32 * ib + ru(q2);
+        if (ur + L.h4 < C::AOUT) fm_st(adhr, ur, L.ld4, L.vo, u[ib][q2]);
       }
     // ---- dh2 = fc3^T du * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
     const rsrc_t ad2r = rsrc(p.AD2), ad1r = rsrc(p.AD1);
@@ -448,9 +467,14 @@ __global__ __launch_bounds__(256, 1) void k_bacm_regress(SacArgs p, BAcmRegArgs 
       for (int r = 0; r < 16; ++r) {
         const int ur = 32 * ib + ru(r);
         const int u = ur + L.h4;
-        const float v = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
-        xin[ib][r] = v;
-        if (u < IN) fm_st(xtr, ur, L.ld4, L.vo, v);
+        xin[ib][r] = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
+      }
+#pragma unroll
+    for (int ib = 0; ib < NB_IN; ++ib)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ur = 32 * ib + ru(r);
+        if (ur + L.h4 < IN) fm_st(xtr, ur, L.ld4, L.vo, xin[ib][r]);
       }
     float* bl = L.bl + kBacmRow * 32;
     float* bimg = big + kBacmRow * 32;
@@ -493,6 +517,14 @@ __global__ __launch_bounds__(256, 1) void k_bacm_regress(SacArgs p, BAcmRegArgs 
     for (int k = 0; k < C::AC; ++k) dt1[k] = 0.f;
     f32x16 p3[1];
     const float sc = 2.f / ((float)g.B * (float)C::AC);
+    float t1v[16], yv[16];  // before the layer (loads behind the epilogue's stores serialise)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = ru(q) + L.h4;
+      const int uu = u < C::AC ? u : 0;
+      t1v[q] = B.t1[uu];
+      yv[q] = g.y[br * C::AC + uu];
+    }
     dense<2, C::RV_B50>(B.W3, 1, h1in, tbl + B.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -500,8 +532,8 @@ __global__ __launch_bounds__(256, 1) void k_bacm_regress(SacArgs p, BAcmRegArgs 
         float v = 0.f;
         if (u < C::AC && valid) {
           const float r = tanhf(acc[q]);
-          const float t1 = B.t1[u];
-          const float df = fsub_rn(fmul_rn(r, t1), g.y[br * C::AC + u]);
+          const float t1 = t1v[q];
+          const float df = fsub_rn(fmul_rn(r, t1), yv[q]);
           lsum += df * df;
           const float dout = sc * df;
 #pragma unroll
@@ -534,7 +566,7 @@ __global__ __launch_bounds__(256, 1) void k_bacm_regress(SacArgs p, BAcmRegArgs 
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
-        const float hh = fm_ld(hr, ur, L.ld4, L.vo);
+        const float hh = ob == 0 ? hin[0][q] : (ob == 1 ? hin[1][q] : (ob == 2 ? hin[2][q] : hin[3][q]));
         fm_st(p1r, ur, L.ld4, L.vo, (ur + L.h4 < 100) ? acc[q] * (1.f - hh * hh) : 0.f);
       }
     });

@@ -256,13 +256,16 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
   });
   f32x16 z2[1];
   lds_load<1>(z2, small);
+  float limv[16];  // before the layer: a load behind the epilogue's buffer stores waits per element
+#pragma unroll
+  for (int q = 0; q < 16; ++q) limv[q] = p.acm_lim[ru(q) + L.h4 < C::AC ? ru(q) + L.h4 : 0];
   dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int u = ru(q) + L.h4;
       if (u < C::AC) {
         const float t = tanhf(acc[q]);
-        L.sl[ru(q) * 32] = t * p.acm_lim[u];
+        L.sl[ru(q) * 32] = t * limv[q];
         if constexpr (ST) fm_st(t3r, ru(q), L.ld4, L.vo, t);
       }
     }
@@ -557,16 +560,41 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     SPP_TP(31);  // critics backward
     // ---- through the frozen ACM to d a_d  (basic_model.py:118-126 backward)
     if constexpr (C::ACMC) {
+      // Every scratch value of the three layers is requested up front: buffer loads cannot be
+      // moved across the epilogues' LDS stores (no alias proof), so loads issued inside an
+      // epilogue run as one round trip each.
+      // (Wide-head configs keep the per-element loads: their registers are taken.)
+      constexpr bool kPre = !kParkHeads;
+      float t3v[16], limv[16], z2v[16], z1v[2][16];
+      const rsrc_t t3r = rsrc_n(z.T3, C::AC * L.ld4);  // rows >= AC read 0
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = ru(q) + L.h4;
+        t3v[q] = fm_ldb(t3r, ru(q), L.ld4, L.vo);
+        limv[q] = p.acm_lim[u < C::AC ? u : 0];
+      }
+      if constexpr (kPre) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) z2v[q] = fm_ld(rsrc(z.Z2), ru(q), L.ld4, L.vo);
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) z1v[ob][q] = fm_ld(rsrc(z.Z1), 32 * ob + ru(q), L.ld4, L.vo);
+      }
+      auto z2at = [&](int q) {
+        if constexpr (kPre) return z2v[q];
+        else return fm_ld(rsrc(z.Z2), ru(q), L.ld4, L.vo);
+      };
+      auto z1at = [&](int ob, int q) {
+        if constexpr (kPre) return ob ? z1v[1][q] : z1v[0][q];
+        else return fm_ld(rsrc(z.Z1), 32 * ob + ru(q), L.ld4, L.vo);
+      };
       f32x16 dp3[1];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int u = ru(q) + L.h4;
-        float v = 0.f;
-        if (u < C::AC) {
-          const float t = fm_ld(rsrc(z.T3), ru(q), L.ld4, L.vo);
-          v = dca[0][q] * p.acm_lim[u] * (1.f - t * t);
-        }
-        dp3[0][q] = v;
+        const float t = t3v[q];
+        dp3[0][q] = u < C::AC ? dca[0][q] * limv[q] * (1.f - t * t) : 0.f;
       }
 #ifdef SPP_PROF_NODENSE
       SPP_TP(23);  // ACM bwd input
@@ -574,7 +602,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       dense<1, C::RV_AC, C::BF>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const float zz = fm_ld(rsrc(z.Z2), ru(q), L.ld4, L.vo);
+          const float zz = z2at(q);
           L.sl[ru(q) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
@@ -586,9 +614,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       dense<1, C::RV_Z2, C::BF>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int ur = 32 * ob + ru(q);
-          const float zz = fm_ld(rsrc(z.Z1), ur, L.ld4, L.vo);
-          L.sl[ur * 32] = acc[q] * (1.f - zz * zz);
+          const float zz = z1at(ob, q);
+          L.sl[(32 * ob + ru(q)) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
 #ifdef SPP_PROF_NODENSE
@@ -618,51 +645,115 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     float dist_part = 0.f;
     const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
     const int h8 = 8 * L.h;
+    if constexpr (kParkHeads) {
+      // wide heads: per-slot form (the branch-free form's batched loads exceed the registers)
 #pragma unroll
-    for (int ib = 0; ib < C::NB_PAIR; ++ib)
+      for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int j0 = 16 * ib + r;
-        const int j = j0 + h8;
-        float gmu = 0.f, gls = 0.f;
-        if (j < C::AOUT) {
-          const float mu = kParkHeads ? fm_ld(rsrc(p.ADH), j0, L.ld4, L.vp) : hd[ib][r];
-          const float lsr = kParkHeads ? fm_ld(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp) : hd[ib][r + 8];
+        for (int r = 0; r < 8; ++r) {
+          const int j0 = 16 * ib + r;
+          const int j = j0 + h8;
+          float gmu = 0.f, gls = 0.f;
+          if (j < C::AOUT) {
+            const float mu = fm_ld(rsrc(p.ADH), j0, L.ld4, L.vp);
+            const float lsr = fm_ld(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp);
+            const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
+            const float sc = expf(ls);
+            const float e = fm_ld(rsrc(p.EPS2), j0, L.ld4, L.vp);
+            const float u = fadd_rn(mu, fmul_rn(e, sc));
+            const float d = fsub_rn(u, mu);
+            const float t = tanhf(u);
+            const float lim = p.actor_lim[j];
+            const float a = fmul_rn(t, lim);
+            float g_ad = L.pl[j0 * 32];
+            float g_a = 0.f;
+            if (p.custom_loss != 0.f) {
+              const float s2 = fm_ld(rsrc(p.S2), j0, L.ld4, L.vp);
+              if (p.norm_closs) {
+                const float df = fsub_rn(a, normalize(p, j, s2));
+                g_a += cl_scale * df;
+                dist_part += valid ? df * df : 0.f;
+              } else {
+                const float df = fsub_rn(denorm(p, j, a), s2);
+                g_ad += cl_scale * df;
+                dist_part += valid ? df * df : 0.f;
+              }
+            }
+            g_a += g_ad * denorm_scale(p, j);
+            const float var = fmul_rn(sc, sc);
+            const float sig_m2u = 1.f / (1.f + expf(2.f * u));
+            const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
+            gmu = gu + g_lp * d / var;
+            const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
+            gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
+            fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, gmu);
+            fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, gls);
+          }
+          hd[ib][r] = gmu;
+          hd[ib][r + 8] = gls;
+        }
+    } else {
+      // Branch-free over the pairing slots: every lane loads through resources bounded to the
+      // arrays (slots j >= AOUT read 0) and computes; results of those slots are dropped.  Per-slot
+      // branches would put each load and its use in one block, i.e. one round trip per slot.
+      const rsrc_t adhr = rsrc_n(p.ADH, 2 * C::AOUT * L.ld4);
+      const rsrc_t epsr = rsrc_n(p.EPS2, C::AOUT * L.ld4);
+      const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4);
+      const bool closs = p.custom_loss != 0.f;
+  #pragma unroll
+      for (int ib = 0; ib < C::NB_PAIR; ++ib)
+  #pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int j0 = 16 * ib + r;
+          const int j = j0 + h8;
+          const bool ok = j < C::AOUT;
+          const int jj = ok ? j : 0;
+          const float mu = kParkHeads ? fm_ldb(adhr, j0, L.ld4, L.vp) : hd[ib][r];
+          const float lsr = kParkHeads ? fm_ldb(adhr, C::AOUT + j0, L.ld4, L.vp) : hd[ib][r + 8];
+          const float e = fm_ldb(epsr, j0, L.ld4, L.vp);
+          const float s2 = closs ? fm_ldb(s2r, j0, L.ld4, L.vp) : 0.f;
           const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
           const float sc = expf(ls);
-          const float e = fm_ld(rsrc(p.EPS2), j0, L.ld4, L.vp);
           const float u = fadd_rn(mu, fmul_rn(e, sc));
           const float d = fsub_rn(u, mu);
           const float t = tanhf(u);
-          const float lim = p.actor_lim[j];
+          const float lim = p.actor_lim[jj];
           const float a = fmul_rn(t, lim);
           float g_ad = L.pl[j0 * 32];  // from the critics through the ACM
           float g_a = 0.f;
-          if (p.custom_loss != 0.f) {
-            const float s2 = fm_ld(rsrc(p.S2), j0, L.ld4, L.vp);
+          if (closs) {
             if (p.norm_closs) {
-              const float df = fsub_rn(a, normalize(p, j, s2));
+              const float df = fsub_rn(a, normalize(p, jj, s2));
               g_a += cl_scale * df;
-              dist_part += valid ? df * df : 0.f;
+              dist_part += (valid && ok) ? df * df : 0.f;
             } else {
-              const float df = fsub_rn(denorm(p, j, a), s2);
+              const float df = fsub_rn(denorm(p, jj, a), s2);
               g_ad += cl_scale * df;
-              dist_part += valid ? df * df : 0.f;
+              dist_part += (valid && ok) ? df * df : 0.f;
             }
           }
-          g_a += g_ad * denorm_scale(p, j);
+          g_a += g_ad * denorm_scale(p, jj);
           const float var = fmul_rn(sc, sc);
           const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
           const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
-          gmu = gu + g_lp * d / var;
+          const float gmu = gu + g_lp * d / var;
           const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
-          gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
-          fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, gmu);
-          fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, gls);
+          const float gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
+          hd[ib][r] = ok ? gmu : 0.f;
+          hd[ib][r + 8] = ok ? gls : 0.f;
         }
-        hd[ib][r] = gmu;
-        hd[ib][r + 8] = gls;
-      }
+      // stores after all of the loop's loads (a buffer store would order every later load behind it)
+  #pragma unroll
+      for (int ib = 0; ib < C::NB_PAIR; ++ib)
+  #pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int j0 = 16 * ib + r;
+          if (j0 + h8 < C::AOUT) {
+            fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, hd[ib][r]);
+            fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, hd[ib][r + 8]);
+          }
+        }
+    }
     SPP_TP(17);  // heads backward
     // ---- dh2 = Wh^T dheads * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
     dense<C::NB_PAIR, C::RV_PAIR, C::BF>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
@@ -797,9 +888,15 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
       for (int r = 0; r < 16; ++r) {
         const int ur = 32 * ib + ru(r);
         const int u = ur + L.h4;
-        const float v = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
-        xin[ib][r] = v;
-        if (u < IN) fm_st(rsrc(g.XT), ur, L.ld4, L.vo, v);
+        xin[ib][r] = (u < IN && valid) ? g.x[br * IN + u] : 0.f;
+      }
+    // stores after all loads (a buffer store orders every later load behind it)
+#pragma unroll
+    for (int ib = 0; ib < NB_IN; ++ib)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ur = 32 * ib + ru(r);
+        if (ur + L.h4 < IN) fm_st(rsrc(g.XT), ur, L.ld4, L.vo, xin[ib][r]);
       }
     dense<NB_IN, RV_IN, C::BF>(p.acm.W1, 2, xin, tbl + p.acm.tb1, [&](int ob, const f32x16& acc) {
 #pragma unroll
@@ -825,6 +922,14 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     float lsum = 0.f;
     f32x16 p3[1];
     const float sc = 2.f / ((float)g.B * (float)C::AC);
+    float limv[16], yv[16];  // requested before the layer (see above)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = ru(q) + L.h4;
+      const int uu = u < C::AC ? u : 0;
+      limv[q] = p.acm_lim[uu];
+      yv[q] = g.y[br * C::AC + uu];
+    }
     dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -832,8 +937,8 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
         float v = 0.f;
         if (u < C::AC && valid) {
           const float t = tanhf(acc[q]);
-          const float lim = p.acm_lim[u];
-          const float df = fsub_rn(fmul_rn(t, lim), g.y[br * C::AC + u]);
+          const float lim = limv[q];
+          const float df = fsub_rn(fmul_rn(t, lim), yv[q]);
           lsum += df * df;
           v = sc * df * lim * (1.f - t * t);
         }

@@ -161,7 +161,7 @@ __device__ __forceinline__ void bacm_backward(const SacArgs& p, const f32x16& dc
 
 // Deterministic actor head (ddpg/models.py:17-22): a = tanh(fc3) * lim, a_d = denormalize(a)
 // (natural tile of the fc3 pre-activation in BIG rows [0, AOUT)); a_d overwrites those rows.
-template <class C>
+template <class C, bool BRF = false>
 __device__ __forceinline__ void ddpg_head(const SacArgs& p, const Lane& L, f32x16 (&u)[C::NB_AOUT]) {
   lds_load<C::NB_AOUT>(u, L.img);
 #pragma unroll
@@ -169,7 +169,12 @@ __device__ __forceinline__ void ddpg_head(const SacArgs& p, const Lane& L, f32x1
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ur = 32 * ib + ru(q), j = ur + L.h4;
-      if (j < C::AOUT) L.bl[ur * 32] = denorm(p, j, fmul_rn(tanhf(u[ib][q]), p.actor_lim[j]));
+      const bool ok = j < C::AOUT;
+      if (BRF || ok) {  // BRF: no per-unit branch around the table loads (one round trip each)
+        const int jj = ok ? j : 0;
+        const float ad = denorm(p, jj, fmul_rn(tanhf(u[ib][q]), p.actor_lim[jj]));
+        if (ok) L.bl[ur * 32] = ad;
+      }
     }
 }
 
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_critic_phase(SacArgs p, BAcmScr
     actor_trunk<C, false, C::NB_AOUT, C::AOUT>(p.actor_targ, p.S2, C::OB * L.ld4, L, nullptr, nullptr, d0, d1, d2, d3);
     {
       f32x16 u[C::NB_AOUT];
-      ddpg_head<C>(p, L, u);
+      ddpg_head<C, true>(p, L, u);
     }
     // ---- critic-target input [s' | ACM(s', a'_d)] or [s' | a'_d]   (:116-118)
     f32x16 tin[C::NB_CIN];
@@ -222,10 +227,12 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_critic_phase(SacArgs p, BAcmScr
     const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
     for (int ob = 0; ob < 8; ++ob) {
+      float tv[16];
+      tvals(w3, ob, L.h4, tv);
 #pragma unroll
       for (int q2 = 0; q2 < 16; ++q2) {
         const int ur = 32 * ob + ru(q2);
-        const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tval(w3, ob, q2, L.h4) : 0.f;
+        const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tv[q2] : 0.f;
         L.bl[ur * 32] = v;
         fm_st(d2r, ur, L.ld4, L.vo, v);
       }
@@ -279,9 +286,10 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
     const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
     for (int ob = 0; ob < 8; ++ob) {
+      float tv[16];
+      tvals(w3, ob, L.h4, tv);
 #pragma unroll
-      for (int q2 = 0; q2 < 16; ++q2)
-        L.bl[(32 * ob + ru(q2)) * 32] = getbit(k2, k3, ob, q2) ? dqv * tval(w3, ob, q2, L.h4) : 0.f;
+      for (int q2 = 0; q2 < 16; ++q2) L.bl[(32 * ob + ru(q2)) * 32] = getbit(k2, k3, ob, q2) ? dqv * tv[q2] : 0.f;
     }
     dense_lds<8>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll

@@ -59,6 +59,20 @@ __device__ __forceinline__ void load_table(const SacArgs& p, float* tbl) {
 }
 // Natural-order table vector at (block ob, register q) of this lane half.
 __device__ __forceinline__ float tval(const float* t, int ob, int q, int h4) { return t[32 * ob + ru(q) + h4]; }
+// All 16 table values of output block ob for this lane half (v[q] = tval(t, ob, q, h4)) as 4
+// broadcast ds_read_b128, read before any use: an LDS read inside a select is turned into a
+// branch with its own wait, i.e. one LDS round trip per element.
+__device__ __forceinline__ void tvals(const float* t, int ob, int h4, float (&v)[16]) {
+  const float4* p = reinterpret_cast<const float4*>(t + 32 * ob + h4);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float4 x = p[2 * k];
+    v[4 * k + 0] = x.x;
+    v[4 * k + 1] = x.y;
+    v[4 * k + 2] = x.z;
+    v[4 * k + 3] = x.w;
+  }
+}
 
 __device__ __forceinline__ void setbits(uint64_t& lo, uint64_t& hi, int ob, uint32_t bits) {
   if (ob < 4) lo |= (uint64_t)bits << (16 * ob);
@@ -296,11 +310,13 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
   const float* w3 = L.tbl + Q.tw3;
   dense_lds<8, C::BF>(Q.W2, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
+    float tv[16];
+    tvals(w3, ob, L.h4, tv);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = fmaxf(acc[q], 0.f);
       if constexpr (ST) fm_st(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
-      qp = fmaf(v, tval(w3, ob, q, L.h4), qp);
+      qp = fmaf(v, tv[q], qp);
       bits |= (uint32_t)(v > 0.f) << q;
     }
     setbits(m2lo, m2hi, ob, bits);
@@ -311,7 +327,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
 
 // Squash (sac/models.py:37-52) of the pairing-layout heads tile with eps [aout][Bp].
 // Writes a_d = denormalize(tanh(u)*lim) into LDS rows [0, AOUT); returns logpi.
-template <class C>
+template <class C, bool BRF = false>
 __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&hd)[C::NB_PAIR],
                                               const float* __restrict__ EPS, const Lane& L) {
   float lp = 0.f, corr = 0.f;
@@ -325,13 +341,19 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
     for (int r = 0; r < 8; ++r) ev[ib][r] = fm_ldb(er, 16 * ib + r, L.ld4, L.vp);
+  // BRF, narrow heads: no per-slot branch (a branch holding a table load and its use costs one
+  // round trip per slot); slots j >= AOUT compute on index 0 and are dropped.  The actor phase
+  // keeps the branches: the branch-free form's live ranges spill there.
+  constexpr bool kBranchFree = BRF && C::NB_PAIR <= 2;
 #pragma unroll
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int j0 = 16 * ib + r;
       const int j = j0 + h8;
-      if (j < C::AOUT) {
+      const bool ok = j < C::AOUT;
+      if (kBranchFree || ok) {
+        const int jj = ok ? j : 0;
         const float mu = hd[ib][r];
         const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
         const float sc = expf(ls);
@@ -339,10 +361,13 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         const float u = fadd_rn(mu, fmul_rn(e, sc));
         const float d = fsub_rn(u, mu);
         const float var = fmul_rn(sc, sc);
-        lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(d, d), 2.f * var), logf(sc)), kLogSqrt2Pi);
-        corr += 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
-        const float a = fmul_rn(tanhf(u), p.actor_lim[j]);
-        L.pl[j0 * 32] = denorm(p, j, a);
+        const float lpj = fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(d, d), 2.f * var), logf(sc)), kLogSqrt2Pi);
+        const float cj = 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
+        lp += ok ? lpj : 0.f;
+        corr += ok ? cj : 0.f;
+        const float a = fmul_rn(tanhf(u), p.actor_lim[jj]);
+        const float ad = denorm(p, jj, a);
+        if (ok) L.pl[j0 * 32] = ad;
       }
     }
   const float tot = lp + __shfl_xor(lp, 32, 64);
@@ -378,7 +403,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     {
       f32x16 hd[C::NB_PAIR];
       load_pair<C>(hd, big);
-      lp2 = squash_write<C>(p, hd, p.EPS1, L);
+      lp2 = squash_write<C, true>(p, hd, p.EPS1, L);
     }
     SPP_TP(4);
     // ---- critic-target input: [s' | ACM(s', a'_d)] or [s' | a'_d]   (:46-48)
@@ -426,10 +451,12 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
       for (int ob = 0; ob < 8; ++ob) {
+        float tv[16];
+        tvals(w3, ob, L.h4, tv);
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2) {
           const int ur = 32 * ob + ru(q2);
-          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tval(w3, ob, q2, L.h4) : 0.f;
+          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tv[q2] : 0.f;
           L.bl[ur * 32] = v;
           fm_st(d2r, ur, L.ld4, L.vo, v);
         }
@@ -534,9 +561,10 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
       for (int ob = 0; ob < 8; ++ob) {
+        float tv[16];
+        tvals(w3, ob, L.h4, tv);
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-          L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tval(w3, ob, q, L.h4) : 0.f;
+        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tv[q] : 0.f;
       }
 #ifdef SPP_PROF_NODENSE
       SPP_TP(20);  // delta staging

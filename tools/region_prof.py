@@ -20,8 +20,8 @@ NAMES = {0: "tile start", 1: "actor L1", 2: "actor L2", 3: "actor heads", 4: "sq
          22: "dense_lds epilogue | A: W1Ta (nodense)",
          23: "dense prologue | A: ACM bwd input (nodense)", 24: "dense mfma | A: ACM W3T (nodense)",
          25: "dense epilogue | A: ACM W2T (nodense)",
-         26: "A: tile start", 27: "A: actor trunk", 28: "A: squash", 29: "A: ACM fwd", 30: "A: critics fwd",
-         31: "A: critics bwd", 16: "A: ACM bwd", 17: "A: heads bwd", 18: "A: trunk bwd"}
+         26: "A: tile start", 27: "A: actor trunk", 28: "A: squash", 29: "A: ACM fwd", 19: "A: q min",
+         30: "A: critics L1 (fwd)", 31: "A: critics L2 (fwd)", 16: "A: ACM bwd", 17: "A: heads bwd", 18: "A: trunk bwd"}
 
 
 def main():

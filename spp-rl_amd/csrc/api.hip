@@ -609,6 +609,7 @@ struct sppAgent {
   int o_actor = 0, o_acm = 0, o_targ = 0, o_cfwd = 0, o_call = 0, o_acmreg = 0;
   // LDS constant-table segments (canonical bias / fc3 vectors, read at kernel start)
   std::vector<TabSeg> tab;
+  int tab_floats = 0;  // weight part of the table (make_args appends the limit / normaliser segments)
   ActorDev actor{};
   CriticDev critic[2]{}, targ[2]{};
   AcmDev acm{};
@@ -799,8 +800,11 @@ static sppStatus build_packs(sppAgent* a) {
     cd.tw3 = T(w3, 256);
     cd.b3 = b3;
   }
-  SPP_REQUIRE(toff <= kTabMax && (int)a->tab.size() <= kTabSegs, SPP_E_SHAPE,
-              "LDS table too large (%d floats, %d segments)", toff, (int)a->tab.size());
+  // + the per-launch limit / normaliser segments appended by make_args
+  a->tab_floats = toff;
+  const int extra = 3 * (int)round_up(aout, 32) + (int)round_up(std::max(ac, 1), 32);
+  SPP_REQUIRE(toff + extra <= kTabMax && (int)a->tab.size() + 4 <= kTabSegs, SPP_E_SHAPE,
+              "LDS table too large (%d floats, %d segments)", toff + extra, (int)a->tab.size() + 4);
   // allocate images
   size_t nf4 = 0;
   for (auto& m : ms) nf4 += (size_t)m.job.NBO * m.job.NBI * 4 * 64;
@@ -1062,6 +1066,20 @@ static SacArgs make_args(sppAgent* a, int B) {
   p.part = a->part;
   p.nseg = (int)a->tab.size();
   for (int i = 0; i < p.nseg; ++i) p.seg[i] = a->tab[i];
+  // limits and normaliser vectors (read per output slot by the squash / head epilogues: LDS
+  // instead of a global round trip each); unbound vectors read as zeros
+  int off = a->tab_floats;
+  auto X = [&](const float* v, int n) {
+    const int o = off, np = (int)round_up(std::max(n, 1), 32);
+    p.seg[p.nseg++] = TabSeg{v ? v : a->limits.ptr, v ? n : 0, np, o, 0};
+    off += np;
+    return o;
+  };
+  const int aout = a->cfg.aout;
+  p.t_lim = X(a->limits.ptr, aout);
+  p.t_alim = X(a->limits.ptr + aout, a->cfg.ac);
+  p.t_n0 = X(p.min_max ? a->lo : a->mean, aout);
+  p.t_n1 = X(p.min_max ? a->hi : a->std, aout);
   return p;
 }
 

@@ -172,7 +172,7 @@ __device__ __forceinline__ void ddpg_head(const SacArgs& p, const Lane& L, f32x1
       const bool ok = j < C::AOUT;
       if (BRF || ok) {  // BRF: no per-unit branch around the table loads (one round trip each)
         const int jj = ok ? j : 0;
-        const float ad = denorm(p, jj, fmul_rn(tanhf(u[ib][q]), p.actor_lim[jj]));
+        const float ad = denorm<(C::NB_AOUT <= 2)>(p, L.tbl, jj, fmul_rn(tanhf(u[ib][q]), actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, jj)));
         if (ok) L.bl[ur * 32] = ad;
       }
     }
@@ -332,22 +332,22 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
         const int jj = ok ? j : 0;
         const float s2 = closs ? fm_ldb(s2r, ur, L.ld4, L.vo) : 0.f;
         const float t = tanhf(u[ib][q2]);
-        const float lim = p.actor_lim[jj];
+        const float lim = actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, jj);
         const float a = fmul_rn(t, lim);
         float g_ad = L.bl[ur * 32];
         float g_a = 0.f;
         if (closs) {
           if (p.norm_closs) {
-            const float df = fsub_rn(a, normalize(p, jj, s2));
+            const float df = fsub_rn(a, normalize<(C::NB_AOUT <= 2)>(p, L.tbl, jj, s2));
             g_a += cl_scale * df;
             dist_part += (valid && ok) ? df * df : 0.f;
           } else {
-            const float df = fsub_rn(denorm(p, jj, a), s2);
+            const float df = fsub_rn(denorm<(C::NB_AOUT <= 2)>(p, L.tbl, jj, a), s2);
             g_ad += cl_scale * df;
             dist_part += (valid && ok) ? df * df : 0.f;
           }
         }
-        g_a += g_ad * denorm_scale(p, jj);
+        g_a += g_ad * denorm_scale<(C::NB_AOUT <= 2)>(p, L.tbl, jj);
         u[ib][q2] = ok ? g_a * lim * (1.f - t * t) : 0.f;
       }
 #pragma unroll
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_policy_act(SacArgs p, ActArgs a
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ib + ru(q), j = ur + L.h4;
         if (j < C::AOUT) {
-          const float lim = p.actor_lim[j];
+          const float lim = actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, j);
           float act;
           if (a.mode == 0) {
             act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_policy_act(SacArgs p, ActArgs a
             if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
             act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);
           }
-          if (a.denorm_out) act = denorm(p, j, act);
+          if (a.denorm_out) act = denorm<(C::NB_AOUT <= 2)>(p, L.tbl, j, act);
           L.bl[ur * 32] = act;
           if (valid) a.target_out[er * C::AOUT + j] = act;
         }

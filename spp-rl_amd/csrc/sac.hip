@@ -85,25 +85,53 @@ __device__ __forceinline__ bool getbit(uint64_t lo, uint64_t hi, int ob, int q) 
 }
 
 // memory.py:107-121 (denormalize) and :76-87 / utils.py:62-73 (normalize, force=True)
-__device__ __forceinline__ float denorm(const SacArgs& p, int j, float x) {
-  if (p.min_max) {
-    const float lo = p.lo[j], hi = p.hi[j];
-    const float mid = fadd_rn(hi, lo) * 0.5f, delta = fsub_rn(hi, lo) * 0.5f;
+// TB: read the kernel's LDS table T (make_args puts the limits at t_lim / t_alim and the
+// normaliser vectors at t_n0 / t_n1) instead of the global arrays.  Narrow-head kernels use the
+// table (per-slot global loads are one round trip each there); the wide-head (Ant) kernels keep
+// the global reads.
+template <bool TB>
+__device__ __forceinline__ float nv0(const SacArgs& p, const float* T, int j) {
+  if constexpr (TB) return T[p.t_n0 + j];
+  else return p.min_max ? p.lo[j] : p.mean[j];
+}
+template <bool TB>
+__device__ __forceinline__ float nv1(const SacArgs& p, const float* T, int j) {
+  if constexpr (TB) return T[p.t_n1 + j];
+  else return p.min_max ? p.hi[j] : p.std[j];
+}
+template <bool TB>
+__device__ __forceinline__ float denorm(const SacArgs& p, const float* T, int j, float x) {
+  const float n0 = nv0<TB>(p, T, j), n1 = nv1<TB>(p, T, j);
+  if (p.min_max) {  // n0 = lo, n1 = hi
+    const float mid = fadd_rn(n1, n0) * 0.5f, delta = fsub_rn(n1, n0) * 0.5f;
     return fadd_rn(mid, fmul_rn(x, delta));
   }
-  return fadd_rn(fmul_rn(fadd_rn(p.std[j], 1e-8f), x), p.mean[j]);
+  return fadd_rn(fmul_rn(fadd_rn(n1, 1e-8f), x), n0);  // n0 = mean, n1 = std
 }
-__device__ __forceinline__ float denorm_scale(const SacArgs& p, int j) {
-  if (p.min_max) return fsub_rn(p.hi[j], p.lo[j]) * 0.5f;
-  return fadd_rn(p.std[j], 1e-8f);
+template <bool TB>
+__device__ __forceinline__ float denorm_scale(const SacArgs& p, const float* T, int j) {
+  const float n0 = nv0<TB>(p, T, j), n1 = nv1<TB>(p, T, j);
+  if (p.min_max) return fsub_rn(n1, n0) * 0.5f;
+  return fadd_rn(n1, 1e-8f);
 }
-__device__ __forceinline__ float normalize(const SacArgs& p, int j, float x) {
+template <bool TB>
+__device__ __forceinline__ float normalize(const SacArgs& p, const float* T, int j, float x) {
+  const float n0 = nv0<TB>(p, T, j), n1 = nv1<TB>(p, T, j);
   if (p.min_max) {
-    const float lo = p.lo[j], hi = p.hi[j];
-    const float mid = fadd_rn(hi, lo) * 0.5f;
-    return fdiv_rn(fsub_rn(x, mid), fadd_rn(fsub_rn(hi, mid), 1e-8f));
+    const float mid = fadd_rn(n1, n0) * 0.5f;
+    return fdiv_rn(fsub_rn(x, mid), fadd_rn(fsub_rn(n1, mid), 1e-8f));
   }
-  return fminf(fmaxf(fdiv_rn(fsub_rn(x, p.mean[j]), fadd_rn(p.std[j], 1e-8f)), -10.f), 10.f);
+  return fminf(fmaxf(fdiv_rn(fsub_rn(x, n0), fadd_rn(n1, 1e-8f)), -10.f), 10.f);
+}
+template <bool TB>
+__device__ __forceinline__ float actor_lim(const SacArgs& p, const float* T, int j) {
+  if constexpr (TB) return T[p.t_lim + j];
+  else return p.actor_lim[j];
+}
+template <bool TB>
+__device__ __forceinline__ float acm_lim(const SacArgs& p, const float* T, int u) {
+  if constexpr (TB) return T[p.t_alim + u];
+  else return p.acm_lim[u];
 }
 __device__ __forceinline__ float softplus_t(float x) {  // torch softplus(beta=1, threshold=20)
   return x > 20.f ? x : log1pf(expf(x));
@@ -272,7 +300,10 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
   lds_load<1>(z2, small);
   float limv[16];  // before the layer: a load behind the epilogue's buffer stores waits per element
 #pragma unroll
-  for (int q = 0; q < 16; ++q) limv[q] = p.acm_lim[ru(q) + L.h4 < C::AC ? ru(q) + L.h4 : 0];
+  for (int q = 0; q < 16; ++q) {
+    const int u = ru(q) + L.h4;
+    limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, u < C::AC ? u : 0);
+  }
   dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -365,8 +396,8 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         const float cj = 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
         lp += ok ? lpj : 0.f;
         corr += ok ? cj : 0.f;
-        const float a = fmul_rn(tanhf(u), p.actor_lim[jj]);
-        const float ad = denorm(p, jj, a);
+        const float a = fmul_rn(tanhf(u), actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, jj));
+        const float ad = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, jj, a);
         if (ok) L.pl[j0 * 32] = ad;
       }
     }
@@ -599,7 +630,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       for (int q = 0; q < 16; ++q) {
         const int u = ru(q) + L.h4;
         t3v[q] = fm_ldb(t3r, ru(q), L.ld4, L.vo);
-        limv[q] = p.acm_lim[u < C::AC ? u : 0];
+        limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, u < C::AC ? u : 0);
       }
       if constexpr (kPre) {
 #pragma unroll
@@ -691,23 +722,23 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
             const float u = fadd_rn(mu, fmul_rn(e, sc));
             const float d = fsub_rn(u, mu);
             const float t = tanhf(u);
-            const float lim = p.actor_lim[j];
+            const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, j);
             const float a = fmul_rn(t, lim);
             float g_ad = L.pl[j0 * 32];
             float g_a = 0.f;
             if (p.custom_loss != 0.f) {
               const float s2 = fm_ld(rsrc(p.S2), j0, L.ld4, L.vp);
               if (p.norm_closs) {
-                const float df = fsub_rn(a, normalize(p, j, s2));
+                const float df = fsub_rn(a, normalize<(C::NB_PAIR <= 2)>(p, L.tbl, j, s2));
                 g_a += cl_scale * df;
                 dist_part += valid ? df * df : 0.f;
               } else {
-                const float df = fsub_rn(denorm(p, j, a), s2);
+                const float df = fsub_rn(denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, a), s2);
                 g_ad += cl_scale * df;
                 dist_part += valid ? df * df : 0.f;
               }
             }
-            g_a += g_ad * denorm_scale(p, j);
+            g_a += g_ad * denorm_scale<(C::NB_PAIR <= 2)>(p, L.tbl, j);
             const float var = fmul_rn(sc, sc);
             const float sig_m2u = 1.f / (1.f + expf(2.f * u));
             const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
@@ -745,22 +776,22 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           const float u = fadd_rn(mu, fmul_rn(e, sc));
           const float d = fsub_rn(u, mu);
           const float t = tanhf(u);
-          const float lim = p.actor_lim[jj];
+          const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, jj);
           const float a = fmul_rn(t, lim);
           float g_ad = L.pl[j0 * 32];  // from the critics through the ACM
           float g_a = 0.f;
           if (closs) {
             if (p.norm_closs) {
-              const float df = fsub_rn(a, normalize(p, jj, s2));
+              const float df = fsub_rn(a, normalize<(C::NB_PAIR <= 2)>(p, L.tbl, jj, s2));
               g_a += cl_scale * df;
               dist_part += (valid && ok) ? df * df : 0.f;
             } else {
-              const float df = fsub_rn(denorm(p, jj, a), s2);
+              const float df = fsub_rn(denorm<(C::NB_PAIR <= 2)>(p, L.tbl, jj, a), s2);
               g_ad += cl_scale * df;
               dist_part += (valid && ok) ? df * df : 0.f;
             }
           }
-          g_a += g_ad * denorm_scale(p, jj);
+          g_a += g_ad * denorm_scale<(C::NB_PAIR <= 2)>(p, L.tbl, jj);
           const float var = fmul_rn(sc, sc);
           const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
           const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
@@ -851,7 +882,7 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
         const int j0 = 16 * ib + r;
         const int j = j0 + h8;
         if (j < C::AOUT) {
-          const float lim = p.actor_lim[j];
+          const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, j);
           float act;
           if (a.mode == 0) {
             act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;  // off_policy.py:50-54
@@ -868,7 +899,7 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
             if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
             act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);  // ddpg_acm.py:43-45
           }
-          if (a.denorm_out) act = denorm(p, j, act);
+          if (a.denorm_out) act = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, act);
           L.pl[j0 * 32] = act;
           if (valid) a.target_out[er * C::AOUT + j] = act;
         }
@@ -955,7 +986,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     for (int q = 0; q < 16; ++q) {
       const int u = ru(q) + L.h4;
       const int uu = u < C::AC ? u : 0;
-      limv[q] = p.acm_lim[uu];
+      limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, uu);
       yv[q] = g.y[br * C::AC + uu];
     }
     dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {

@@ -35,8 +35,8 @@ struct TabSeg {
   const float* src;
   int n, npad, off, pad_;
 };
-constexpr int kTabSegs = 20;
-constexpr int kTabMax = 4096;  // floats (16 KiB)
+constexpr int kTabSegs = 28;
+constexpr int kTabMax = 6144;  // floats (24 KiB)
 
 // Feature-major ("unit-major") scratch: X[f][Bp], zero padded beyond B.
 struct SacArgs {
@@ -62,9 +62,11 @@ struct SacArgs {
   // actor-phase outputs
   float *AH1, *AH2, *AD1, *AD2, *ADH;
   float *part;  // per-tile partial sums [ntiles][8]
-  // per-workgroup LDS constant table (biases, critic fc3 weights)
+  // per-workgroup LDS constant table (biases, critic fc3 weights; then the limits and the
+  // normaliser vectors at t_lim / t_alim / t_n0 / t_n1: lo, hi or mean, std)
   TabSeg seg[kTabSegs];
   int nseg;
+  int t_lim, t_alim, t_n0, t_n1;
 };
 
 constexpr int kParts = 8;

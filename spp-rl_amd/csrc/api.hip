@@ -1010,7 +1010,7 @@ static void launch_dw_set(DwSet& D, int ph, hipStream_t st) {
   const int* is = ij + D.nitems[ph];
   const DwJob* jobs = D.jobs.ptr + D.j0[ph];
   hipLaunchKernelGGL(k_dw, dim3(D.nitems[ph]), dim3(kDwThreads), 0, st, jobs, ij, is);
-  hipLaunchKernelGGL(k_dw_reduce, dim3(cdiv(D.max_elems[ph], 4 * 256), D.nj[ph]), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_dw_reduce, dim3(cdiv(D.max_elems[ph], 256), D.nj[ph]), dim3(256), 0, st, jobs);
 }
 static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) { launch_dw_set(a->dws[set], ph, st); }
 

@@ -11,8 +11,8 @@
 // consecutive MFMA k-steps for both A and X (same sample<->k map on both
 // sides).  Each lane streams its 4 A rows and 4 X rows straight from HBM
 // through an R-deep register ring (loads for step t+R-1 issued before step
-// t's MFMAs; R from dw_ring, deeper for thin tile sets).  Partial slabs are summed in a fixed order by k_dw_reduce
-// (deterministic, no atomics).
+// t's MFMAs; R from dw_ring, deeper for thin tile sets).  Partial slabs are
+// summed in a fixed order by k_dw_reduce (deterministic, no atomics).
 #include "common.h"
 #include "internal.h"
 
@@ -211,8 +211,10 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   }
 }
 
-// Fixed-order reduction of the split slabs: one thread per 4 consecutive
-// elements of a job's [N*K | N] image, slabs summed in split order.
+// Fixed-order reduction of the split slabs: one thread per element of a job's [N*K | N] image,
+// slabs summed in split order.  A job has few elements (<= 64K) against 128-256 slabs, so the
+// walk is latency-bound: one element per thread (4x the threads of a float4 walk) and 16
+// slabs' loads in flight.
 __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const DwJob J = jobs[blockIdx.y];
   const int nslab = J.nsplit * J.wsplit;
@@ -220,42 +222,27 @@ __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const int N = J.N, K = J.K0 + J.K1;
   const int64_t nw = (int64_t)N * K;
   const int64_t total = nw + (J.db ? N : 0);
-  const int64_t e0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  if (e0 >= total) return;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* p = J.slab + e0;
-  if (e0 + 4 <= total) {
-    int sp = 0;
-    for (; sp + 4 <= nslab; sp += 4) {
-      float4 v[4];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const float* p = J.slab + e;
+  float s = 0.f;
+  int sp = 0;
+  for (; sp + 16 <= nslab; sp += 16) {
+    float v[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(sp + u) * J.slab_stride);
+    for (int u = 0; u < 16; ++u) v[u] = p[(int64_t)(sp + u) * J.slab_stride];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s[0] += v[u].x; s[1] += v[u].y; s[2] += v[u].z; s[3] += v[u].w;
-      }
-    }
-    for (; sp < nslab; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)sp * J.slab_stride);
-      s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-    }
-  } else {
-    for (int sp = 0; sp < nslab; ++sp)
-      for (int u = 0; e0 + u < total; ++u) s[u] += p[(int64_t)sp * J.slab_stride + u];
+    for (int u = 0; u < 16; ++u) s += v[u];
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t e = e0 + u;
-    if (e >= total) break;
-    if (e < nw) {
-      const int n = (int)(e / K), k = (int)(e % K);
-      if (n < J.nrow2) J.dW[(int64_t)n * K + k] = s[u];
-      else J.dW2[(int64_t)(n - J.nrow2) * K + k] = s[u];
-    } else {
-      const int n = (int)(e - nw);
-      if (n < J.nrow2) J.db[n] = s[u];
-      else J.db2[n - J.nrow2] = s[u];
-    }
+  for (; sp < nslab; ++sp) s += p[(int64_t)sp * J.slab_stride];
+  if (e < nw) {
+    const int n = (int)(e / K), k = (int)(e % K);
+    if (n < J.nrow2) J.dW[(int64_t)n * K + k] = s;
+    else J.dW2[(int64_t)(n - J.nrow2) * K + k] = s;
+  } else {
+    const int n = (int)(e - nw);
+    if (n < J.nrow2) J.db[n] = s;
+    else J.db2[n - J.nrow2] = s;
   }
 }
 

@@ -149,7 +149,6 @@ __device__ __forceinline__ float funkey(uint32_t k) {
 constexpr int kStatsBlocks = 1024;      // pass-1 workgroups (moment partials)
 constexpr int kStatsColsPerThread = 8;  // columns per tx lane (ob <= 128)
 constexpr int kStatsRows = 8;           // rows in flight per thread (index then row loads)
-constexpr int kStatsRowsK = 16;         // passes 2-4: fewer resident waves (64 KiB LDS) -> more loads in flight
 
 // Non-zero LDS bins -> the global histogram (device atomics; sparse after pass 1).
 __device__ __forceinline__ void flush_hist(const uint32_t* sh, int n, uint32_t* g) {

@@ -194,6 +194,10 @@ sppStatus sppSacAcmActorApply(sppAgentHandle h, float* losses_dev, void* stream)
 sppStatus sppAgentBindAlphaGrad(sppAgentHandle h, float* alpha_grad_dev);
 /* Draw both rsample eps tensors of the staged batch on device (Philox, (seed, counter)). */
 sppStatus sppSacAcmDrawEps(sppAgentHandle h, uint64_t seed, uint64_t counter, void* stream);
+/* Test hook: copy the staged eps (which = 0: next-state draw, 1: current-state draw) to a
+ * caller-owned row-major [B][aout] device buffer, so parity tests can replay the exact
+ * device draws through the oracle. */
+sppStatus sppAgentReadEps(sppAgentHandle h, int which, float* out_dev, void* stream);
 /* Fused replay sample + gather into the agent's staging area (device indices). */
 sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int B,
                                   void* stream);

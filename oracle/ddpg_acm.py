@@ -18,17 +18,18 @@ from .adam import OracleAdam
 class OracleDdpgAcm:
     def __init__(self, ob, aout, ac, *, acm_critic=True, custom_loss=1.0, norm_closs=False, norm=None,
                  actor_lim=1.0, acm_lim=1.0, acm_kind="basic", gamma=0.95, tau=0.005, actor_lr=5e-4,
-                 critic_lr=5e-4, params=None):
+                 critic_lr=5e-4, params=None, dtype=torch.float32):
+        self.dt = dtype  # float64: clean reference for the large-batch parity tests
         self.acm_critic, self.custom_loss, self.norm_closs, self.norm = acm_critic, custom_loss, norm_closs, norm
-        self.actor_lim = torch.as_tensor(actor_lim, dtype=torch.float32)
-        self.acm_lim = torch.as_tensor(acm_lim, dtype=torch.float32)
+        self.actor_lim = torch.as_tensor(actor_lim, dtype=dtype)
+        self.acm_lim = torch.as_tensor(acm_lim, dtype=dtype)
         self.acm_kind, self.gamma, self.tau = acm_kind, gamma, tau
         cin = ob + (ac if acm_critic else aout)
         acm_lay = nets.basic_acm_layout(2 * ob, ac) if acm_kind == "basic" else nets.acm_layout(2 * ob, ac)
         self.layouts = {"actor": nets.ddpg_actor_layout(ob, aout), "critic": nets.critic_layout(cin),
                         "actor_targ": nets.ddpg_actor_layout(ob, aout), "critic_targ": nets.critic_layout(cin),
                         "acm": acm_lay}
-        self.p = {k: {n: torch.as_tensor(params[k][n], dtype=torch.float32).clone()
+        self.p = {k: {n: torch.as_tensor(params[k][n]).to(dtype).clone()
                       .requires_grad_(k in ("actor", "critic")) for n, _ in lay}
                   for k, lay in self.layouts.items()}
         self.opt = {"actor": OracleAdam(self.p["actor"].values(), actor_lr),
@@ -40,7 +41,7 @@ class OracleDdpgAcm:
         return nets.acm(self.p["acm"], x, self.acm_lim)
 
     def update(self, obs, next_obs, action, reward, done, acm_action):
-        t = lambda a, dt=torch.float32: torch.as_tensor(np.asarray(a)).to(dt)  # noqa: E731
+        t = lambda a, dt=self.dt: torch.as_tensor(np.asarray(a)).to(dt)  # noqa: E731
         obs, next_obs, action, reward = t(obs), t(next_obs), t(action), t(reward)
         done, acm_action = t(done, torch.int8), t(acm_action)
         P, losses = self.p, {}

@@ -21,12 +21,15 @@ from .adam import OracleAdam
 class OracleSacAcm:
     def __init__(self, ob, aout, ac, *, acm_critic=True, custom_loss=0.2, norm_closs=False,
                  norm=None, actor_lim=1.0, acm_lim=1.0, gamma=0.99, tau=0.005, actor_lr=1e-3,
-                 critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, target_entropy=None, params=None):
+                 critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, target_entropy=None, params=None, dtype=torch.float32):
+        # dtype=torch.float64 gives a clean reference for the large-batch parity tests (the
+        # device path is fp32; at B = 409,600 its summation order differs from torch's)
+        self.dt = dtype
         self.ob, self.aout, self.ac = ob, aout, ac
         self.acm_critic, self.custom_loss, self.norm_closs = acm_critic, custom_loss, norm_closs
         self.norm = norm
-        self.actor_lim = torch.as_tensor(actor_lim, dtype=torch.float32)
-        self.acm_lim = torch.as_tensor(acm_lim, dtype=torch.float32)
+        self.actor_lim = torch.as_tensor(actor_lim, dtype=dtype)
+        self.acm_lim = torch.as_tensor(acm_lim, dtype=dtype)
         self.gamma, self.tau = gamma, tau
         self.target_entropy = float(-ac if target_entropy is None else target_entropy)
         cin = ob + (ac if acm_critic else aout)
@@ -36,7 +39,7 @@ class OracleSacAcm:
         self.p = {}
         for k, lay in self.layouts.items():
             trainable = k in ("actor", "critic_1", "critic_2")
-            self.p[k] = {n: torch.as_tensor(params[k][n], dtype=torch.float32).clone()
+            self.p[k] = {n: torch.as_tensor(params[k][n]).to(dtype).clone()
                          .requires_grad_(trainable) for n, _ in lay}
         self.opt = {"actor": OracleAdam(self.p["actor"].values(), actor_lr),
                     "critic_1": OracleAdam(self.p["critic_1"].values(), critic_lr),
@@ -49,9 +52,8 @@ class OracleSacAcm:
     def _acm(self, x):
         return nets.acm(self.p["acm"], x, self.acm_lim)
 
-    @staticmethod
-    def _t(a, dt=torch.float32):
-        return torch.as_tensor(np.asarray(a)).to(dt)
+    def _t(self, a, dt=None):
+        return torch.as_tensor(np.asarray(a)).to(self.dt if dt is None else dt)
 
     def critic_grads(self, obs, next_obs, action, reward, done, acm_action, eps_next):
         """compute_qfunc_targ (sac_acm.py:30-58) + both critic losses (:97-131).
@@ -130,7 +132,7 @@ class OracleSacAcm:
         g, ga, l2, lpd = self.actor_grads(obs, next_obs, eps_cur)
         losses.update(l2)
         self.actor_apply(g, ga)
-        flat = lambda gs: torch.cat([x.reshape(-1) for x in gs]).numpy()  # noqa: E731
+        flat = lambda gs: torch.cat([x.detach().reshape(-1) for x in gs]).numpy()  # noqa: E731
         self.last = {"y": y, "logp": lpd, "grads": {"critic_1": flat(cg["critic_1"]), "critic_2": flat(cg["critic_2"]),
                                                     "actor": flat(g)}}
         return losses

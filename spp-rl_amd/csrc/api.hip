@@ -1377,6 +1377,16 @@ sppStatus sppSacAcmDrawEps(sppAgentHandle a, uint64_t seed, uint64_t counter, vo
   return SPP_OK;
 }
 
+sppStatus sppAgentReadEps(sppAgentHandle a, int which, float* out, void* stream) {
+  SPP_REQUIRE(a && out && (which == 0 || which == 1), SPP_E_INVALID_ARG, "read_eps: bad args");
+  SPP_REQUIRE(a->cur_B > 0, SPP_E_STATE, "no staged batch");
+  const int B = a->cur_B, Bp = (int)round_up(B, 32);
+  hipLaunchKernelGGL(k_eps_read_fm, dim3(cdiv((int64_t)a->cfg.aout * B, 256)), dim3(256), 0, S(stream),
+                     (const float*)(which ? a->EPS2 : a->EPS1), out, a->cfg.aout, B, Bp);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
 sppStatus sppAgentSetTiming(sppAgentHandle a, int enable) {
   SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
   a->timing = enable != 0;

@@ -1066,6 +1066,14 @@ __global__ void k_eps_copy_fm(const float* eps, float* E, int aout, int B, int B
   E[i] = b < B ? eps[b * aout + j] : 0.f;
 }
 
+// Feature-major [aout][Bp] -> row-major [B][aout] (read-back of the staged eps).
+__global__ void k_eps_read_fm(const float* E, float* eps, int aout, int B, int Bp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)aout * B) return;
+  const int64_t b = i / aout, j = i % aout;
+  eps[i] = E[j * Bp + b];
+}
+
 // Device-side Gaussian eps straight into the feature-major layout (zero padded).
 __global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint64_t ctr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pair index

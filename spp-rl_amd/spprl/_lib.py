@@ -91,6 +91,7 @@ _SIGS = {
                              c_void_p, c_void_p]),
     "sppAgentBindAlphaGrad": (c_int, [c_void_p, c_void_p]),
     "sppSacAcmDrawEps": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "sppAgentReadEps": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "sppAcmRegressGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "sppAcmRegressApply": (c_int, [c_void_p, c_void_p]),
     "sppReplayGatherAcm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),

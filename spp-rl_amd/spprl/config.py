@@ -44,3 +44,18 @@ ENV_SPECS = {
     "Ant-v3": (111, 8, 1.0, 1000),
     "Pendulum-v0": (3, 1, 2.0, 200),
 }
+
+
+def default_max_batch(update_batch_size, kw):
+    """Largest batch the agent's device scratch must hold when the caller gives no
+    ``max_batch``: the reference batch, or with E > 1 envs the fused schedule's rho*E
+    grad-step batch and sigma*E ACM batch (trainer.OffPolicyLoop.fused_batch_sizes)."""
+    env = kw.get("env")
+    E = int(env.n) if env is not None else int(kw.get("n_envs", 1))
+    rho = update_batch_size * kw.get("grad_steps", GRAD_STEPS) / kw.get("update_freq", UPDATE_FREQ)
+    nb = kw.get("acm_update_batches", ACM_UPDATE_BATCHES)
+    sigma = nb * kw.get("acm_batch_size", ACM_BATCH_SIZE) / kw.get("acm_update_freq", ACM_UPDATE_FREQ) if nb else 0
+    out = max(int(update_batch_size), int(kw.get("acm_batch_size", ACM_BATCH_SIZE)))
+    if E > 1 and kw.get("schedule", "fused") == "fused":
+        out = max(out, int(round(rho * E)), int(round(sigma * E)))
+    return out

@@ -42,7 +42,7 @@ class DDPG_AcM(OffPolicyLoop):
         self.actor_output_dim = aout = ob
         lim = 1.0 if self.min_max_denormalize else float(config.MAX_ABS_OBS_VALUE)  # acm.py:102-108
         self.actor_ac_lim = torch.full((aout,), lim)
-        self.max_batch = int(max_batch or update_batch_size)
+        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, unused))
         cin = ob + (ac if self.acm_critic else aout)
         self.layouts = {_lib.SPP_NET_ACTOR: nets.ddpg_actor_layout(ob, aout),
                         _lib.SPP_NET_ACTOR_TARG: nets.ddpg_actor_layout(ob, aout),

@@ -41,6 +41,19 @@ def make_allreduce_sum(group=None):
     return allreduce_sum
 
 
+def stream_key(seed, tag):
+    """Philox key of one random-stream consumer (policy eps, replay indices, update eps, env
+    resets, env actions): splitmix64 of (seed, tag), so consumers sharing a seed never share
+    a (key, counter) pair."""
+    import zlib
+
+    m = (1 << 64) - 1
+    z = (int(seed) * 0x9E3779B97F4A7C15 + zlib.crc32(tag.encode()) * 0xD1B54A32D192ED03) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return (z ^ (z >> 31)) & ((1 << 63) - 1)
+
+
 def shard_seed(base, rank):
     """Per-rank seed of the env / sampling / eps streams (ranks must differ)."""
     return int(base) + 1000 * int(rank)

@@ -33,6 +33,7 @@ from ._lib import call, ptr, stream_handle
 from .onpolicy import OnPolicyNets
 from .ppo import calculate_gae
 from .sac_acm import SAC_AcM
+from .dp import stream_key
 from .trainer import StatsLogger, SynthVecEnv
 
 
@@ -86,6 +87,7 @@ class PPO_AcM:
         self.stats_logger = StatsLogger()
         self.iteration = 0
         self.loop_seed, self._ctr = int(loop_seed), 0
+        self._key_policy = stream_key(loop_seed, "policy")
         self.loss = {}
         d = self.device
         self._ep_ret = torch.zeros(E, device=d)
@@ -96,14 +98,14 @@ class PPO_AcM:
     # ---------------------------------------------------------------- helpers
     def _randn(self, t):
         self._ctr += 1
-        call("sppRandNormal", ptr(t), t.numel(), self.loop_seed, self._ctr, stream_handle())
+        call("sppRandNormal", ptr(t), t.numel(), self._key_policy, self._ctr, stream_handle())
         return t
 
     def normalize(self, x):
         """MemoryAcM.normalize with the ring's statistics (memory.py:76-88)."""
         rb = self.replay_buffer
         if self.min_max_denormalize and not rb._have_minmax:
-            return x
+            return x.clone()  # the caller keeps it: never alias the env's double-buffered obs
         return rb._norm(x, 0)
 
     def denormalize(self, x):

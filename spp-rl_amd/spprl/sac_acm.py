@@ -57,7 +57,7 @@ class SAC_AcM(OffPolicyLoop):
         self.ac_lim = torch.full((ac,), float(ac_high))
         self.target_entropy = -float(ac)  # Q4 (sac.py:104-106)
         self.alpha = alpha
-        self.max_batch = int(max_batch or update_batch_size)
+        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, unused))
         aout = self.actor_output_dim
         cin = ob + (ac if self.acm_critic else aout)
         self.layouts = {_lib.SPP_NET_ACTOR: nets.sac_actor_layout(ob, aout),
@@ -177,7 +177,7 @@ class SAC_AcM(OffPolicyLoop):
         call("sppSacAcmActorApply", self._h, ptr(self._losses), st)
 
     def _fused_update(self, idx, counter, allreduce=None):
-        self.update_from_replay_dp(idx, self.loop_seed + 1, counter, allreduce)
+        self.update_from_replay_dp(idx, self._key_update, counter, allreduce)
 
     def acm_update_from_replay(self, idx, x, y, loss, allreduce=None):
         """update_acm_batches body (acm.py:356-372) for one device-sampled batch."""

@@ -39,7 +39,7 @@ import torch
 
 from . import config
 from ._lib import call, ptr, stream_handle
-from .dp import make_allreduce, make_allreduce_sum
+from .dp import make_allreduce, make_allreduce_sum, stream_key
 
 # ---------------------------------------------------------------- stats
 
@@ -86,6 +86,7 @@ class SynthVecEnv:
         self.ac_low = torch.full((ac,), -float(ac_high), device=self.device)
         self.ac_high = torch.full((ac,), float(ac_high), device=self.device)
         self.seed, self._ctr = int(seed), 0
+        self._key_reset, self._key_action = stream_key(seed, "env"), stream_key(seed, "env_action")
         self.obs = torch.empty(self.n, ob, device=self.device)
         self.nobs = torch.empty(self.n, ob, device=self.device)
         self.rew = torch.empty(self.n, device=self.device)
@@ -101,7 +102,8 @@ class SynthVecEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(np.asarray(mask, np.uint8)).to(self.device)
-        call("sppSynthEnvReset", ptr(self.obs), ptr(m), self.n, self.ob, self.seed, self._next(), stream_handle())
+        call("sppSynthEnvReset", ptr(self.obs), ptr(m), self.n, self.ob, self._key_reset, self._next(),
+             stream_handle())
         self._keep = m
         if mask is None:
             self.t = 0
@@ -121,7 +123,7 @@ class SynthVecEnv:
 
     def sample_actions(self, out):
         """action_space.sample() for every env, on device (pre-train collector)."""
-        call("sppRandUniform", ptr(out), out.numel(), ptr(self.ac_low), ptr(self.ac_high), self.ac, self.seed + 7,
+        call("sppRandUniform", ptr(out), out.numel(), ptr(self.ac_low), ptr(self.ac_high), self.ac, self._key_action,
              self._next(), stream_handle())
         return out
 
@@ -135,11 +137,15 @@ class HostVecEnv:
 
     Actions go device -> pinned host on a side stream; observations/rewards come back
     pinned host -> device on the same side stream; the compute stream waits on an event,
-    so the copies overlap whatever the compute stream has queued (the update)."""
+    so the copies overlap whatever the compute stream has queued (the update).
+
+    The pinned staging is a ring of ``n_stage`` buffer sets, each with the event of the
+    upload that last read it: the host only writes a set once that upload has completed,
+    so a queued (not yet executed) H2D copy never sees the next step's or a reset's rows."""
 
     is_host = True
 
-    def __init__(self, envs, device="cuda", env_fn=None):
+    def __init__(self, envs, device="cuda", env_fn=None, n_stage=4):
         self.env_fn = env_fn
         self.envs = list(envs)
         self.n = len(self.envs)
@@ -150,9 +156,10 @@ class HostVecEnv:
         self.device = torch.device(device)
         self.side = torch.cuda.Stream(device=self.device)
         pin = dict(pin_memory=True)
-        self.h_obs = torch.empty(self.n, self.ob, **pin)
-        self.h_rew = torch.empty(self.n, **pin)
-        self.h_end = torch.empty(self.n, dtype=torch.uint8, **pin)
+        self._stage = [(torch.zeros(self.n, self.ob, **pin), torch.zeros(self.n, **pin),
+                        torch.zeros(self.n, dtype=torch.uint8, **pin)) for _ in range(int(n_stage))]
+        self._stage_ev = [None] * len(self._stage)
+        self._cur = 0
         self.h_act = torch.empty(self.n, self.ac, **pin)
         self.obs = torch.empty(self.n, self.ob, device=self.device)
         self.rew = torch.empty(self.n, device=self.device)
@@ -160,19 +167,38 @@ class HostVecEnv:
         self._act_ev = torch.cuda.Event()
         self._pending = False
 
+    def _writable(self, carry):
+        """Advance to the next staging set, wait for its last upload, and (carry) copy the
+        current set's rows into it (a partial reset keeps the other envs' observations)."""
+        prev = self._stage[self._cur]
+        self._cur = (self._cur + 1) % len(self._stage)
+        ev = self._stage_ev[self._cur]
+        if ev is not None:
+            ev.synchronize()
+        cur = self._stage[self._cur]
+        if carry:
+            for dst, src in zip(cur, prev):
+                dst.copy_(src)
+        return cur
+
     def _upload(self):
+        h_obs, h_rew, h_end = self._stage[self._cur]
         main = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(self.side):
             self.side.wait_stream(main)  # do not overwrite obs still being read by queued kernels
-            self.obs.copy_(self.h_obs, non_blocking=True)
-            self.rew.copy_(self.h_rew, non_blocking=True)
-            self.end_dev.copy_(self.h_end, non_blocking=True)
+            self.obs.copy_(h_obs, non_blocking=True)
+            self.rew.copy_(h_rew, non_blocking=True)
+            self.end_dev.copy_(h_end, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self._stage_ev[self._cur] = ev
         main.wait_stream(self.side)
 
     def reset(self, mask=None):
+        h_obs, _, _ = self._writable(carry=mask is not None)
         idx = range(self.n) if mask is None else np.flatnonzero(mask)
         for e in idx:
-            self.h_obs[e] = torch.as_tensor(np.asarray(self.envs[e].reset(), np.float32).reshape(-1))
+            h_obs[e] = torch.as_tensor(np.asarray(self.envs[e].reset(), np.float32).reshape(-1))
         self._upload()
         return self.obs
 
@@ -189,13 +215,14 @@ class HostVecEnv:
         self._act_ev.synchronize()
         self._pending = False
         act = self.h_act.numpy()
+        h_obs, h_rew, h_end = self._writable(carry=False)
         end = np.zeros(self.n, bool)
         for e, env in enumerate(self.envs):
             o, r, d, _ = env.step(act[e])
-            self.h_obs[e] = torch.as_tensor(np.asarray(o, np.float32).reshape(-1))
-            self.h_rew[e] = float(r)
+            h_obs[e] = torch.as_tensor(np.asarray(o, np.float32).reshape(-1))
+            h_rew[e] = float(r)
             end[e] = bool(d)
-        self.h_end.copy_(torch.from_numpy(end.astype(np.uint8)))
+        h_end.copy_(torch.from_numpy(end.astype(np.uint8)))
         self._upload()
         return self.obs, self.rew, end, self.end_dev
 
@@ -256,6 +283,9 @@ class OffPolicyLoop:
         self.allreduce = allreduce if allreduce is not None else make_allreduce()
         self.allreduce_sum = make_allreduce_sum() if self.allreduce is not None else None
         self.loop_seed = int(loop_seed)
+        # one Philox key per random-stream consumer (never a shared (key, counter) pair)
+        self._key_policy, self._key_index = stream_key(loop_seed, "policy"), stream_key(loop_seed, "index")
+        self._key_update = stream_key(loop_seed, "update_eps")
         self._ctr = 0
         E = self.n_envs
         self.rho = self.update_batch_size * self.grad_steps / self.update_freq
@@ -277,7 +307,7 @@ class OffPolicyLoop:
         return self._ctr
 
     def _randn(self, t):
-        call("sppRandNormal", ptr(t), t.numel(), self.loop_seed, self._next(), stream_handle())
+        call("sppRandNormal", ptr(t), t.numel(), self._key_policy, self._next(), stream_handle())
         return t
 
     def _set_acm_lr(self, lr):
@@ -323,12 +353,9 @@ class OffPolicyLoop:
     def update_obs_stats(self):
         """update_obs_mean_std (rl.py:93-112); global over the ranks' shards under DP."""
         if self.allreduce_sum is not None:
-            # every rank runs the same cadence over the same number of envs, so the shards
-            # hold equally many rows: no host sync to learn the global count
-            import torch.distributed as dist
-
-            n_global = len(self.replay_buffer) * dist.get_world_size()
-            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, n_global)
+            # shard lengths differ across ranks once resets (early terminations) advance the
+            # obs rings unevenly: the global row count is all-reduced, never assumed
+            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum)
         else:
             self.replay_buffer.update_obs_mean_std()
 
@@ -418,7 +445,7 @@ class OffPolicyLoop:
         B, BA = self.fused_batch_sizes()
         if n > self.update_batch_size:
             idx = torch.empty(B, dtype=torch.int64, device=self.device)
-            call("sppRandIndex", ptr(idx), B, n, self.loop_seed, self._next(), stream_handle())
+            call("sppRandIndex", ptr(idx), B, n, self._key_index, self._next(), stream_handle())
             self._fused_update(idx, self._ctr, self.allreduce)
             self._keep_idx = idx
         if self.iteration > 0 and self.acm_epochs > 0:
@@ -437,7 +464,7 @@ class OffPolicyLoop:
 
     def _rand_idx(self, B, n):
         idx = torch.empty(B, dtype=torch.int64, device=self.device)
-        call("sppRandIndex", ptr(idx), B, n, self.loop_seed, self._next(), stream_handle())
+        call("sppRandIndex", ptr(idx), B, n, self._key_index, self._next(), stream_handle())
         return idx
 
     # ---------------------------------------------------------- ACM regression

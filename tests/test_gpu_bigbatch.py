@@ -1,0 +1,261 @@
+"""GPU parity of the TIMED configuration: the update at the bench's batch sizes.
+
+bench.py runs SAC_AcM / DDPG_AcM at B = rho*E = 409,600 (E = 4096 envs, rho = 100,
+SURVEY.md §8d).  At that size the device path differs from the B <= 100 fixture
+cases in ways only a large batch exercises:
+  - split-K weight gradients over 2048-sample slabs (~200 slabs per job) and the
+    fixed-order slab reduce ``k_dw_reduce``; the thin-job wave split;
+  - grid-stride tile loops of the phase kernels over 12,800 tiles;
+  - the replay stage (``k_replay_stage_fm``: random-row gather -> feature-major);
+  - the device Philox eps (``k_eps_fm``) and indices (``k_rand_index``).
+Each case runs the device step and the oracle (oracle/sac_acm.py, oracle/ddpg_acm.py,
+float64 so its own summation error is negligible) on the same inputs and compares:
+  fp32 path : losses rtol 1e-4; ||g - g_ref|| / ||g_ref|| < 2e-4 per network;
+              post-Adam parameters |d| <= 2 lr (first Adam step moves by ~lr sign(g))
+              with fewer than 0.2 % of weights beyond 1e-5
+  bf16 MLP  : losses rtol 3e-2; gradient relative error < 6e-2 (bf16 operands,
+              8-bit mantissa, fp32 accumulation)
+Reference: acm/off_policy/sac_acm.py:89-162, ddpg_acm.py:147-201 (rltoolkit).
+The sampler checks at the end cover sppRandIndex / sppRandNormal / sppSacAcmDrawEps
+(range, uniformity, moments), which feed every timed step.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import spprl  # noqa: E402
+from spprl import _lib  # noqa: E402
+from oracle.ddpg_acm import OracleDdpgAcm  # noqa: E402
+from oracle.nets import Norm  # noqa: E402
+from oracle.sac_acm import OracleSacAcm  # noqa: E402
+
+DEV = torch.device("cuda:0")
+F64 = torch.float64
+SAC_NETS = {"actor": _lib.SPP_NET_ACTOR, "critic_1": _lib.SPP_NET_CRITIC1, "critic_2": _lib.SPP_NET_CRITIC2,
+            "critic_1_targ": _lib.SPP_NET_CRITIC1_TARG, "critic_2_targ": _lib.SPP_NET_CRITIC2_TARG,
+            "acm": _lib.SPP_NET_ACM}
+DDPG_NETS = {"actor": _lib.SPP_NET_ACTOR, "critic": _lib.SPP_NET_CRITIC1, "actor_targ": _lib.SPP_NET_ACTOR_TARG,
+             "critic_targ": _lib.SPP_NET_CRITIC1_TARG, "acm": _lib.SPP_NET_ACM}
+
+
+def relerr(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def snapshot(ag, names):
+    return {k: {n: v.numpy().copy() for n, v in ag.net_state(net).items()} for k, net in names.items()}
+
+
+def random_batch(rng, B, ob, aout, ac):
+    return (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
+            rng.uniform(-1, 1, (B, aout)).astype(np.float32), rng.randn(B).astype(np.float32),
+            (rng.rand(B) < 0.05).astype(np.int8), rng.uniform(-1, 1, (B, ac)).astype(np.float32))
+
+
+def set_minmax(ag, rng, ob):
+    lo = -rng.uniform(0.5, 2, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2, ob).astype(np.float32)
+    rb = ag.replay_buffer
+    rb.min_obs.copy_(torch.from_numpy(lo))
+    rb.max_obs.copy_(torch.from_numpy(hi))
+    rb._have_minmax = True
+    return Norm(True, torch.from_numpy(lo), torch.from_numpy(hi))
+
+
+def check_sac(ag, o, ol, grad_tol, loss_tol, params_check=True, params0=None):
+    errs = {}
+    for k in ("critic_1", "critic_2", "actor"):
+        errs[k] = relerr(ag.grads[SAC_NETS[k]].cpu().numpy(), o.last["grads"][k])
+    gl = ag.loss
+    print("grad rel err", {k: "%.2e" % v for k, v in errs.items()},
+          "losses", {k: (round(gl[k], 6), round(ol[k], 6)) for k in gl})
+    for k, e in errs.items():
+        assert e < grad_tol, (k, e)
+    for k in gl:
+        assert abs(gl[k] - ol[k]) <= loss_tol * abs(ol[k]) + 1e-6, (k, gl[k], ol[k])
+    if params_check:
+        assert ag.current_alpha() == pytest.approx(o.alpha, rel=1e-5)
+        lr = 1e-3
+        for k in ("actor", "critic_1", "critic_2", "critic_1_targ", "critic_2_targ"):
+            got = ag.params[SAC_NETS[k]].cpu().numpy().astype(np.float64)
+            want = o.flat(k).astype(np.float64)
+            d = np.abs(got - want)
+            assert d.max() <= 2 * lr * 1.01, (k, d.max())
+            assert np.mean(d > 1e-5) < 2e-3, (k, np.mean(d > 1e-5))
+
+
+# ------------------------------------------------------------------ caller-batch path
+@pytest.mark.parametrize("env_name,ob,ac,B,bf16", [
+    ("Hopper-v2", 11, 3, 65536, False),
+    ("Hopper-v2", 11, 3, 409600, False),
+    ("Ant-v2", 111, 8, 65536, True),
+    ("Ant-v2", 111, 8, 409600, True),
+])
+def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
+    rng = np.random.RandomState(B % 1000 + ob)
+    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
+                       denormalize_actor_out=True, gamma=0.99, max_batch=B, buffer_size=128, device=DEV, seed=3,
+                       mlp_bf16=bf16)
+    params = snapshot(ag, SAC_NETS)
+    norm = set_minmax(ag, rng, ob)
+    batch = random_batch(rng, B, ob, ob, ac)
+    e1, e2 = rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32)
+    ag.update(*batch, eps_next=e1, eps_cur=e2)
+    torch.cuda.synchronize()
+    o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm, actor_lim=1.0,
+                     acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params, dtype=F64)
+    ol = o.update(*batch, e1, e2)
+    if bf16:
+        check_sac(ag, o, ol, grad_tol=6e-2, loss_tol=3e-2, params_check=False)
+    else:
+        check_sac(ag, o, ol, grad_tol=2e-4, loss_tol=1e-4)
+
+
+@pytest.mark.parametrize("B", [65536, 409600])
+def test_ddpg_acm_update_large_batch_matches_oracle(B):
+    ob, ac = 17, 6
+    rng = np.random.RandomState(B % 977)
+    ag = spprl.DDPG_AcM(env_name="HalfCheetah-v2", gamma=0.95, actor_lr=5e-4, critic_lr=5e-4, acm_critic=True,
+                        custom_loss=1.0, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                        max_batch=B, buffer_size=64, device=DEV, seed=4)
+    params = snapshot(ag, DDPG_NETS)
+    norm = set_minmax(ag, rng, ob)
+    batch = random_batch(rng, B, ob, ob, ac)
+    ag.update(*batch)
+    torch.cuda.synchronize()
+    o = OracleDdpgAcm(ob, ob, ac, norm=norm, actor_lim=1.0, gamma=0.95, tau=0.005, params=params, dtype=F64)
+    ol = o.update(*batch)
+    gl = ag.loss
+    for k in ("critic", "actor"):
+        e = relerr(ag.grads[DDPG_NETS[k]].cpu().numpy(), o.last["grads"][k])
+        print(k, "grad rel err %.2e" % e)
+        assert e < 2e-4, (k, e)
+    for k in ("critic", "actor", "ddpg", "dist"):
+        assert abs(gl[k] - ol[k]) <= 1e-4 * abs(ol[k]) + 1e-6, (k, gl[k], ol[k])
+    for k in ("actor", "critic"):
+        d = np.abs(ag.params[DDPG_NETS[k]].cpu().numpy() - o.flat(k))
+        assert d.max() <= 2 * 5e-4 * 1.01 and np.mean(d > 1e-5) < 2e-3, (k, d.max())
+
+
+# ------------------------------------------------------------------ the bench's staged path
+def _filled(ag, rng, n_rows, ob, ac):
+    rb = ag.replay_buffer
+    slots = rb.add_obs_batch(torch.from_numpy(rng.randn(n_rows + 1, ob).astype(np.float32)))
+    rb.add_timestep_batch(slots[:n_rows], slots[1:], torch.from_numpy(rng.randn(n_rows, ob).astype(np.float32)),
+                          rng.randn(n_rows).astype(np.float32), rng.rand(n_rows) < 0.05, rng.rand(n_rows) < 0.05,
+                          torch.from_numpy(rng.uniform(-1, 1, (n_rows, ac)).astype(np.float32)))
+    rb.update_obs_mean_std()
+    return rb
+
+
+@pytest.mark.parametrize("env_name,ob,ac,B,bf16", [("Hopper-v2", 11, 3, 409600, False),
+                                                   ("Ant-v2", 111, 8, 409600, True)])
+def test_staged_replay_update_with_device_draws_matches_oracle(env_name, ob, ac, B, bf16):
+    """The exact sequence bench.py times per vector step (OffPolicyLoop._fused_make_update):
+    sppRandIndex -> sppAgentStageFromReplay -> sppSacAcmDrawEps -> critic grads / apply ->
+    actor grads / apply.  The device indices and eps are read back and replayed through the
+    oracle on the gathered tuples."""
+    rng = np.random.RandomState(11)
+    n_rows = 200_000
+    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
+                       denormalize_actor_out=True, gamma=0.99, max_batch=B, buffer_size=n_rows + 64, device=DEV,
+                       seed=5, mlp_bf16=bf16)
+    rb = _filled(ag, rng, n_rows, ob, ac)
+    params = snapshot(ag, SAC_NETS)
+    st = _lib.stream_handle()
+    idx = torch.empty(B, dtype=torch.int64, device=DEV)
+    _lib.call("sppRandIndex", _lib.ptr(idx), B, len(rb), 77, 5, st)
+    _lib.call("sppAgentStageFromReplay", ag._h, rb._h, _lib.ptr(idx), B, st)
+    _lib.call("sppSacAcmDrawEps", ag._h, 78, 3, st)
+    eps = [torch.empty(B, ob, device=DEV) for _ in range(2)]
+    for w in (0, 1):
+        _lib.call("sppAgentReadEps", ag._h, w, _lib.ptr(eps[w]), st)
+    batch = [t.cpu().numpy() for t in rb.gather(idx)]  # reference layout tuples (bit-exact gather)
+    norm = Norm(True, rb.min_obs.cpu().clone(), rb.max_obs.cpu().clone())
+    _lib.call("sppSacAcmCriticGrads", ag._h, None, None, _lib.ptr(ag._losses), st)
+    _lib.call("sppSacAcmCriticApply", ag._h, st)
+    _lib.call("sppSacAcmActorGrads", ag._h, None, _lib.ptr(ag._losses), st)
+    _lib.call("sppSacAcmActorApply", ag._h, _lib.ptr(ag._losses), st)
+    torch.cuda.synchronize()
+    ix = idx.cpu().numpy()
+    assert ix.min() >= 0 and ix.max() < len(rb)
+    e1, e2 = eps[0].cpu().numpy(), eps[1].cpu().numpy()
+    for e in (e1, e2):  # k_eps_fm draws: standard normal moments over 4.5e6 (11 dims) / 4.5e7 (111) values
+        n = e.size
+        assert abs(e.mean()) < 6 / np.sqrt(n) and abs(e.var() - 1) < 6 * np.sqrt(2.0 / n), (e.mean(), e.var())
+    assert abs(np.corrcoef(e1.ravel()[:1 << 20], e2.ravel()[:1 << 20])[0, 1]) < 6 / np.sqrt(1 << 20)
+    o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm, actor_lim=1.0,
+                     acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params, dtype=F64)
+    ol = o.update(*batch, e1, e2)
+    if bf16:
+        check_sac(ag, o, ol, grad_tol=6e-2, loss_tol=3e-2, params_check=False)
+    else:
+        check_sac(ag, o, ol, grad_tol=2e-4, loss_tol=1e-4)
+
+
+# ------------------------------------------------------------------ device samplers
+@pytest.mark.parametrize("high", [3, 1 << 20, 999_983, 1_000_000, 10_000_000])
+def test_rand_index_range_and_uniformity(high):
+    from scipy import stats
+
+    n = (1 << 22) + 5
+    idx = torch.empty(n, dtype=torch.int64, device=DEV)
+    _lib.call("sppRandIndex", _lib.ptr(idx), n, high, 1234, 9, _lib.stream_handle())
+    x = idx.cpu().numpy()
+    assert x.min() >= 0 and x.max() < high
+    nb = min(high, 256)
+    counts = np.bincount((x * nb) // high, minlength=nb)
+    # equal-width bins of [0, high): expected mass proportional to the integers per bin
+    edges = (np.arange(nb + 1) * high + nb - 1) // nb
+    expected = np.diff(edges) / high * n
+    p = stats.chisquare(counts, expected).pvalue
+    assert p > 1e-4, p
+    assert abs(x.mean() - (high - 1) / 2) < 6 * high / np.sqrt(12 * n)
+    # consecutive draws uncorrelated; another counter gives another stream
+    assert abs(np.corrcoef(x[:-1], x[1:])[0, 1]) < 6 / np.sqrt(n)
+    _lib.call("sppRandIndex", _lib.ptr(idx), n, high, 1234, 10, _lib.stream_handle())
+    y = idx.cpu().numpy()
+    q = 1.0 / high
+    assert np.mean(x == y) < q + 6 * np.sqrt(q * (1 - q) / n) + 1e-12
+
+
+@pytest.mark.parametrize("n", [(1 << 22) + 3, 1001])
+def test_rand_normal_moments(n):
+    from scipy import stats
+
+    out = torch.empty(n, device=DEV)
+    _lib.call("sppRandNormal", _lib.ptr(out), n, 42, 1, _lib.stream_handle())
+    x = out.cpu().numpy().astype(np.float64)
+    assert np.isfinite(x).all()
+    tol = 6 / np.sqrt(n)
+    assert abs(x.mean()) < tol
+    assert abs(x.var() - 1) < 6 * np.sqrt(2.0 / n)
+    if n > 10000:
+        assert abs(stats.skew(x)) < 6 * np.sqrt(6.0 / n)
+        assert abs(stats.kurtosis(x)) < 6 * np.sqrt(24.0 / n)
+        assert stats.kstest(x[: 1 << 20], "norm").pvalue > 1e-4
+        assert abs(np.corrcoef(x[:-1], x[1:])[0, 1]) < tol
+        assert np.abs(x).max() < 7.0  # u01 never returns 0: the Box-Muller radius is bounded (~5.7)
+
+
+def test_rand_streams_do_not_alias():
+    """Distinct (key, counter) pairs give unrelated streams (the loop derives one key per
+    consumer: policy eps, indices, update eps, env resets)."""
+    from spprl.dp import stream_key
+
+    keys = {stream_key(0, t) for t in ("policy", "index", "update_eps", "env", "env_action")}
+    assert len(keys) == 5
+    n = 1 << 16
+    a = torch.empty(n, device=DEV)
+    b = torch.empty(n, device=DEV)
+    _lib.call("sppRandNormal", _lib.ptr(a), n, stream_key(0, "policy"), 1, _lib.stream_handle())
+    _lib.call("sppRandNormal", _lib.ptr(b), n, stream_key(0, "env"), 1, _lib.stream_handle())
+    x, y = a.cpu().numpy(), b.cpu().numpy()
+    assert abs(np.corrcoef(x, y)[0, 1]) < 6 / np.sqrt(n)
+    assert not np.any(x == y)

@@ -272,3 +272,88 @@ def test_acm_act_given_action_matches_oracle():
     ref = onets.acm(P, torch.cat([obs, ad], 1), ag.ac_lim)
     np.testing.assert_allclose(tgt.cpu().numpy(), ad.numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(env.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------------ advisor round-1 regressions
+def test_default_max_batch_covers_fused_schedule():
+    """SAC_AcM(n_envs=E) without max_batch must size its scratch for rho*E (and sigma*E)."""
+    from spprl import config
+
+    kw = dict(n_envs=4096, grad_steps=50, update_freq=50, acm_update_batches=100, acm_batch_size=100,
+              acm_update_freq=1000)
+    assert config.default_max_batch(100, kw) == 409_600
+    kw = dict(n_envs=8192, acm_update_batches=200, acm_batch_size=128, acm_update_freq=500)
+    assert config.default_max_batch(100, kw) == max(819_200, 419_430)
+    assert config.default_max_batch(100, dict(n_envs=1)) == 128  # reference cadence: B and acm batch
+    assert config.default_max_batch(100, dict(env=_FakeEnv(64), schedule="reference")) == 128
+
+
+def test_dp_obs_stats_count_is_all_reduced_not_assumed():
+    """Under DP the obs-stats call must not assume equal shard lengths (resets advance the
+    obs rings unevenly): the trainer passes no n_global, so the buffer all-reduces it."""
+    calls = []
+
+    class RB(_FakeRB):
+        def update_obs_mean_std_dp(self, allreduce_sum, n_global=None):
+            calls.append(n_global)
+
+    ag = _FakeAgent(n_envs=4)
+    ag.replay_buffer = RB()
+    ag.allreduce_sum = lambda t: t
+    ag.update_obs_stats()
+    assert calls == [None]
+
+
+def test_stream_keys_are_distinct_per_consumer():
+    from spprl.dp import stream_key
+
+    tags = ("policy", "index", "update_eps", "env", "env_action")
+    keys = [stream_key(s, t) for s in (0, 1, 1000, 2000) for t in tags]
+    assert len(set(keys)) == len(keys)
+    assert all(0 <= k < (1 << 63) for k in keys)
+
+
+class _RecordingEnv(_NpSynthEnv):
+    """Records every terminal observation it returns (episode end)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.terminal = []
+
+    def step(self, a):
+        o, r, d, info = super().step(a)
+        if d:
+            self.terminal.append(o.copy())
+        return o, r, d, info
+
+
+@pytest.mark.gpu
+def test_host_env_terminal_next_obs_survives_reset():
+    """A terminal transition's next_obs must be the env's terminal observation even though
+    the reset observation is written to the pinned staging right after (the
+    queued H2D copy used to pick up the reset row)."""
+    from spprl.trainer import HostVecEnv
+
+    envs = [_RecordingEnv(T=5 + 3 * i, seed=i) for i in range(6)]
+    env = HostVecEnv(envs, device="cuda:0")
+    ag = _sac(env=env, max_batch=600, batch_size=60, iterations=3, random_frames=30, buffer_size=10_000)
+    ag.train()
+    torch.cuda.synchronize()
+    rb = ag.replay_buffer
+    n = len(rb)
+    obs, nobs, act, rew, done, acm = rb.gather(torch.arange(n))
+    got = nobs[done.bool()].cpu().numpy()
+    want = np.concatenate([np.stack(e.terminal) for e in envs if e.terminal])
+    assert got.shape == want.shape
+    key = lambda a: a[np.lexsort(a.T[::-1])]  # noqa: E731  (compare as multisets of rows)
+    np.testing.assert_array_equal(key(got), key(want))
+
+
+@pytest.mark.gpu
+def test_agent_with_many_envs_needs_no_max_batch():
+    E = 64
+    ag = _sac(n_envs=E, batch_size=2 * E, iterations=1, random_frames=0)
+    assert ag.max_batch >= 100 * E
+    ag.train()
+    torch.cuda.synchronize()
+    assert all(np.isfinite(v) for v in ag.loss.values())

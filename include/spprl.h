@@ -112,7 +112,9 @@ typedef struct {
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);
 
 /* ------------------------------------------------------------------ agent */
-enum { SPP_ALGO_SAC_ACM = 1, SPP_ALGO_DDPG_ACM = 2 };
+/* SPP_ALGO_SAC: vanilla SAC (rltoolkit/algorithms/sac/sac.py:138-280), BASELINE configs[0]: no ACM,
+ * the actor emits the env action (aout == ac) and feeds the critics directly. */
+enum { SPP_ALGO_SAC_ACM = 1, SPP_ALGO_DDPG_ACM = 2, SPP_ALGO_SAC = 3 };
 enum { /* network ids for parameter binding (SAC_AcM) */
   SPP_NET_ACTOR = 0, SPP_NET_CRITIC1 = 1, SPP_NET_CRITIC2 = 2,
   SPP_NET_CRITIC1_TARG = 3, SPP_NET_CRITIC2_TARG = 4, SPP_NET_ACM = 5,

@@ -28,6 +28,7 @@
 #include "ks_sac_small.hip"
 #include "ks_ddpg.hip"
 #include "ks_sac_bf16.hip"
+#include "ks_sac_vanilla.hip"
 #endif
 #endif
 #include "onp.hip"
@@ -573,6 +574,13 @@ static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, 
     return false;
 #endif
   }
+  if (algo == SPP_ALGO_SAC) {
+#ifndef SPP_ONLY_HOPPER
+    return kset_sac_vanilla(ob, aout, ac, acmc, ks);
+#else
+    return false;
+#endif
+  }
   if (algo == SPP_ALGO_SAC_ACM) {
     if (kset_sac_hopper(ob, aout, ac, acmc, ks)) return true;
 #ifndef SPP_ONLY_HOPPER  // kernel-development builds: one instantiation, fast compile
@@ -604,6 +612,7 @@ struct sppAgent {
   DevArray<float4> pk;     // all matrix images
   std::vector<PackJob> pj_actor, pj_acm, pj_targ, pj_critic_fwd, pj_critic_all, pj_acmreg;
   bool ddpg = false;
+  bool plain = false;  // vanilla SAC (SPP_ALGO_SAC): the ACM net exists but is never evaluated
   DevArray<PackJob> d_pj;
   // job-table offsets inside d_pj
   int o_actor = 0, o_acm = 0, o_targ = 0, o_cfwd = 0, o_call = 0, o_acmreg = 0;
@@ -1106,8 +1115,10 @@ extern "C" {
 
 sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int device) {
   SPP_REQUIRE(out && cfg, SPP_E_INVALID_ARG, "null arg");
-  SPP_REQUIRE(cfg->algo == SPP_ALGO_SAC_ACM || cfg->algo == SPP_ALGO_DDPG_ACM, SPP_E_INVALID_ARG,
-              "unsupported algo %d", cfg->algo);
+  SPP_REQUIRE(cfg->algo == SPP_ALGO_SAC_ACM || cfg->algo == SPP_ALGO_DDPG_ACM || cfg->algo == SPP_ALGO_SAC,
+              SPP_E_INVALID_ARG, "unsupported algo %d", cfg->algo);
+  SPP_REQUIRE(cfg->algo != SPP_ALGO_SAC || (cfg->acm_critic == 0 && cfg->aout == cfg->ac && cfg->custom_loss == 0.f),
+              SPP_E_INVALID_ARG, "vanilla SAC: the actor emits the env action (aout == ac), no ACM critic / loss");
   SPP_REQUIRE(cfg->max_batch > 0, SPP_E_INVALID_ARG, "max_batch must be > 0");
   KernelSet ks;
   SPP_REQUIRE(find_kset(cfg->algo, cfg->ob, cfg->aout, cfg->ac, cfg->acm_critic != 0, cfg->mlp_bf16 != 0, &ks),
@@ -1124,6 +1135,7 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   const int ob = cfg->ob, aout = cfg->aout, ac = cfg->ac;
   a->cin = ob + (cfg->acm_critic ? ac : aout);
   a->ddpg = cfg->algo == SPP_ALGO_DDPG_ACM;
+  a->plain = cfg->algo == SPP_ALGO_SAC;
   const bool dd = a->ddpg;
   a->nsize[SPP_NET_ACTOR] = dd ? ddpg_actor_size(ob, aout) : sac_actor_size(ob, aout);
   a->nsize[SPP_NET_ACTOR_TARG] = dd ? ddpg_actor_size(ob, aout) : 0;
@@ -1633,7 +1645,7 @@ sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* e
   if (s) return s;
   launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size()), st);
   SacArgs p = make_args(a, 32);
-  ActArgs g{E, mode, denorm_out, act_noise, obs, eps, noise, target_out, env_out};
+  ActArgs g{E, mode, denorm_out, act_noise, obs, eps, noise, target_out, env_out, a->plain ? 1 : 0};
   const int grid = std::max(1, std::min(cdiv(cdiv(E, 32), kWavesPerWG), a->num_cu));
   if (a->ddpg)
     hipLaunchKernelGGL(a->ks.dact, dim3(grid), dim3(256), 0, st, p, g, a->bz);

@@ -44,5 +44,6 @@ bool kset_sac_ant(int ob, int aout, int ac, bool acmc, KernelSet* ks);       // 
 bool kset_sac_small(int ob, int aout, int ac, bool acmc, KernelSet* ks);     // ks_sac_small.hip
 bool kset_ddpg(int ob, int aout, int ac, bool acmc, KernelSet* ks);          // ks_ddpg.hip
 bool kset_sac_bf16(int ob, int aout, int ac, bool acmc, KernelSet* ks);      // ks_sac_bf16.hip
+bool kset_sac_vanilla(int ob, int aout, int ac, bool acmc, KernelSet* ks);   // ks_sac_vanilla.hip
 
 }  // namespace spp

@@ -850,6 +850,7 @@ struct ActArgs {
   float act_noise;
   const float *obs, *eps, *noise;  // row-major [E][ob], [E][aout]
   float *target_out, *env_out;     // [E][aout], [E][ac]
+  int plain;  // vanilla SAC (sac.py + DDPG.noise_action, ddpg.py:171-176): no ACM, env action = actor action
 };
 
 template <class C>
@@ -884,7 +885,19 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
         if (j < C::AOUT) {
           const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, j);
           float act;
-          if (a.mode == 0) {
+          if (a.plain && (a.mode == 0 || a.mode == 3)) {
+            act = valid ? a.eps[er * C::AOUT + j] : 0.f;  // action_space.sample() drawn by the caller (ddpg.py:178-180)
+          } else if (a.plain) {  // DDPG.noise_action: a + act_noise * N(0,1), clip to [-lim, lim]
+            const float mu = hd[ib][r];
+            float u = mu;
+            if (a.mode == 1 && a.eps) {
+              const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
+              u = fadd_rn(mu, fmul_rn(valid ? a.eps[er * C::AOUT + j] : 0.f, expf(ls)));
+            }
+            act = fmul_rn(tanhf(u), lim);
+            if (a.mode == 1 && a.noise) act = fadd_rn(act, a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f));
+            act = fminf(fmaxf(act, -lim), lim);
+          } else if (a.mode == 0) {
             act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;  // off_policy.py:50-54
           } else if (a.mode == 3) {
             act = valid ? a.eps[er * C::AOUT + j] : 0.f;  // caller's action (on-policy process_action)
@@ -899,11 +912,13 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
             if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
             act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);  // ddpg_acm.py:43-45
           }
-          if (a.denorm_out) act = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, act);
+          if (a.denorm_out && !a.plain) act = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, act);
           L.pl[j0 * 32] = act;
           if (valid) a.target_out[er * C::AOUT + j] = act;
+          if (valid && a.plain) a.env_out[er * C::AOUT + j] = act;  // process_action: identity (ddpg.py:371-384)
         }
       }
+    if (a.plain) continue;
     // env action = ACM(cat(obs, a))  (off_policy.py:89-106)
     f32x16 xin[C::NB_ACMIN];
     load_cat_gl<C::NB_OB, C::NB_AOUT>(xin, a.obs, a.E * C::OB * 4, C::OB, L.ld4, L.vo, big, C::AOUT);

@@ -6,10 +6,11 @@ include/spprl.h.
 """
 from . import _lib, config, dp, nets, onpolicy, ppo  # noqa: F401
 from ._lib import SppError, load  # noqa: F401
-from .replay import BufferAcMOffPolicy  # noqa: F401
+from .replay import BufferAcMOffPolicy, ReplayBuffer  # noqa: F401
 from .sac_acm import SAC_AcM  # noqa: F401
+from .sac import SAC  # noqa: F401
 from .ddpg_acm import DDPG_AcM  # noqa: F401
 from .ppo_acm import PPO_AcM  # noqa: F401
 from .trainer import HostVecEnv, SynthVecEnv  # noqa: F401
 
-__all__ = ["SAC_AcM", "DDPG_AcM", "PPO_AcM", "SynthVecEnv", "HostVecEnv", "BufferAcMOffPolicy", "SppError", "load"]
+__all__ = ["SAC", "SAC_AcM", "DDPG_AcM", "PPO_AcM", "SynthVecEnv", "HostVecEnv", "BufferAcMOffPolicy", "ReplayBuffer", "SppError", "load"]

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("SPPRL_LIB") or os.path.join(HERE, "libspprl.so")
 
 (SPP_NET_ACTOR, SPP_NET_CRITIC1, SPP_NET_CRITIC2, SPP_NET_CRITIC1_TARG, SPP_NET_CRITIC2_TARG, SPP_NET_ACM,
  SPP_NET_ACTOR_TARG) = range(7)
-SPP_ALGO_SAC_ACM, SPP_ALGO_DDPG_ACM = 1, 2
+SPP_ALGO_SAC_ACM, SPP_ALGO_DDPG_ACM, SPP_ALGO_SAC = 1, 2, 3
 NUM_LOSSES = 8
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,

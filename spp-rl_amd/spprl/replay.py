@@ -200,3 +200,17 @@ class BufferAcMOffPolicy:
              ptr(self.max_obs), ptr(self.obs_mean), ptr(self.obs_std), int(self.min_max_denormalize), int(inverse),
              ptr(out), stream_handle())
         return out
+
+
+class ReplayBuffer(BufferAcMOffPolicy):
+    """ReplayBuffer (rltoolkit/buffer/replay_buffer.py:99-261): the same HBM obs-index ring
+    without the ACM action; ``sample_batch`` returns (obs, next_obs, action, reward, done)."""
+
+    def __init__(self, size, obs_shape, act_shape, device="cuda", **kw):
+        super().__init__(size, obs_shape, act_shape, act_shape, device=device, **kw)
+
+    def gather(self, idx):
+        return super().gather(idx)[:5]
+
+    def sample_acm_batch(self, batch_size=64):
+        raise AttributeError("ReplayBuffer has no ACM actions")

@@ -20,11 +20,14 @@ import torch
 
 from . import _lib, config, nets
 from ._lib import call, ptr, stream_handle
-from .replay import BufferAcMOffPolicy
+from .replay import BufferAcMOffPolicy, ReplayBuffer
 from .trainer import OffPolicyLoop
 
 
 class SAC_AcM(OffPolicyLoop):
+    ALGO = _lib.SPP_ALGO_SAC_ACM
+    VANILLA = False
+
     def __init__(self, env_name="Hopper-v2", gamma=config.GAMMA, actor_lr=config.DDPG_LR,
                  critic_lr=config.DDPG_LR, alpha_lr=config.ALPHA_LR, alpha=config.ALPHA, tau=config.TAU,
                  act_noise=0.0, update_batch_size=config.UPDATE_BATCH_SIZE, buffer_size=config.BUFFER_SIZE,
@@ -34,9 +37,14 @@ class SAC_AcM(OffPolicyLoop):
                  seed=None, mlp_bf16=False, **unused):
         _lib.load()
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
+        vanilla = self.VANILLA
+        if vanilla:  # SAC (sac.py): no ACM anywhere, the actor emits the env action
+            acm_critic, custom_loss, acm_ob_idx = False, 0.0, None
+            unused.setdefault("acm_epochs", 0)
         self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
         self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
-        self.max_ep_len = None  # Q3: AcMOffPolicy never masks time-limit done (off_policy.py:43)
+        # Q3: AcMOffPolicy never masks time-limit done (off_policy.py:43); RL does (rl.py:185)
+        self.max_ep_len = int(max_ep) if vanilla else None
         self.device = torch.device(device)
         self.gamma, self.actor_lr, self.critic_lr, self.alpha_lr, self.acm_lr = gamma, actor_lr, critic_lr, alpha_lr, acm_lr
         self.tau = config.TAU  # Q1: SAC consumes `tau` (sac.py:21) -> DDPG default
@@ -47,9 +55,11 @@ class SAC_AcM(OffPolicyLoop):
         self.acm_ob_idx = list(range(ob)) if acm_ob_idx is None else list(acm_ob_idx)
         if len(self.acm_ob_idx) != ob:
             raise NotImplementedError("acm_ob_idx subsets are not on the device path")
-        self.actor_output_dim = len(self.acm_ob_idx)
+        self.actor_output_dim = ac if vanilla else len(self.acm_ob_idx)
         # acm.py:102-108 actor limit
-        if self.min_max_denormalize:
+        if vanilla:
+            lim = float(ac_high)  # SAC_Actor(ob, self.ac_lim, ac) (sac.py:97)
+        elif self.min_max_denormalize:
             lim = 1.0
         else:
             lim = float(config.MAX_ABS_OBS_VALUE)  # obs spaces of these envs are unbounded
@@ -64,7 +74,7 @@ class SAC_AcM(OffPolicyLoop):
                         _lib.SPP_NET_CRITIC1: nets.critic_layout(cin), _lib.SPP_NET_CRITIC2: nets.critic_layout(cin),
                         _lib.SPP_NET_CRITIC1_TARG: nets.critic_layout(cin),
                         _lib.SPP_NET_CRITIC2_TARG: nets.critic_layout(cin), _lib.SPP_NET_ACM: nets.acm_layout(2 * ob, ac)}
-        cfg = _lib.AgentConfig(_lib.SPP_ALGO_SAC_ACM, ob, aout, ac, int(self.acm_critic), int(self.min_max_denormalize),
+        cfg = _lib.AgentConfig(self.ALGO, ob, aout, ac, int(self.acm_critic), int(self.min_max_denormalize or vanilla),
                                int(self.norm_closs), self.custom_loss, gamma, self.tau, actor_lr, critic_lr, alpha_lr,
                                acm_lr, self.target_entropy, self.max_batch, int(bool(mlp_bf16)))
         self.mlp_bf16 = bool(mlp_bf16)  # bf16 MFMA MLP layers, fp32 everything else (BASELINE configs[4])
@@ -107,9 +117,18 @@ class SAC_AcM(OffPolicyLoop):
         self.alpha_f32 = torch.tensor([alpha], dtype=torch.float32, device=self.device)
         call("sppAgentBindAlpha", self._h, ptr(self.alpha_state), ptr(self.alpha_f32))
         call("sppAgentBindAlphaGrad", self._h, ptr(self.alpha_grad))
-        self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
-                                                min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
-        self.bind_normalizer(self.replay_buffer)
+        if vanilla:
+            if obs_norm:
+                raise NotImplementedError("vanilla SAC with obs_norm=True is not on the device path")
+            self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=False)
+            # identity denormalisation of the actor output: min-max over [-1, 1] is 0 + x * 1, exact
+            self._ident = torch.stack([-torch.ones(ob), torch.ones(ob), torch.zeros(ob), torch.ones(ob)]).to(self.device)
+            call("sppAgentBindNormalizer", self._h, ptr(self._ident[0]), ptr(self._ident[1]), ptr(self._ident[2]),
+                 ptr(self._ident[3]))
+        else:
+            self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
+                                                    min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
+            self.bind_normalizer(self.replay_buffer)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
         self._init_loop(update_batch_size=update_batch_size, **unused)
 

@@ -300,6 +300,7 @@ class OffPolicyLoop:
         self._acm_loss_acc = torch.zeros(1, device=d)
         self._obs = None
         self._prev_slots = None
+        self._ep_len = np.zeros(E, np.int64)  # frames into the current episode, per env (time-limit done, Q3)
 
     # ---------------------------------------------------------- helpers
     def _next(self):
@@ -360,6 +361,7 @@ class OffPolicyLoop:
             self.replay_buffer.update_obs_mean_std()
 
     def _start_episodes(self):
+        self._ep_len[:] = 0
         obs = self.env.reset()
         self._obs = obs
         self._prev_slots = self.replay_buffer.add_obs_batch(obs)
@@ -389,7 +391,11 @@ class OffPolicyLoop:
         E = self.n_envs
         rb = self.replay_buffer
         mode = 0 if self.stats_logger.frames < self.random_frames else 1  # initial_act (off_policy.py:50-54)
-        self._randn(self._eps)
+        vanilla = getattr(self, "VANILLA", False)
+        if mode == 0 and vanilla:
+            self.env.sample_actions(self._eps)  # DDPG.initial_act: env.action_space.sample() (ddpg.py:178-180)
+        else:
+            self._randn(self._eps)
         if mode == 1:
             self._randn(self._noise)
         obs_in = rb.normalize(self._obs)
@@ -405,8 +411,19 @@ class OffPolicyLoop:
         call("sppEpisodeAccum", ptr(rew), ptr(end_dev) if any_end else None, E, ptr(self._ep_ret),
              ptr(self._ret_sums), stream_handle())
         slots = rb.add_obs_batch(nobs)
-        # AcMOffPolicy keeps max_ep_len None: done == end (Q3, off_policy.py:43, ddpg.py:210-211)
-        rb.add_timestep_batch(self._prev_slots, slots, tgt, rew, end_dev, end_dev, env_act)
+        # done = end, except at the time limit when max_ep_len is set (Q3, ddpg.py:210-212);
+        # AcMOffPolicy keeps max_ep_len None (off_policy.py:43)
+        done_dev = end_dev
+        max_ep = getattr(self, "max_ep_len", None)
+        if max_ep is not None:
+            self._ep_len += 1
+            if any_end:
+                done_h = end & (self._ep_len != max_ep)
+                done_dev = torch.from_numpy(done_h.astype(np.uint8)).to(self.device, non_blocking=False)
+            else:
+                done_dev = end_dev  # all zero
+            self._ep_len[end] = 0
+        rb.add_timestep_batch(self._prev_slots, slots, tgt, rew, done_dev, end_dev, None if vanilla else env_act)
         self._prev_slots = slots
         self._obs = nobs
         self.stats_logger.frames += E

@@ -94,6 +94,10 @@ sys.modules["pyvirtualdisplay"] = pvd
 sys.path.insert(0, "/root/reference/rltoolkit")
 
 from rltoolkit.acm.models.basic_acm import BasicAcM  # noqa: E402
+from rltoolkit.acm.on_policy import PPO_AcM  # noqa: E402
+from rltoolkit.algorithms import A2C, SAC  # noqa: E402
+from rltoolkit.basic_model import Actor  # noqa: E402
+from rltoolkit.buffer import MemoryAcM  # noqa: E402
 from rltoolkit.acm.off_policy import DDPG_AcM, SAC_AcM  # noqa: E402
 from rltoolkit.algorithms.ppo.ppo import PPO  # noqa: E402
 from rltoolkit.buffer import BufferAcMOffPolicy, Memory  # noqa: E402
@@ -423,11 +427,125 @@ def gen_ppo(seed=31):
     save("ppo_gae_clip.npz", **out)
 
 
+# ---------------------------------------------------------------- vanilla SAC.update (configs[0])
+def gen_sac_vanilla(seed=41, B=100, steps=2):
+    """SAC.update (rltoolkit/algorithms/sac/sac.py:218-280) at HalfCheetah dims: no ACM, the
+    actor emits the env action (ac = 6), the critics take cat(obs, action)."""
+    torch.manual_seed(0)
+    m = SAC(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2,
+            buffer_size=1000, update_batch_size=B, use_gpu=False)
+    ob, ac = m.ob_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic_1": m._critic_1, "critic_2": m._critic_2,
+            "critic_1_targ": m.critic_1_targ, "critic_2_targ": m.critic_2_targ}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    out = dict(dims=np.array([ob, ac, B]), seed=np.array(seed), ac_lim=m.ac_lim.numpy().astype(np.float32),
+               alpha0=np.array(m.alpha), target_entropy=np.array(m.target_entropy), tau=np.array(m.tau),
+               gamma=np.array(m.gamma), act_noise=np.array(m.act_noise),
+               max_ep_len=np.array(m.max_ep_len if m.max_ep_len is not None else -1))
+    losses = []
+    for s in range(steps):
+        obs, next_obs, act, rew, done, _ = make_batch(rng, B, ob, ac, ac)
+        act = np.clip(act, -1, 1)
+        EPS.q = [rng.randn(B, ac).astype(np.float32), rng.randn(B, ac).astype(np.float32)]
+        m.update(torch.from_numpy(obs), torch.from_numpy(next_obs), torch.from_numpy(act), torch.from_numpy(rew),
+                 torch.from_numpy(done))
+        assert not EPS.q
+        losses.append([m.loss[k] for k in ("critic_1", "critic_2", "actor")])
+    out["losses"] = np.array(losses)
+    out["log_alpha"] = np.array(float(m.log_alpha))
+    out["alpha"] = np.array(m.alpha)
+    for k, mod in nets.items():
+        out["post_" + k] = flat_params(mod)
+    save("sac_vanilla_hcheetah.npz", **out)
+
+
+# ---------------------------------------------------------------- on-policy (A2C / PPO_AcM)
+def onp_batch(rng, N, ob):
+    obs = (rng.randn(N, ob) * 1.2).astype(np.float32)
+    nobs = (rng.randn(N, ob) * 1.2).astype(np.float32)
+    rew = rng.randn(N).astype(np.float32)
+    done = (rng.rand(N) < 0.05).astype(np.float32)
+    return obs, nobs, rew, done
+
+
+def gen_onpolicy(seed=51):
+    """Actor.act log-prob (basic_model.py:32-51), A2C.update_critic (a2c.py:186-225) and one
+    PPO_AcM.update_actor_acm epoch over a single full-batch minibatch (acm/on_policy.py:164-216)."""
+    out = {}
+    ob = 17
+    rng = np.random.RandomState(seed)
+    # ---- Actor.act: sampled and deterministic actions, log-probs
+    torch.manual_seed(seed)
+    actor = Actor(ob, torch.ones(ob), ob, discrete=False)
+    load(actor, seed * 100)
+    with torch.no_grad():
+        actor.log_scale.add_(torch.from_numpy(rng.uniform(-0.3, 0.3, ob).astype(np.float32)))
+    x = (rng.randn(257, ob) * 1.3).astype(np.float32)
+    a_s, lp_s = actor.act(torch.from_numpy(x))
+    a_d, lp_d = actor.act(torch.from_numpy(x), deterministic=True)
+    out.update(act_params=flat_params(actor), act_x=x, act_a=a_s.numpy(), act_lp=lp_s.detach().numpy(),
+               act_mu=a_d.numpy(), act_lp_det=lp_d.detach().numpy())
+    # ---- A2C.update_critic: 10 targets x 10 full-batch Adam steps on 0.5 * adv^2
+    torch.manual_seed(seed + 1)
+    a2c = A2C(env_name="HalfCheetah-v2", gamma=0.99, critic_lr=3e-4, use_gpu=False)
+    load(a2c.critic, seed * 100 + 1)
+    c0 = flat_params(a2c.critic)
+    N = 300
+    obs, nobs, rew, done = onp_batch(rng, N, ob)
+    buf = Memory()
+    prev = buf.add_obs(torch.from_numpy(obs[:1]))
+    for i in range(N):  # one transition per rollout: obs_i -> next_obs_i
+        if i:
+            buf.new_rollout()
+            prev = buf.add_obs(torch.from_numpy(obs[i:i + 1]))
+        nxt = buf.add_obs(torch.from_numpy(nobs[i:i + 1]))
+        buf.add_timestep(prev, nxt, torch.zeros(1, ob), torch.zeros(1), float(rew[i]), bool(done[i]), True)
+    buf.end_rollout()
+    assert np.array_equal(buf.norm_obs.numpy(), obs) and np.array_equal(buf.norm_next_obs.numpy(), nobs)
+    adv = a2c.update_critic(buf)
+    out.update(crit_params0=c0, crit_obs=obs, crit_nobs=nobs, crit_rew=rew, crit_done=done,
+               crit_loss=np.array(a2c.loss["critic"]), crit_adv=adv.numpy(), crit_post=flat_params(a2c.critic),
+               crit_lr=np.array(3e-4), crit_gamma=np.array(0.99))
+    # ---- PPO_AcM.update_actor_acm: one epoch, one minibatch of the whole buffer
+    torch.manual_seed(seed + 2)
+    ppo = PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, custom_loss=0.1,
+                  norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True, ppo_batch_size=N,
+                  max_ppo_epochs=1, entropy_coef=0.01, acm_pre_train_samples=10, use_gpu=False)
+    load(ppo.actor, seed * 100 + 2)
+    p0 = flat_params(ppo.actor)
+    mem = MemoryAcM(min_max_denormalize=True)
+    acts = rng.uniform(-1.1, 1.1, (N, ob)).astype(np.float32)
+    with torch.no_grad():
+        lp_cur = ppo.actor.get_actions_dist(torch.from_numpy(obs)).log_prob(torch.from_numpy(acts)).numpy()
+    lp_old = (lp_cur + 0.2 * rng.randn(N)).astype(np.float32)
+    adv_in = (rng.randn(N) * 2 + 0.5).astype(np.float32)
+    prev = mem.add_obs(torch.from_numpy(obs[:1]))
+    for i in range(N):
+        if i:
+            mem.new_rollout()
+            prev = mem.add_obs(torch.from_numpy(obs[i:i + 1]))
+        nxt = mem.add_obs(torch.from_numpy(nobs[i:i + 1]))
+        mem.add_timestep(prev, nxt, torch.from_numpy(acts[i:i + 1]), torch.from_numpy(lp_old[i:i + 1]),
+                         float(rew[i]), bool(done[i]), True)
+    mem.end_rollout()
+    ppo.update_actor_acm(torch.from_numpy(adv_in), mem)
+    out.update(ppo_params0=p0, ppo_acts=acts, ppo_lp_old=lp_old, ppo_adv=adv_in, ppo_post=flat_params(ppo.actor),
+               ppo_losses=np.array([ppo.loss[k] for k in ("actor", "entropy", "policy", "dist")]),
+               ppo_lr=np.array(3e-4), ppo_eps=np.array(ppo.ppo_epsilon), ppo_entropy_coef=np.array(0.01),
+               ppo_custom_loss=np.array(0.1))
+    save("onpolicy_hcheetah.npz", **out)
+
+
+GROUPS = {"randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
+          "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy}
+
 if __name__ == "__main__":
-    gen_randint()
-    gen_replay()
-    for i, (name, (env, B, flags, steps, adam)) in enumerate(SAC_VARIANTS.items()):
-        gen_sac(name, env, B, flags, steps, adam, seed=1 + i)
-    gen_ddpg()
-    gen_acm()
-    gen_ppo()
+    which = sys.argv[1:] or list(GROUPS) + ["sac"]
+    for g in which:
+        if g == "sac":
+            for i, (name, (env, B, flags, steps, adam)) in enumerate(SAC_VARIANTS.items()):
+                gen_sac(name, env, B, flags, steps, adam, seed=1 + i)
+        else:
+            GROUPS[g]()

@@ -74,3 +74,34 @@ def ddpg_case():
     norm = Norm(True, torch.from_numpy(lo), torch.from_numpy(hi))
     batches = [make_batch(rng, B, ob, aout, ac) for _ in range(2)]
     return fx, params, layouts, norm, batches
+
+
+def sac_vanilla_case():
+    """Vanilla SAC (HalfCheetah, configs[0]): (fixture, params, steps[(batch5, eps1, eps2)])."""
+    fx = load("sac_vanilla_hcheetah")
+    ob, ac, B = (int(v) for v in fx["dims"])
+    seed = int(fx["seed"])
+    layouts = {"actor": nets.sac_actor_layout(ob, ac), "critic_1": nets.critic_layout(ob + ac),
+               "critic_2": nets.critic_layout(ob + ac), "critic_1_targ": nets.critic_layout(ob + ac),
+               "critic_2_targ": nets.critic_layout(ob + ac)}
+    params = {k: fill_params(lay, seed * 100 + i) for i, (k, lay) in enumerate(layouts.items())}
+    rng = np.random.RandomState(seed)
+    steps = []
+    for _ in range(len(fx["losses"])):
+        obs, next_obs, act, rew, done, _ = make_batch(rng, B, ob, ac, ac)
+        act = np.clip(act, -1, 1)
+        e1 = rng.randn(B, ac).astype(np.float32)
+        e2 = rng.randn(B, ac).astype(np.float32)
+        steps.append(((obs, next_obs, act, rew, done), e1, e2))
+    return fx, params, steps
+
+
+def onpolicy_case():
+    """A2C / PPO_AcM fixture (tests/golden/onpolicy_hcheetah.npz): every input is stored."""
+    return load("onpolicy_hcheetah")
+
+
+def normalize_adv_ref(adv):
+    """AdvantageDataset normalisation (advantage_dataset.py:8-12): torch.std is unbiased."""
+    a = torch.as_tensor(adv)
+    return ((a - a.mean()) / (a.std() + 1.2e-7)).numpy()

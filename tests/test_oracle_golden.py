@@ -179,3 +179,91 @@ def test_clip_loss_reference_kat(case):
     """KATs of rltoolkit/algorithms/ppo/test/test_ppo.py:34-76."""
     old, new, adv, want = case
     assert clip_loss(np.float32(old), np.float32(new), np.float32(adv)) == pytest.approx(want, rel=1e-4)
+
+
+# ------------------------------------------------------------------ vanilla SAC (configs[0])
+def test_vanilla_sac_update_matches_reference():
+    from golden_cases import sac_vanilla_case
+    from oracle.sac import OracleSac
+
+    fx, params, steps = sac_vanilla_case()
+    ob, ac, B = (int(v) for v in fx["dims"])
+    assert float(fx["act_noise"]) == 0.1 and float(fx["tau"]) == 0.005  # quirk Q1
+    assert int(fx["max_ep_len"]) == 1000  # quirk Q3: time-limit ends are not done
+    o = OracleSac(ob, ac, ac_lim=fx["ac_lim"], gamma=float(fx["gamma"]), tau=float(fx["tau"]),
+                  alpha=float(fx["alpha0"]), params=params)
+    for i, (batch, e1, e2) in enumerate(steps):
+        losses = o.update(*batch, e1, e2)
+        np.testing.assert_allclose([losses[k] for k in ("critic_1", "critic_2", "actor")], fx["losses"][i],
+                                   rtol=1e-6, atol=1e-7)
+    for k in ("actor", "critic_1", "critic_2", "critic_1_targ", "critic_2_targ"):
+        np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-6, atol=1e-7, err_msg=k)
+    assert o.alpha == pytest.approx(float(fx["alpha"]), rel=1e-12)
+
+
+# ------------------------------------------------------------------ on-policy (rows a21, a22, a24)
+def test_onpolicy_actor_act_logprob_matches_reference():
+    from golden_cases import onpolicy_case
+    from oracle import onpolicy as oo
+
+    fx = onpolicy_case()
+    ob = fx["act_x"].shape[1]
+    flat = fx["act_params"]
+    sc = np.exp(flat[:ob].astype(np.float64))
+    mu_ref = fx["act_mu"]
+    eps = ((fx["act_a"] - mu_ref) / sc).astype(np.float32)  # the reference's normal draws, recovered
+    a, lp = oo.act(flat, ob, ob, np.ones(ob, np.float32), fx["act_x"], eps)
+    np.testing.assert_allclose(a, fx["act_a"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(lp, fx["act_lp"], rtol=1e-5, atol=1e-4)
+    a, lp = oo.act(flat, ob, ob, np.ones(ob, np.float32), fx["act_x"], None)
+    np.testing.assert_allclose(a, mu_ref, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(lp, fx["act_lp_det"], rtol=1e-6, atol=1e-5)
+
+
+def test_onpolicy_update_critic_matches_reference():
+    from golden_cases import onpolicy_case
+    from oracle import onpolicy as oo
+    from oracle.adam import OracleAdam
+
+    fx = onpolicy_case()
+    ob = fx["crit_obs"].shape[1]
+    flat = torch.from_numpy(fx["crit_params0"].copy())
+    opt = OracleAdam([flat], float(fx["crit_lr"]))
+    g = float(fx["crit_gamma"])
+    rew, done = torch.from_numpy(fx["crit_rew"]), torch.from_numpy(fx["crit_done"])
+    total = 0.0
+    for _ in range(10):
+        with torch.no_grad():
+            vn = oo.critic(oo._params(flat.numpy(), oo.critic_layout(ob)), torch.from_numpy(fx["crit_nobs"]))
+        q = (rew + g * (1 - done) * vn.squeeze(-1)).numpy()
+        for _ in range(10):
+            loss, grad = oo.critic_step(flat.numpy(), ob, fx["crit_obs"], q)
+            opt.step([torch.from_numpy(grad)])
+            total += loss
+    assert total / 100 == pytest.approx(float(fx["crit_loss"]), rel=1e-5)
+    np.testing.assert_allclose(flat.numpy(), fx["crit_post"], rtol=1e-5, atol=1e-6)
+    P = oo._params(flat.numpy(), oo.critic_layout(ob))
+    with torch.no_grad():
+        q = rew + g * (1 - done) * oo.critic(P, torch.from_numpy(fx["crit_nobs"])).squeeze(-1)
+        adv = q - oo.critic(P, torch.from_numpy(fx["crit_obs"])).squeeze(-1)
+    np.testing.assert_allclose(adv.numpy(), fx["crit_adv"], rtol=1e-5, atol=1e-5)
+
+
+def test_onpolicy_ppo_acm_actor_step_matches_reference():
+    from golden_cases import normalize_adv_ref, onpolicy_case
+    from oracle import onpolicy as oo
+    from oracle.adam import OracleAdam
+
+    fx = onpolicy_case()
+    ob = fx["crit_obs"].shape[1]
+    adv = normalize_adv_ref(fx["ppo_adv"])
+    out, g = oo.actor_step(fx["ppo_params0"], ob, ob, np.ones(ob, np.float32), fx["crit_obs"], fx["ppo_acts"],
+                           fx["ppo_lp_old"], adv, eps_clip=float(fx["ppo_eps"]),
+                           entropy_coef=float(fx["ppo_entropy_coef"]), next_obs=fx["crit_nobs"])
+    policy = out["actor"] - float(fx["ppo_entropy_coef"]) * out["entropy"] + float(fx["ppo_custom_loss"]) * out["dist"]
+    np.testing.assert_allclose([out["actor"], out["entropy"], policy, out["dist"]], fx["ppo_losses"], rtol=1e-5,
+                               atol=1e-6)
+    flat = torch.from_numpy(fx["ppo_params0"].copy())
+    OracleAdam([flat], float(fx["ppo_lr"])).step([torch.from_numpy(g)])
+    d = np.abs(flat.numpy() - fx["ppo_post"])
+    assert d.max() < 1e-6, d.max()

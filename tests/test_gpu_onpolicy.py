@@ -1,6 +1,7 @@
 """GPU parity of the on-policy (A2C / PPO) network kernels
 against the oracle restatement of rltoolkit/basic_model.py Actor / Critic
-(oracle/onpolicy.py; parity pinned by the oracle, which follows the reference modules line by line)."""
+(oracle/onpolicy.py) and the reference fixture tests/golden/onpolicy_hcheetah.npz (Actor.act,
+A2C.update_critic, PPO_AcM.update_actor_acm run by the reference itself)."""
 import numpy as np
 import pytest
 import torch
@@ -116,3 +117,72 @@ def test_update_loops_run_and_improve(nets):
     kl = nets.update_actor(adv, obs, act, lp, generator=torch.Generator().manual_seed(0))
     assert np.isfinite(kl)
     assert all(torch.isfinite(p).all() for p in nets.params)
+
+
+# ------------------------------------------------------------------ pinned by reference fixtures
+# tests/golden/onpolicy_hcheetah.npz (make_golden.py gen_onpolicy): the reference's own Actor.act,
+# A2C.update_critic and PPO_AcM.update_actor_acm on fixed inputs.
+def _fx():
+    from golden_cases import onpolicy_case
+
+    return onpolicy_case()
+
+
+def test_act_matches_reference_fixture():
+    """basic_model.Actor.act (basic_model.py:32-51): sampled action and Independent-Normal log-prob,
+    and the deterministic mean; the reference's normal draws are recovered from its sampled actions."""
+    from spprl.onpolicy import OnPolicyNets
+
+    fx = _fx()
+    ob = fx["act_x"].shape[1]
+    n = OnPolicyNets(ob, ob, ac_lim=1.0, max_batch=512, device=DEV)
+    n.load_net(0, fx["act_params"])
+    sc = np.exp(fx["act_params"][:ob].astype(np.float64))
+    eps = ((fx["act_a"] - fx["act_mu"]) / sc).astype(np.float32)
+    a, lp = n.act(fx["act_x"], eps)
+    np.testing.assert_allclose(a.cpu().numpy(), fx["act_a"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(lp.cpu().numpy(), fx["act_lp"], rtol=1e-5, atol=2e-4)
+    a, lp = n.act(fx["act_x"], None)
+    np.testing.assert_allclose(a.cpu().numpy(), fx["act_mu"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(lp.cpu().numpy(), fx["act_lp_det"], rtol=1e-5, atol=2e-4)
+
+
+def test_update_critic_matches_reference_fixture():
+    """A2C.update_critic (a2c.py:186-225): 10 targets x 10 full-batch Adam steps on 0.5 * adv^2, then
+    calculate_advantage.  100 sequential Adam steps: parameters within 5e-6 + 1e-4 relative."""
+    from spprl.onpolicy import OnPolicyNets
+
+    fx = _fx()
+    ob = fx["crit_obs"].shape[1]
+    n = OnPolicyNets(ob, ob, critic_lr=float(fx["crit_lr"]), gamma=float(fx["crit_gamma"]), max_batch=512, device=DEV)
+    n.load_net(1, fx["crit_params0"])
+    adv = n.update_critic(fx["crit_obs"], fx["crit_nobs"], fx["crit_rew"], fx["crit_done"])
+    torch.cuda.synchronize()
+    assert n.loss["critic"] == pytest.approx(float(fx["crit_loss"]), rel=1e-4)
+    np.testing.assert_allclose(n.params[1].cpu().numpy(), fx["crit_post"], rtol=1e-4, atol=5e-6)
+    np.testing.assert_allclose(adv.cpu().numpy(), fx["crit_adv"], rtol=1e-4, atol=1e-4)
+
+
+def test_ppo_acm_actor_epoch_matches_reference_fixture():
+    """PPO_AcM.update_actor_acm (acm/on_policy.py:164-216) with one epoch of one full-batch
+    minibatch: normalised advantages, clip loss - entropy_coef * entropy, Adam step.  First Adam
+    step moves each weight by ~lr * sign(g): |d| <= 2 lr, rare beyond 1e-6."""
+    from spprl.onpolicy import OnPolicyNets
+
+    fx = _fx()
+    obs, nobs = fx["crit_obs"], fx["crit_nobs"]
+    N, ob = obs.shape
+    n = OnPolicyNets(ob, ob, actor_lr=float(fx["ppo_lr"]), ppo_epsilon=float(fx["ppo_eps"]),
+                     entropy_coef=float(fx["ppo_entropy_coef"]), max_ppo_epochs=1, ppo_batch_size=N,
+                     normalize_adv=True, max_batch=512, device=DEV)
+    n.load_net(0, fx["ppo_params0"])
+    n.update_actor(fx["ppo_adv"], obs, fx["ppo_acts"], fx["ppo_lp_old"], nobs,
+                   generator=torch.Generator().manual_seed(0))
+    torch.cuda.synchronize()
+    actor, entropy, policy, dist = (float(v) for v in fx["ppo_losses"])
+    assert n.loss["actor"] == pytest.approx(actor, rel=1e-4, abs=1e-6)
+    assert n.loss["entropy"] == pytest.approx(entropy, rel=1e-5)
+    d = np.abs(n.params[0].cpu().numpy() - fx["ppo_post"])
+    lr = float(fx["ppo_lr"])
+    assert d.max() <= 2 * lr * 1.01, d.max()
+    assert np.mean(d > 1e-6) < 2e-3, np.mean(d > 1e-6)

@@ -10,20 +10,33 @@ loop (spprl.trainer.OffPolicyLoop, fused schedule), all on devic
             rho = update_batch_size*grad_steps/update_freq = 100 (train/spp_*.py)
   ACM       sigma*E samples, one AcMTrainer regression step                  acm.py:246-258, 356-372
             sigma = acm_update_batches*acm_batch_size/acm_update_freq (10 SAC, 51.2 DDPG)
-  stats     update_obs_mean_std over the live replay rows                    replay_buffer.py:83-96
+  stats     update_obs_mean_std over the live replay rows at the reference's rate: one pass per
+            batch_size = 1000 frames (ddpg.py:159-170), i.e. floor(frames / 1000) passes so far
 FLOPs per env-step equal the reference cadence (one grad step of 100 samples per env step).
 
 --config sac_hopper (default; BASELINE.json configs[1]: SPP-SAC Hopper-v2, 4096 envs, fp32)
          ddpg_hcheetah (configs[2]: SPP-DDPG HalfCheetah-v2, 8192 envs, 10M-transition HBM replay)
-         sac_ant (configs[4] per-GPU shape: SPP-SAC Ant, 32768 envs / 8 GPUs = 4096 per GPU, fp32 MLP)
+         sac_ant / sac_ant_bf16 (configs[4] per-GPU shape: 32768 envs / 8 GPUs = 4096, fp32 / bf16 MLP)
+         ppo_hcheetah (configs[3] per-GPU shape: 16384 envs / 8 GPUs = 2048, one PPO_AcM iteration per step)
+         vanilla_sac_hcheetah (configs[0]: vanilla SAC, 1 env, the reference cadence frame by frame;
+                               one step = one frame)
 N > 1: one process per GPU (torchrun), each with E envs and a local replay shard; gradient
 buckets are averaged with RCCL all-reduce at the update's exchange points (critic grads,
 actor grads, ACM grads); value = all ranks' env-steps / max-over-ranks time.
+
+Roofline: the dominant kernel's algorithmic FLOPs per launch / its average HIP-event launch
+time inside the timed region.  traffic: HBM bytes per launch of that kernel from two
+rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this same
+script, config, E and library (N = 1 only; null when rocprofv3 is absent or --no-pmc).
 """
 import argparse
+import hashlib
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -38,15 +51,16 @@ import torch.distributed as dist  # noqa: E402
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA peak
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
+LIB = os.path.join(REPO, "spp-rl_amd", "spprl", "libspprl.so")
 
+SAC_AGENT = dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
+                 custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                 update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
+                 acm_update_batches=100, acm_batch_size=100, batch_size=1000)
 CONFIGS = {
     "sac_hopper": dict(
         algo="sac", env="Hopper-v2", ob=11, ac=3, envs=4096, buffer=1_000_000, baseline_idx=1,
-        workload="SPP-SAC Hopper-v2, %d vectorized envs per GPU, fp32 (BASELINE.json configs[1])",
-        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
-                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
-                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
-                   acm_update_batches=100, acm_batch_size=100)),
+        workload="SPP-SAC Hopper-v2, %d vectorized envs per GPU, fp32 (BASELINE.json configs[1])", agent=SAC_AGENT),
     "ddpg_hcheetah": dict(
         algo="ddpg", env="HalfCheetah-v2", ob=17, ac=6, envs=8192, buffer=10_000_000, baseline_idx=2,
         workload="SPP-DDPG HalfCheetah-v2, %d vectorized envs per GPU, 10M-transition HBM replay, fp32 "
@@ -54,139 +68,235 @@ CONFIGS = {
         agent=dict(gamma=0.95, actor_lr=5e-4, critic_lr=5e-4, acm_lr=0.005, act_noise=0.05, acm_critic=True,
                    custom_loss=1.0, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
                    update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=500,
-                   acm_update_batches=200, acm_batch_size=128)),
+                   acm_update_batches=200, acm_batch_size=128, batch_size=1000)),
     "sac_ant_bf16": dict(
         algo="sac", env="Ant-v2", ob=111, ac=8, envs=4096, buffer=1_000_000, baseline_idx=4, bf16=True,
         workload="SPP-SAC Ant (111-dim obs), %d vectorized envs per GPU, bf16 MFMA MLP + fp32 targets "
-                 "(BASELINE.json configs[4] per-GPU shape)",
-        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
-                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
-                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
-                   acm_update_batches=100, acm_batch_size=100, mlp_bf16=True)),
+                 "(BASELINE.json configs[4] per-GPU shape)", agent=dict(SAC_AGENT, mlp_bf16=True)),
     "sac_ant": dict(
         algo="sac", env="Ant-v2", ob=111, ac=8, envs=4096, buffer=1_000_000, baseline_idx=4,
         workload="SPP-SAC Ant (111-dim obs), %d vectorized envs per GPU, fp32 MLP (BASELINE.json configs[4] "
-                 "per-GPU shape)",
-        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, acm_lr=1e-3, acm_critic=True,
-                   custom_loss=0.2, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
-                   update_batch_size=100, update_freq=50, grad_steps=50, acm_update_freq=1000,
-                   acm_update_batches=100, acm_batch_size=100)),
+                 "per-GPU shape)", agent=SAC_AGENT),
+    "vanilla_sac_hcheetah": dict(
+        algo="vanilla", env="HalfCheetah-v2", ob=17, ac=6, envs=1, buffer=1_000_000, baseline_idx=0,
+        workload="vanilla SAC HalfCheetah-v2, 1 env, reference cadence (B=100, 50 grad steps every 50 frames) "
+                 "(BASELINE.json configs[0], train/vanilla_sac_hcheetah.py)",
+        agent=dict(gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2, update_batch_size=100,
+                   update_freq=50, grad_steps=50, batch_size=1000)),
 }
+DEFAULT_STEPS = {"vanilla_sac_hcheetah": (2000, 100), "ppo_hcheetah": (30, 3)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; vanilla: 2000 frames)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10)")
     ap.add_argument("--config", default="sac_hopper", choices=sorted(CONFIGS) + ["ppo_hcheetah"])
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=None)
+    ap.add_argument("--stats-rate", choices=["reference", "per-step"], default="reference",
+                    help="obs-stats passes: one per 1000 frames (reference) or one per vector step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-procs", type=int, default=min(8, os.cpu_count() or 1),
-                    help="concurrent 1-thread oracle processes for the CPU baseline (reference N_CORES)")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="concurrent 1-thread reference-loop processes (default: the host's CPU share, max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic null)")
+    a = ap.parse_args()
+    st, wu = DEFAULT_STEPS.get(a.config, (200, 10))
+    a.steps = st if a.steps is None else a.steps
+    a.warmup = wu if a.warmup is None else a.warmup
+    return a
 
 
-def cpu_baseline(cfg, seconds):
-    """The oracle (CPU restatement of the reference update path, torch 1 thread) run at
-    the reference cadence: per env step one policy act and one grad step of B=100; the
-    ACM regression at its reference rate (sigma/100 batches of 100 per env step); one
-    obs-stats pass over a 1e6-row buffer amortised over an iteration of 1000 frames."""
-    import oracle.nets as onets
-    from oracle.nets import Norm
-    from tests.golden.weights import fill_params
+# ------------------------------------------------------------------ CPU baseline (the reference's N_CORES path)
+def _cpu_worker(args):
+    name, seconds = args
+    return cpu_baseline(name, seconds)
+
+
+def cpu_baseline(name, seconds):
+    """One 1-thread process of the reference's CPU training loop (oracle/cpu_loop.py: the
+    per-frame DDPG.collect_batch_and_train loop with act, env step, fp64 replay ring,
+    sample_batch, the update, the ACM batches and the per-iteration obs statistics)."""
+    from oracle.cpu_loop import CpuLoop
 
     torch.set_num_threads(1)
-    rng = np.random.RandomState(0)
+    cfg = CONFIGS[name]
+    a = cfg["agent"]
+    algo = {"sac": "sac_acm", "ddpg": "ddpg_acm", "vanilla": "sac"}[cfg["algo"]]
+    L = CpuLoop(algo, cfg["ob"], cfg["ac"], update_batch_size=a["update_batch_size"], update_freq=a["update_freq"],
+                grad_steps=a["grad_steps"], acm_update_freq=a.get("acm_update_freq", 1),
+                acm_update_batches=a.get("acm_update_batches", 0), acm_batch_size=a.get("acm_batch_size", 100),
+                batch_size=10 ** 12, buffer_size=1_000_000, prefill=990_000)
+    t0 = time.perf_counter()
+    L._obs_stats()  # one update_obs_mean_std over the 990K-row buffer, amortised over batch_size frames
+    t_stats = time.perf_counter() - t0
+    fps, n, el = L.run(seconds)
+    per = 1.0 / fps + t_stats / a["batch_size"]
+    return {"value": round(1.0 / per, 2), "frames": n, "seconds": round(el, 2), "stats_s": round(t_stats, 3)}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_report(name, seconds, procs):
+    """The reference's N_CORES layout (train/spp_*.py: a multiprocessing pool of independent
+    1-thread runs, evals.py:22-26), on the GPU box's host cores, plus a 1-core run alone."""
+    import multiprocessing as mp
+
+    one = cpu_baseline(name, seconds)
+    # the workers are CPU-only: hide the GPUs from them (the box counts GPU-using processes)
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    for k in saved:
+        os.environ[k] = "-1"
+    try:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, [(name, seconds)] * procs)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    vals = [r["value"] for r in res]
+    ref_per_core = {"sac": 103.4, "vanilla": 113.3}.get(CONFIGS[name]["algo"])
+    out = {"value": round(sum(vals), 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
+           "per_core": round(sum(vals) / procs, 2), "one_core": one["value"], "cpu_model": _cpu_model(),
+           "cores_note": "the box's CPU share is 16 and at most 16 processes may hold the GPU runtime (this "
+                         "process included), so the pool is 15 single-thread workers",
+           "sample": "%d concurrent 1-thread processes of the reference's per-frame training loop restated on the "
+                     "CPU (oracle/cpu_loop.py: act, SynthEnv step, fp64 replay ring, sample_batch, B=100 grad steps "
+                     "at the reference cadence, ACM batches, obs stats of a 990K-row buffer per 1000 frames), "
+                     "%.0f s each (%d frames per process); one_core = the same loop alone"
+                     % (procs, seconds, res[0]["frames"])}
+    if ref_per_core:
+        out["reference_per_core_measured_in_survey"] = ref_per_core
+        out["port_vs_reference_per_core"] = round(one["value"] / ref_per_core, 3)
+    return out
+
+
+def default_cpu_procs():
+    # The GPU box gives one job a 16-CPU share (os.cpu_count() reports the whole machine there)
+    # and counts every process that imports the ROCm torch runtime as a GPU user (at most 16,
+    # the bench's own process included): 15 workers.
+    n = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    return max(1, min(15, n - 1))
+
+
+# ------------------------------------------------------------------ PMC traffic (child passes)
+def lib_digest():
+    h = hashlib.sha1()
+    with open(LIB, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:12]
+
+
+def pmc_traffic(args, E, cap, kernels):
+    """HBM bytes per launch of ``kernels`` (name prefixes) from two rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE; counters cannot share a pass) over a short child run of this
+    script at the same config / E / buffer.  FETCH_SIZE is doubled: gfx950 counts half the
+    bytes of wide streaming reads (MI355X_MICROARCH.md "HBM"); both are KB -> x1024."""
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    per = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="spp_pmc_", dir="/tmp")
+        cmd = ["timeout", "-s", "KILL", "240", rp, "--pmc", c, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--config", args.config, "--envs", str(E), "--buffer",
+               str(cap), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            return None, "rocprofv3 --pmc %s exit %d: %s" % (c, r.returncode, r.stdout[-300:])
+        import csv
+        import glob
+
+        files = glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True)
+        if not files:
+            return None, "no counter csv"
+        vals = {}
+        for row in csv.DictReader(open(files[0])):
+            for k in kernels:
+                if k in row["Kernel_Name"]:
+                    vals.setdefault(k, []).append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        for k, v in vals.items():
+            per.setdefault(k, {})[c] = sum(v) / len(v) * 1024.0
+    out = {}
+    for k, d in per.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            out[k] = int(2 * d["FETCH_SIZE"] + d["WRITE_SIZE"])
+    return out, "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py --config %s " \
+                "--envs %d --steps 2 --warmup 1, same library (sha1 %s); bytes = 2*FETCH + WRITE per launch" % (
+                    args.config, E, lib_digest())
+
+
+# ------------------------------------------------------------------ HBM-bound kernels
+def cuda_time(fn, reps=5):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def hbm_kernels(ag, cfg, B, E):
+    """Algorithmic bytes per launch / HIP-event time (torch's current stream, where these ops
+    launch) for the HBM-bound kernels of the step, measured right after the timed region."""
+    from spprl import _lib
+
+    rb = ag.replay_buffer
     ob, ac = cfg["ob"], cfg["ac"]
-    sac = cfg["algo"] == "sac"
-    norm = Norm(True, torch.full((ob,), -2.0), torch.full((ob,), 2.0))
-    if sac:
-        from oracle.acm import OracleAcmTrainer
-        from oracle.sac_acm import OracleSacAcm
+    aout = ac if cfg["algo"] == "vanilla" else ob
+    n = len(rb)
+    out = {}
 
-        lay = {"actor": onets.sac_actor_layout(ob, ob), "critic_1": onets.critic_layout(ob + ac),
-               "critic_2": onets.critic_layout(ob + ac), "critic_1_targ": onets.critic_layout(ob + ac),
-               "critic_2_targ": onets.critic_layout(ob + ac), "acm": onets.acm_layout(2 * ob, ac)}
-        params = {k: fill_params(v, i) for i, (k, v) in enumerate(lay.items())}
-        o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm,
-                         acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params)
-        acm = OracleAcmTrainer(2 * ob, ac, lr=1e-3, params=params["acm"])
-        P = {k: {n: torch.as_tensor(v) for n, v in params[k].items()} for k in ("actor", "acm")}
+    def rec(name, ms, nbytes, note):
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"ms": round(ms, 4), "bytes": int(nbytes), "GB/s": round(gbs, 1),
+                     "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes": note}
 
-        def act(obs):
-            with torch.no_grad():
-                a, _, _ = onets.sac_actor(P["actor"], obs, torch.tensor(1.0), torch.randn(1, ob))
-                return onets.acm(P["acm"], torch.cat([obs, norm.denormalize(a)], 1), torch.ones(ac))
+    ms = cuda_time(lambda: rb.update_obs_mean_std())
+    rec("obs_stats", ms, n * (4 * ob + 8), "one read of the live rows: len x (4 ob + 8 obs_idx)")
+    idx = torch.randint(0, n, (B,), device=ag.device)
+    acmc = cfg["algo"] != "vanilla"
+    per_s = 24 + 8 * ob + 4 * ac + 5 + (0 if acmc else 4 * aout)
+    per_w = 4 * (2 * ob + ac + 2 + (0 if acmc else aout))
+    ms = cuda_time(lambda: _lib.call("sppAgentStageFromReplay", ag._h, rb._h, _lib.ptr(idx), B, _lib.stream_handle()))
+    rec("replay_stage", ms, B * (per_s + per_w), "per sample: 8 idx + 16 (obs_idx, next_idx) + gathered row values "
+        "+ the same values written feature-major")
+    obs = torch.randn(E, ob, device=ag.device)
 
-        def upd(batch):
-            o.update(*batch, rng.randn(100, ob).astype(np.float32), rng.randn(100, ob).astype(np.float32))
-
-        acm_step = acm.batch_update
-        acm_every = 100.0 / (cfg["agent"]["acm_update_batches"] * cfg["agent"]["acm_batch_size"] /
-                             cfg["agent"]["acm_update_freq"])
-    else:
-        from oracle.ddpg_acm import OracleDdpgAcm
-
-        lay = {"actor": onets.ddpg_actor_layout(ob, ob), "critic": onets.critic_layout(ob + ac),
-               "actor_targ": onets.ddpg_actor_layout(ob, ob), "critic_targ": onets.critic_layout(ob + ac),
-               "acm": onets.basic_acm_layout(2 * ob, ac)}
-        params = {k: fill_params(v, i) for i, (k, v) in enumerate(lay.items())}
-        o = OracleDdpgAcm(ob, ob, ac, acm_critic=True, custom_loss=1.0, norm_closs=False, norm=norm, gamma=0.95,
-                          params=params)
-        Pa = {n: torch.as_tensor(v) for n, v in params["actor"].items()}
-        Pm = {n: torch.as_tensor(v).clone().requires_grad_(True) for n, v in params["acm"].items()}
-        opt = torch.optim.Adam(Pm.values(), lr=0.005)
-
-        def act(obs):
-            with torch.no_grad():
-                a = onets.ddpg_actor(Pa, obs, torch.tensor(1.0)) + 0.05 * torch.randn(1, ob)
-                return onets.basic_acm(Pm, torch.cat([obs, norm.denormalize(a.clamp(-1.1, 1.1))], 1))
-
-        def upd(batch):
-            o.update(*batch)
-
-        def acm_step(x, y):
-            loss = torch.nn.functional.mse_loss(onets.basic_acm(Pm, torch.as_tensor(x)), torch.as_tensor(y))
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-
-        acm_every = 128.0 / (cfg["agent"]["acm_update_batches"] * cfg["agent"]["acm_batch_size"] /
-                             cfg["agent"]["acm_update_freq"])
-
-    t_stats0 = time.perf_counter()
-    big = rng.randn(1_000_000, ob)
-    big.mean(0), big.std(0), np.percentile(big, 99, axis=0), np.percentile(big, 1, axis=0)
-    t_stats = time.perf_counter() - t_stats0
-    n, acc, t_loop = 0, 0.0, 0.0
-    B = 100
-    start = time.perf_counter()
-    while time.perf_counter() - start < seconds:
-        obs = torch.from_numpy(rng.randn(1, ob).astype(np.float32))
-        batch = (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
-                 rng.randn(B, ob).astype(np.float32), rng.randn(B).astype(np.float32),
-                 (rng.rand(B) < 0.01).astype(np.int8), rng.uniform(-1, 1, (B, ac)).astype(np.float32))
-        xa = rng.randn(100 if sac else 128, 2 * ob).astype(np.float32)
-        ya = rng.uniform(-1, 1, (xa.shape[0], ac)).astype(np.float32)
-        t0 = time.perf_counter()
-        act(obs)
-        upd(batch)
-        acc += 1.0
-        while acc >= acm_every:
-            acm_step(xa, ya)
-            acc -= acm_every
-        t_loop += time.perf_counter() - t0
-        n += 1
-    per_step = t_loop / n + t_stats / 1000.0
-    return {"value": round(1.0 / per_step, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d env steps of the %s reference cadence (1 act + 1 grad step B=100 per env step, ACM "
-                      "regression at its reference rate, obs stats of a 1e6-row buffer amortised /1000); oracle = "
-                      "torch-CPU restatement, 1 thread; %.1f s" % (n, cfg["env"], time.perf_counter() - start)}
+    def add():
+        s = rb.add_obs_batch(obs)
+        rb.add_timestep_batch(s, s, torch.zeros(E, aout, device=ag.device), torch.zeros(E, device=ag.device),
+                              torch.zeros(E, dtype=torch.uint8, device=ag.device),
+                              torch.zeros(E, dtype=torch.uint8, device=ag.device),
+                              None if not acmc else torch.zeros(E, ac, device=ag.device))
+    ms = cuda_time(add)
+    rec("replay_add", ms, E * (8 * ob + 4 * aout + 4 * ac + 4 + 2 + 24 + 8), "per env: obs row read + written, "
+        "action / acm / reward / done / end written, (prev, next, ts) metadata; includes the metadata upload")
+    return out
 
 
+# ------------------------------------------------------------------ PPO_AcM (configs[3])
 def bench_ppo(args, world, rank, dev):
     """configs[3]: SPP-PPO HalfCheetah-v2, 16384 envs over 8 GPUs = 2048 per GPU (train/spp_ppo_hcheetah.py
     hyper-parameters).  One step = one PPO_AcM iteration: T = 16 vector steps of rollout (actor sample,
@@ -194,6 +304,7 @@ def bench_ppo(args, world, rank, dev):
     512-sample minibatches with the KL stop, the ACM regression (5 epochs of 64-sample batches over the
     1.1e5 ring every 3 iterations), ring obs statistics."""
     import spprl
+    from spprl import flops
     from spprl.dp import shard_seed
 
     E = args.envs or 2048
@@ -238,6 +349,10 @@ def bench_ppo(args, world, rank, dev):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
     value = world * T * E * args.steps / elapsed
+    mac = flops.onpolicy_macs(ob, ob, ac)
+    N = T * E
+    # algorithmic work of one iteration's 100 full-batch critic steps on N = T*E samples
+    critic_flop = 2.0 * mac["critic_step"] * N * 100
     res = {"metric": "env-steps/sec (rollout+update) SPP-PPO HalfCheetah-v2", "value": round(value, 1),
            "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -247,45 +362,43 @@ def bench_ppo(args, world, rank, dev):
            "config": {"workload": "SPP-PPO HalfCheetah-v2, %d vectorized envs per GPU x %d steps per iteration "
                                   "(BASELINE.json configs[3] per-GPU shape)" % (E, T), "envs_per_gpu": E,
                       "steps_per_iteration": T, "acm_ring": rb.size, "parallelism": "dp%d" % world},
+           "roofline": {"bound": "mfma", "kernel": "whole iteration (64-wide MLPs, latency-bound chain of "
+                                                    "dependent optimizer steps)",
+                        "achieved": round(critic_flop / (elapsed / args.steps) / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": None, "traffic": None,
+                        "note": "achieved = the 100 full-batch critic steps' algorithmic FLOPs per iteration / "
+                                "iteration time; 1719 sequential 64-sample ACM SGD steps and ~64 sequential "
+                                "512-sample actor steps bound the iteration by latency, not by a roofline"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
+    res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = {"value": None, "unit": "env-steps/s", "cores": 0, "kind": "port",
+                               "sample": "not run: the PPO_AcM CPU loop restatement is not built (the oracle pins the "
+                                         "PPO_AcM math per step, tests/test_oracle_golden.py)"}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def _cpu_worker(args):
-    name, seconds = args
-    return cpu_baseline(CONFIGS[name], seconds)
-
-
-def cpu_baseline_pool(name, seconds, procs):
-    """The reference's N_CORES layout (train/spp_*.py: a multiprocessing pool of independent
-    1-thread runs, evals.py:22-26): `procs` concurrent oracle runs on the host cores; the
-    aggregate is the sum of the per-process env-steps/s."""
-    import multiprocessing as mp
-
-    if procs <= 1:
-        return cpu_baseline(CONFIGS[name], seconds)
-    # the workers are CPU-only: hide the GPUs from them (a process that loads the HIP runtime
-    # may count as a GPU user; the box allows 16 per job)
-    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
-    for k in saved:
-        os.environ[k] = "-1"
-    try:
-        with mp.get_context("spawn").Pool(procs) as pool:
-            res = pool.map(_cpu_worker, [(name, seconds)] * procs)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    vals = [r["value"] for r in res]
-    out = dict(res[0])
-    out.update(value=round(sum(vals), 2), cores=procs, per_core=round(sum(vals) / procs, 2),
-               sample="%d concurrent 1-thread processes, each: %s" % (procs, res[0]["sample"]))
-    return out
+# ------------------------------------------------------------------ off-policy configs
+def prefill(ag, rb, cap, E, ob, ac, aout, seed, dev, acm=True):
+    torch.manual_seed(seed)
+    fill = cap - 2 * E
+    chunk = 1 << 18
+    prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
+    done_fill = 0
+    while done_fill < fill:
+        n = min(chunk, fill - done_fill)
+        slots = rb.add_obs_batch(torch.randn(n, ob, device=dev))
+        prevs = np.concatenate([prev[-1:], slots[:-1]])
+        z = torch.zeros(n, dtype=torch.uint8, device=dev)
+        rb.add_timestep_batch(prevs, slots, torch.randn(n, aout, device=dev).clamp(-1, 1) if not acm else
+                              torch.randn(n, aout, device=dev), torch.randn(n, device=dev), z, z,
+                              torch.rand(n, ac, device=dev) * 2 - 1 if acm else None)
+        prev = slots
+        done_fill += n
+    return fill
 
 
 def main():
@@ -314,56 +427,78 @@ def main():
 
     cfg = CONFIGS[args.config]
     ob, ac = cfg["ob"], cfg["ac"]
+    vanilla = cfg["algo"] == "vanilla"
+    aout = ac if vanilla else ob
     E = args.envs or cfg["envs"]
     cap = args.buffer or cfg["buffer"]
-    a = cfg["agent"]
+    a = dict(cfg["agent"])
+    batch_size = a.pop("batch_size")
     rho = a["update_batch_size"] * a["grad_steps"] / a["update_freq"]
-    sigma = a["acm_update_batches"] * a["acm_batch_size"] / a["acm_update_freq"]
-    B, BA = int(round(rho * E)), int(round(sigma * E))
+    sigma = a["acm_update_batches"] * a["acm_batch_size"] / a["acm_update_freq"] if not vanilla else 0.0
     seed = shard_seed(1000, rank)
-    Agent = spprl.SAC_AcM if cfg["algo"] == "sac" else spprl.DDPG_AcM
-    ag = Agent(env_name=cfg["env"], buffer_size=cap, max_batch=max(B, BA), device=dev, seed=0, n_envs=E,
-               schedule="fused", random_frames=0, batch_size=E, iterations=10 ** 9, loop_seed=seed,
-               acm_epochs=1, **a)
+    if vanilla:
+        Agent = spprl.SAC
+        B, BA = a["update_batch_size"], 0
+        sched = "reference" if E == 1 else "fused"
+    else:
+        Agent = spprl.SAC_AcM if cfg["algo"] == "sac" else spprl.DDPG_AcM
+        B, BA = int(round(rho * E)), int(round(sigma * E))
+        sched = "fused"
+    if sched == "fused" and vanilla:
+        B = int(round(rho * E))
+    ag = Agent(env_name=cfg["env"], buffer_size=cap, max_batch=max(B, BA, 128), device=dev, seed=0, n_envs=E,
+               schedule=sched, random_frames=0, batch_size=batch_size, iterations=10 ** 9, loop_seed=seed,
+               **({} if vanilla else dict(acm_epochs=1)), **a)
     rb = ag.replay_buffer
-    assert ag.fused_batch_sizes() == (B, BA)
+    if sched == "fused":
+        assert ag.fused_batch_sizes()[0] == B
 
-    # ---- pre-fill the replay shard with N(0,1) transitions
-    torch.manual_seed(seed)
-    fill = cap - 2 * E
-    chunk = 1 << 18
-    prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
-    done_fill = 0
-    while done_fill < fill:
-        n = min(chunk, fill - done_fill)
-        slots = rb.add_obs_batch(torch.randn(n, ob, device=dev))
-        prevs = np.concatenate([prev[-1:], slots[:-1]])
-        z = torch.zeros(n, dtype=torch.uint8, device=dev)
-        rb.add_timestep_batch(prevs, slots, torch.randn(n, ob, device=dev), torch.randn(n, device=dev), z, z,
-                              torch.rand(n, ac, device=dev) * 2 - 1)
-        prev = slots
-        done_fill += n
+    fill = prefill(ag, rb, cap, E, ob, ac, aout, seed, dev, acm=not vanilla)
     ag.update_obs_stats()
     ag.iteration = 1  # past the first iteration: ACM regression is on (ddpg_acm.py:52-57)
     ag.stats_logger.frames = fill
+    stats = {"passes": 0, "frames": 0}
 
-    def vector_step():
-        ag.collect_batch_and_train(E)  # act -> env -> replay -> rho*E grad step -> sigma*E ACM step
-        ag.update_obs_stats()  # global across ranks (RCCL) when N > 1
+    def obs_stats(frames):
+        """update_obs_mean_std at the reference's per-frame rate (one pass per batch_size frames)."""
+        if args.stats_rate == "per-step":
+            ag.update_obs_stats()
+            stats["passes"] += 1
+            return
+        f0 = stats["frames"]
+        stats["frames"] += frames
+        for _ in range(stats["frames"] // batch_size - f0 // batch_size):
+            ag.update_obs_stats()  # global across ranks (RCCL) when N > 1
+            stats["passes"] += 1
+
+    if sched == "fused":
+        def step():
+            ag.collect_batch_and_train(E)  # act -> env -> replay -> rho*E grad step -> sigma*E ACM step
+            obs_stats(E)
+    else:
+        ag._start_episodes()
+
+        def step():  # one frame of DDPG.collect_batch_and_train (ddpg.py:192-223) with make_update
+            end = ag._vector_step()
+            ag.make_update()
+            if bool(end[0]):
+                ag._start_episodes()
+            obs_stats(1)
 
     for _ in range(args.warmup):
-        vector_step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     ag.set_timing(True)
     ag.get_timing()  # clear
+    stats["passes"] = 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        vector_step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -376,52 +511,53 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
 
-    mac = flops.sac_macs(ob, ac) if cfg["algo"] == "sac" else flops.ddpg_macs(ob, ac)
+    if cfg["algo"] == "ddpg":
+        mac = flops.ddpg_macs(ob, ac)
+    else:
+        mac = flops.sac_macs(ob, ac, aout=aout, acm_critic=not vanilla, with_acm=not vanilla)
     value = world * E * args.steps / elapsed
-    k_ms = {name: ms[i] / max(cnt[i], 1) for i, name in enumerate(["critic_phase", "actor_phase", "dw_gemm",
-                                                                      "adam", "acm_regress"])}
-    tf = lambda m, t: 2.0 * m * B / (t * 1e-3) / 1e12  # noqa: E731
+    names = ["critic_phase", "actor_phase", "dw_gemm", "adam", "acm_regress"]
+    k_ms = {name: ms[i] / max(cnt[i], 1) for i, name in enumerate(names)}
+    k_cnt = {name: int(cnt[i]) for i, name in enumerate(names)}
+    tf = lambda m, t: 2.0 * m * B / (t * 1e-3) / 1e12 if t > 0 else 0.0  # noqa: E731
     crit_tf, act_tf = tf(mac["critic_phase"], k_ms["critic_phase"]), tf(mac["actor_phase"], k_ms["actor_phase"])
     dw_tf = tf(mac["dw"] / 2, k_ms["dw_gemm"])  # two dW launches per grad step
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            key = "critic_phase_bytes_per_launch" if cfg["algo"] == "sac" else "ddpg_critic_phase_bytes_per_launch"
-            t = json.load(open(pmc))
-            if t.get("config", "sac_hopper") == args.config:
-                traffic = t.get(key)
-        except Exception:
-            traffic = None
-    flop_step = 2.0 * (mac["update"] * B + mac["acm_reg"] * BA + mac["act"] * E)
     bf16 = cfg.get("bf16", False)
     peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
-    kname = "k_sac_critic_phase" if cfg["algo"] == "sac" else "k_ddpg_critic_phase"
+    kname = "k_ddpg_critic_phase" if cfg["algo"] == "ddpg" else "k_sac_critic_phase"
+    grad_steps_per_step = k_cnt["critic_phase"] / args.steps
+    flop_step = 2.0 * (mac["update"] * B * grad_steps_per_step + mac["acm_reg"] * BA + mac["act"] * E)
+    metric = {"sac": "SPP-SAC ", "ddpg": "SPP-DDPG ", "vanilla": "vanilla SAC "}[cfg["algo"]] + cfg["env"]
     result = {
-        "metric": "env-steps/sec (rollout+update) %s" % ("SPP-SAC " + cfg["env"] if cfg["algo"] == "sac"
-                                                         else "SPP-DDPG " + cfg["env"]),
+        "metric": "env-steps/sec (rollout+update) %s" % metric,
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16 MFMA MLP, fp32 accumulate / targets / optimizer" if bf16 else "fp32",
         "data": "synthetic: SynthEnv linear-tanh dynamics (%s shapes ob=%d, ac=%d), random-init networks, replay "
                 "pre-filled with N(0,1) transitions" % (cfg["env"], ob, ac),
-        "config": {"workload": cfg["workload"] % E, "envs_per_gpu": E, "update_batch": B, "acm_batch": BA,
-                   "rho": rho, "sigma": sigma, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world},
+        "config": {"workload": cfg["workload"] % E if "%d" in cfg["workload"] else cfg["workload"],
+                   "envs_per_gpu": E, "update_batch": B, "acm_batch": BA, "rho": rho, "sigma": sigma,
+                   "schedule": sched, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world,
+                   "obs_stats": "%s rate: %d passes over %d timed steps (one per %d frames)" % (
+                       args.stats_rate, stats["passes"], args.steps, batch_size)},
         "roofline": {"bound": "mfma", "kernel": "%s (critic targets + critic fwd/bwd)" % kname,
-                     "achieved": round(crit_tf, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(crit_tf / peak, 4), "traffic": traffic,
-                     "flop_per_launch": 2.0 * mac["critic_phase"] * B, "avg_launch_ms": round(k_ms["critic_phase"], 3)},
-        "kernels_ms_per_launch": {k: round(v, 3) for k, v in k_ms.items()},
+                     "achieved": round(crit_tf, 3), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(crit_tf / peak, 5), "traffic": None,
+                     "flop_per_launch": 2.0 * mac["critic_phase"] * B,
+                     "algorithmic": "2 x %d MAC per replayed sample x B = %d samples per launch" % (
+                         mac["critic_phase"], B),
+                     "avg_launch_ms": round(k_ms["critic_phase"], 4), "launches": k_cnt["critic_phase"]},
+        "kernels_ms_per_launch": {k: round(v, 4) for k, v in k_ms.items()},
         "kernels_tflops": {"critic_phase": round(crit_tf, 2), "actor_phase": round(act_tf, 2),
                            "dw_gemm": round(dw_tf, 2)},
-        "step_tflops": round(flop_step * args.steps / elapsed / 1e12, 2),
+        "step_tflops": round(flop_step * args.steps / elapsed / 1e12, 3),
         "losses": {k: round(v, 5) for k, v in losses.items()},
     }
     if world > 1:  # data-parallel replicas must stay bit-identical (same averaged grads, same Adam)
@@ -430,8 +566,19 @@ def main():
         allc = [torch.empty_like(chk) for _ in range(world)]
         dist.all_gather(allc, chk)
         result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
+    if world == 1:
+        result["hbm_kernels"] = hbm_kernels(ag, cfg, B, E)
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic, src = pmc_traffic(args, E, cap, [kname, "k_stats_", "k_replay_stage_fm"])
+        if traffic:
+            result["roofline"]["traffic"] = traffic.get(kname)
+            result["roofline"]["traffic_source"] = src
+            result["pmc_bytes_per_launch"] = traffic
+        else:
+            result["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_pool(args.config, args.cpu_seconds, args.cpu_procs)
+        result["cpu_baseline"] = cpu_baseline_report(args.config, args.cpu_seconds,
+                                                     args.cpu_procs or default_cpu_procs())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -17,6 +17,7 @@
 #include "optim.hip"
 #include "ppo.hip"
 #include "replay.hip"
+#include "stats.hip"
 #include "sac.hip"
 #include "ddpg.hip"
 #include "kset.h"
@@ -99,6 +100,10 @@ struct sppReplay {
   double* st_mean = nullptr;
   uint32_t* st_state = nullptr;
   uint32_t* st_hist = nullptr;
+  // sample-bracketed single-device path (stats.hip)
+  uint32_t *sf_bounds = nullptr, *sf_cpart = nullptr, *sf_wgl = nullptr, *sf_wgn = nullptr, *sf_ovf = nullptr,
+           *sf_ovf_n = nullptr;
+  double* sf_part = nullptr;
 };
 
 extern "C" {
@@ -201,6 +206,8 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
     hipEventDestroy(h->ev[i]);
   }
   hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_state); hipFree(h->st_hist);
+  hipFree(h->sf_bounds); hipFree(h->sf_part); hipFree(h->sf_cpart); hipFree(h->sf_wgl); hipFree(h->sf_wgn);
+  hipFree(h->sf_ovf); hipFree(h->sf_ovf_n);
   delete h;
   return SPP_OK;
 }
@@ -338,27 +345,48 @@ static void stats_sel(sppReplayHandle h, int p, uint32_t* hist, int64_t n, float
                      first_update);
 }
 
+constexpr int kStNblk = 1024;  // pass workgroups along the rows
+
+constexpr int kStNw = kStNblk * (kStPassThreads / 64);  // pass waves
+
+static sppStatus stats_fast_alloc(sppReplayHandle h) {
+  if (h->sf_bounds) return SPP_OK;
+  const int ob = h->d.ob;
+  SPP_CHECK_HIP(hipMalloc(&h->sf_bounds, sizeof(uint32_t) * ob * 4));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_part, sizeof(double) * kStNblk * ob * 2));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_cpart, sizeof(uint32_t) * kStNblk * ob * 6));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_wgl, sizeof(uint32_t) * (size_t)kStNblk * ob * 2 * kStWgCap));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_wgn, sizeof(uint32_t) * (size_t)kStNblk * ob * 2));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_ovf, sizeof(uint32_t) * (size_t)ob * 2 * kStOvfCap));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_ovf_n, sizeof(uint32_t) * ob * 2));
+  return SPP_OK;
+}
+
 sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
                             int first_update, void* stream) {
   SPP_REQUIRE(h && mean && std && max_obs && min_obs, SPP_E_INVALID_ARG, "obs_stats: bad args");
   const int64_t len = h->len;
   if (len <= 10) return SPP_OK;  // replay_buffer.py:84
-  SPP_REQUIRE(len < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats: len too large");
   const int ob = h->d.ob;
-  SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats: ob %d > %d", ob, 16 * kStatsColsPerThread);
-  sppStatus s = stats_alloc(h);
+  SPP_REQUIRE(ob <= 128, SPP_E_SHAPE, "obs_stats: ob %d > 128", ob);
+  // per-lane counters are 16-bit: rows per lane = len / (waves * G) < 65536
+  SPP_REQUIRE(len / ((int64_t)kStNw * st_groups(ob)) < 60000, SPP_E_INVALID_ARG, "obs_stats: len too large");
+  sppStatus s = stats_fast_alloc(h);
   if (s) return s;
   hipStream_t st = S(stream);
-  stats_pass1(h, h->st_hist, nullptr, st);
-  hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, h->st_hist, kStatsBlocks, ob, 0, ob, 24, 1,
-                     (const double*)h->st_part, len, h->st_state, h->st_mean, max_obs, min_obs, first_update);
-  hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std,
-                     (const float*)nullptr);
-  const int npass = kStatsPasses;
-  for (int p = 0; p < npass; ++p) {
-    stats_pk(h, p, h->st_hist, st);
-    stats_sel(h, p, h->st_hist, len, max_obs, min_obs, first_update, st);
-  }
+  const bool big = len > kStBigLen;
+  const int ns = (int)std::min<int64_t>(len, big ? kStSampMax : kStSampSmall);
+  SPP_CHECK_HIP(hipMemsetAsync(h->sf_ovf_n, 0, sizeof(uint32_t) * ob * 2, st));
+  if (big)
+    hipLaunchKernelGGL(k_st_bracket<1024>, dim3(ob), dim3(1024), 0, st, h->d, len, ns, h->sf_bounds);
+  else
+    hipLaunchKernelGGL(k_st_bracket<256>, dim3(ob), dim3(256), 0, st, h->d, len, ns, h->sf_bounds);
+  StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
+                h->sf_ovf_n};
+  hipLaunchKernelGGL(k_st_pass, dim3(kStNblk), dim3(kStPassThreads), 0, st, pa);
+  StSelArgs sa{h->d, len, kStNblk, h->sf_part, h->sf_cpart, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf,
+               h->sf_ovf_n, nullptr, mean, std, max_obs, min_obs, first_update};
+  hipLaunchKernelGGL(k_st_select, dim3(ob, 2), dim3(kStSelThreads), 0, st, sa);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

@@ -1,0 +1,99 @@
+"""GPU parity of update_obs_mean_std (rltoolkit/buffer/replay_buffer.py:83-96) on the
+single-device sample-bracketed path (csrc/stats.hip) against numpy on the same rows:
+percentiles (np.percentile 'linear') bit-exact, mean / std within fp32 rounding of the fp64
+result (rtol 2e-7), running max / min.  Cases cover the edge cases of the bracket: tiny and
+sample-sized buffers, ties at the bounds, constant columns, heavy tails, wide observations,
+a wrapped ring (obs_idx not in slot order) and a layout built so the stride sample misses the
+tail (the exact raw-data fallback inside k_st_select)."""
+import numpy as np
+import pytest
+import torch
+
+import spprl
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _fill(rows, ac=3, extra=10):
+    n, ob = rows.shape[0] - 1, rows.shape[1]
+    rb = spprl.BufferAcMOffPolicy(n + extra, ob, ob, ac, device=DEV)
+    slots = rb.add_obs_batch(torch.from_numpy(rows))
+    rb.add_timestep_batch(slots[:n], slots[1:n + 1], torch.zeros(n, ob), np.zeros(n), np.zeros(n, bool),
+                          np.zeros(n, bool), torch.zeros(n, ac))
+    assert len(rb) == n
+    return rb
+
+
+def _check(rb, x, prev=None):
+    rb.update_obs_mean_std()
+    x = x.astype(np.float64)
+    p99, p1 = np.percentile(x, 99, axis=0).astype(np.float32), np.percentile(x, 1, axis=0).astype(np.float32)
+    if prev is not None:
+        p99, p1 = np.maximum(p99, prev[0]), np.minimum(p1, prev[1])
+    got = [t.cpu().numpy() for t in (rb.obs_mean, rb.obs_std, rb.max_obs, rb.min_obs)]
+    np.testing.assert_array_equal(got[2], p99)
+    np.testing.assert_array_equal(got[3], p1)
+    np.testing.assert_allclose(got[0], x.mean(0).astype(np.float32), rtol=2e-7, atol=1e-30)
+    np.testing.assert_allclose(got[1], x.std(0).astype(np.float32), rtol=2e-7, atol=1e-30)
+    return got
+
+
+@pytest.mark.parametrize("n,ob", [(11, 3), (100, 11), (16384, 11), (16385, 17), (300_001, 11), (150_000, 111)])
+def test_obs_stats_exact_sizes(n, ob):
+    rng = np.random.RandomState(n % 997 + ob)
+    rows = (rng.standard_t(3, size=(n + 1, ob)) * rng.uniform(0.1, 5, ob) + rng.randn(ob)).astype(np.float32)
+    _check(_fill(rows), rows[:n])
+
+
+def test_obs_stats_ties_constant_and_discrete_columns():
+    rng = np.random.RandomState(5)
+    n, ob = 200_000, 6
+    rows = np.empty((n + 1, ob), np.float32)
+    rows[:, 0] = 3.0                                     # constant
+    rows[:, 1] = rng.randint(-3, 4, n + 1)               # 7 values: ties at every bound
+    rows[:, 2] = np.where(rng.rand(n + 1) < 0.985, 0.0, rng.randn(n + 1))  # mass at 0, sparse tail
+    rows[:, 3] = rng.randn(n + 1) * 1e-30                # tiny magnitudes (denormal neighbourhood)
+    rows[:, 4] = -np.abs(rng.standard_cauchy(n + 1))     # heavy one-sided tail
+    rows[:, 5] = np.round(rng.randn(n + 1), 1)           # 0.1 grid
+    _check(_fill(rows), rows[:n])
+
+
+def test_obs_stats_fallback_when_sample_misses_tail():
+    """Rows the stride sample ((2s+1) len / 2S) never visits carry the upper 2 %: every sample
+    key is 0, the bracket is [0, 0] and the 99th-percentile ranks fall outside it."""
+    n, ob = 100_000, 2
+    S = 16384
+    sampled = np.zeros(n, bool)
+    sampled[((2 * np.arange(S) + 1) * n) // (2 * S)] = True
+    rows = np.zeros((n + 1, ob), np.float32)
+    free = np.flatnonzero(~sampled)
+    rng = np.random.RandomState(1)
+    pick = rng.choice(free, size=n // 50, replace=False)
+    rows[pick, 0] = rng.uniform(1, 2, pick.size)
+    rows[pick, 1] = -rng.uniform(1, 2, pick.size)
+    _check(_fill(rows), rows[:n])
+
+
+def test_obs_stats_wrapped_ring_and_running_extremes():
+    """A ring that wrapped (Q6: obs_idx no longer in slot order) and a second update that keeps
+    the running max / min (replay_buffer.py:93-96)."""
+    rng = np.random.RandomState(9)
+    size, ob = 50_000, 11
+    rb = spprl.BufferAcMOffPolicy(size, ob, ob, 3, device=DEV)
+    prev = rb.add_obs_batch(torch.from_numpy(rng.randn(1, ob).astype(np.float32)))
+    for it in range(4):  # 4 x 20000 transitions into a 50000-slot ring: wraps
+        E = 20_000
+        obs = (rng.randn(E, ob) * (1 + it)).astype(np.float32)
+        slots = rb.add_obs_batch(torch.from_numpy(obs))
+        prevs = np.concatenate([prev[-1:], slots[:-1]])
+        rb.add_timestep_batch(prevs, slots, torch.zeros(E, ob), np.zeros(E), np.zeros(E, bool), np.zeros(E, bool),
+                              torch.zeros(E, 3))
+        prev = slots
+    n = len(rb)
+    x = rb.gather(torch.arange(n))[0].cpu().numpy()  # obs[obs_idx[t]] (bit-exact gather)
+    first = _check(rb, x)
+    # one more obs slot (it overwrites the ring slot of the oldest live obs): running extremes hold
+    rb.add_obs_batch(torch.zeros(1, ob))
+    x = rb.gather(torch.arange(n))[0].cpu().numpy()
+    _check(rb, x, prev=(first[2], first[3]))

@@ -101,7 +101,7 @@ struct sppReplay {
   uint32_t* st_state = nullptr;
   uint32_t* st_hist = nullptr;
   // sample-bracketed single-device path (stats.hip)
-  uint32_t *sf_bounds = nullptr, *sf_cpart = nullptr, *sf_wgl = nullptr, *sf_wgn = nullptr, *sf_ovf = nullptr,
+  uint32_t *sf_samp = nullptr, *sf_bounds = nullptr, *sf_cpart = nullptr, *sf_wgl = nullptr, *sf_wgn = nullptr, *sf_ovf = nullptr,
            *sf_ovf_n = nullptr;
   double* sf_part = nullptr;
 };
@@ -206,7 +206,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
     hipEventDestroy(h->ev[i]);
   }
   hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_state); hipFree(h->st_hist);
-  hipFree(h->sf_bounds); hipFree(h->sf_part); hipFree(h->sf_cpart); hipFree(h->sf_wgl); hipFree(h->sf_wgn);
+  hipFree(h->sf_samp); hipFree(h->sf_bounds); hipFree(h->sf_part); hipFree(h->sf_cpart); hipFree(h->sf_wgl); hipFree(h->sf_wgn);
   hipFree(h->sf_ovf); hipFree(h->sf_ovf_n);
   delete h;
   return SPP_OK;
@@ -345,20 +345,22 @@ static void stats_sel(sppReplayHandle h, int p, uint32_t* hist, int64_t n, float
                      first_update);
 }
 
-constexpr int kStNblk = 1024;  // pass workgroups along the rows
-
-constexpr int kStNw = kStNblk * (kStPassThreads / 64);  // pass waves
+static int st_nblk(sppReplayHandle h) {  // every pass workgroup resident at once (4 per CU)
+  return std::max(1, std::min(kStNblkMax, 4 * h->num_cu));
+}
 
 static sppStatus stats_fast_alloc(sppReplayHandle h) {
   if (h->sf_bounds) return SPP_OK;
-  const int ob = h->d.ob;
+  const int ob = h->d.ob, nb = kStNblkMax;
   SPP_CHECK_HIP(hipMalloc(&h->sf_bounds, sizeof(uint32_t) * ob * 4));
-  SPP_CHECK_HIP(hipMalloc(&h->sf_part, sizeof(double) * kStNblk * ob * 2));
-  SPP_CHECK_HIP(hipMalloc(&h->sf_cpart, sizeof(uint32_t) * kStNblk * ob * 6));
-  SPP_CHECK_HIP(hipMalloc(&h->sf_wgl, sizeof(uint32_t) * (size_t)kStNblk * ob * 2 * kStWgCap));
-  SPP_CHECK_HIP(hipMalloc(&h->sf_wgn, sizeof(uint32_t) * (size_t)kStNblk * ob * 2));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_samp, sizeof(uint32_t) * (size_t)ob * kStSampBig));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_part, sizeof(double) * nb * ob * 2));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_cpart, sizeof(uint32_t) * nb * ob * 6));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_wgl, sizeof(uint32_t) * (size_t)nb * ob * 2 * st_list_cap(ob)));
+  SPP_CHECK_HIP(hipMalloc(&h->sf_wgn, sizeof(uint32_t) * (size_t)nb * ob * 2));
   SPP_CHECK_HIP(hipMalloc(&h->sf_ovf, sizeof(uint32_t) * (size_t)ob * 2 * kStOvfCap));
   SPP_CHECK_HIP(hipMalloc(&h->sf_ovf_n, sizeof(uint32_t) * ob * 2));
+  SPP_CHECK_HIP(hipMemset(h->sf_ovf_n, 0, sizeof(uint32_t) * ob * 2));  // k_st_select re-zeroes
   return SPP_OK;
 }
 
@@ -369,22 +371,26 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   if (len <= 10) return SPP_OK;  // replay_buffer.py:84
   const int ob = h->d.ob;
   SPP_REQUIRE(ob <= 128, SPP_E_SHAPE, "obs_stats: ob %d > 128", ob);
+  const int nblk = st_nblk(h);
   // per-lane counters are 16-bit: rows per lane = len / (waves * G) < 65536
-  SPP_REQUIRE(len / ((int64_t)kStNw * st_groups(ob)) < 60000, SPP_E_INVALID_ARG, "obs_stats: len too large");
+  SPP_REQUIRE(len / ((int64_t)nblk * (kStPassThreads / 64) * st_groups(ob)) < 60000, SPP_E_INVALID_ARG,
+              "obs_stats: len too large");
   sppStatus s = stats_fast_alloc(h);
   if (s) return s;
   hipStream_t st = S(stream);
   const bool big = len > kStBigLen;
-  const int ns = (int)std::min<int64_t>(len, big ? kStSampMax : kStSampSmall);
-  SPP_CHECK_HIP(hipMemsetAsync(h->sf_ovf_n, 0, sizeof(uint32_t) * ob * 2, st));
+  const int ns = (int)std::min<int64_t>(len, big ? kStSampBig : kStSampSmall);
+  hipLaunchKernelGGL(k_st_sample, dim3(cdiv(ns, 256)), dim3(256), 0, st, h->d, len, ns, h->sf_samp);
   if (big)
-    hipLaunchKernelGGL(k_st_bracket<1024>, dim3(ob), dim3(1024), 0, st, h->d, len, ns, h->sf_bounds);
+    hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns, h->sf_bounds);
   else
-    hipLaunchKernelGGL(k_st_bracket<256>, dim3(ob), dim3(256), 0, st, h->d, len, ns, h->sf_bounds);
+    hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns,
+                       h->sf_bounds);
+  const int cap = st_list_cap(ob);
   StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
-                h->sf_ovf_n};
-  hipLaunchKernelGGL(k_st_pass, dim3(kStNblk), dim3(kStPassThreads), 0, st, pa);
-  StSelArgs sa{h->d, len, kStNblk, h->sf_part, h->sf_cpart, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf,
+                h->sf_ovf_n, cap};
+  st_launch_pass(pa, nblk, st);
+  StSelArgs sa{h->d, len, nblk, cap, h->sf_part, h->sf_cpart, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                h->sf_ovf_n, nullptr, mean, std, max_obs, min_obs, first_update};
   hipLaunchKernelGGL(k_st_select, dim3(ob, 2), dim3(kStSelThreads), 0, st, sa);
   SPP_CHECK_HIP(hipGetLastError());

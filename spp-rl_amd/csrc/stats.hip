@@ -1,135 +1,207 @@
 // update_obs_mean_std (rltoolkit/buffer/replay_buffer.py:83-96) over the live replay rows
 // X = obs[obs_idx[0:len)], by sample-bracketed exact selection: ONE read of X.
 //
-//   k_st_bracket  one workgroup per column: S = min(len, 4096 | 16384) stride-sampled rows -> sort
-//                 keys, a 256 | 1024-thread bitonic sort (16 keys per thread: in-register,
-//                 cross-lane shuffle, only the cross-wave stages through LDS); each target percentile
-//                 (99th, 1st) is bracketed by the sample ranks +-(4 sigma + 4) around it
+//   k_st_sample   S = min(len, 16384 | 65536) stride-sampled rows gathered by a grid (one row per
+//                 thread), stored column-major as keys
+//   k_st_bracket  one workgroup per column: the column's S keys in registers (16 | 64 per
+//                 thread); the 4 bracket ranks (lo / hi around the 99th and the 1st percentile,
+//                 sample ranks +-(4 sigma + 4)) by an 8-bit radix select whose histograms live in
+//                 LDS (one histogram per distinct prefix, the bin search a wave-wide prefix scan)
 //   k_st_pass     one read of every live row.  Lanes take (row, column) pairs of G = 64 / ob
 //                 consecutive rows (one row, two column halves for ob > 64), so a wave's loads
 //                 cover contiguous row runs.  Per lane: fp64 moments about a pivot; per target
 //                 the count of keys outside the bracket on the far side and of keys equal to
-//                 either bound; the keys strictly inside go to the lane's LDS slots, then to one
-//                 list per (workgroup, column, target) (a global overflow list, one atomic per
-//                 key, only past the slots / the list capacity); per-workgroup partials of
-//                 moments and counts to a slab.  No atomics on the fast path.
+//                 either bound.  Keys strictly inside a bracket are appended (LDS atomic cursor)
+//                 to the workgroup's LDS list for (column, target), then copied to global
+//                 lists; a full LDS list spills to a global overflow list.  Per-workgroup
+//                 partials (moments, counts) go to a slab.  The grid is sized so every
+//                 workgroup is resident at once (36 KiB of LDS: 4 per CU).
 //   k_st_select   one workgroup per (column, target): reduces the slabs, places the 2 ranks numpy's
 //                 'linear' percentile needs (floor((len-1) q) and the next) in
-//                 [outside | = lo | candidates | = hi | outside] and radix-selects them inside
-//                 the candidates (thread i reads workgroup list i) from their common key prefix
-//                 on (8-bit digits).  mean / std and the running max (target 0) or min
-//                 (target 1) are written here.  A rank outside the bracket (a sample miss) or an
-//                 overflowed list falls back to a radix select over the column's raw data: the
-//                 result is exact in every case.
+//                 [outside | = lo | candidates | = hi | outside], gathers the candidates into LDS
+//                 (block prefix sum over the list lengths) and radix-selects them there from
+//                 their common key prefix on.  mean / std and the running max (target 0) or
+//                 min (target 1) are written here, and the overflow counter is re-zeroed for the
+//                 next call.  A rank outside the bracket (a sample miss) falls back to a radix
+//                 select over the column's raw data; more candidates than the LDS holds are
+//                 visited in the global lists: the result is exact in every case.
 // Keys: fkey() is the order-preserving uint32 image of a float (replay.hip).
 #pragma once
 #include "replay.h"
 
 namespace spp {
 
-constexpr int kStSampMax = 16384;   // bracketing sample per column (16 keys x 1024 threads)
-constexpr int kStSampSmall = 4096;  // len <= kStBigLen: 16 keys x 256 threads
-constexpr int64_t kStBigLen = 2000000;
-constexpr int kStLaneK = 8;          // LDS candidate slots per (lane, column half, target)
-constexpr int kStWgCap = 128;        // candidate keys per (workgroup, column, target) list
+constexpr int kStSampSmall = 16384;  // len <= kStBigLen: 16 keys x 1024 threads
+constexpr int kStSampBig = 65536;    // beyond: 64 keys x 1024 threads
+constexpr int64_t kStBigLen = 4000000;
+constexpr int kStLdsKeys = 6144;     // per-workgroup LDS list space (keys), split over 2 ob lists
 constexpr int kStOvfCap = 1 << 18;   // overflow keys per (column, target)
 constexpr int kStPassThreads = 256;
-constexpr int kStUnroll = 8;         // row groups per lane in flight
+constexpr int kStUnroll = 8;         // row groups per lane in flight (halved for ob > 64)
+constexpr int kStNblkMax = 1024;     // pass workgroups (<= select threads)
+constexpr int kStSelThreads = 1024;
+constexpr int kStSelKeys = 32768;    // candidates gathered into the select workgroup's LDS
 
-// ---------------------------------------------------------------- sample bracket
-// Bitonic network position e = 16 * tid + i; partner e ^ j; ascending where (e & k) == 0.
-template <int J>
-__device__ __forceinline__ void bitonic_in_thread(uint32_t (&v)[16], int tid, int k) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    constexpr int jj = J;
-    const int p = i ^ jj;
-    if (p > i) {
-      const bool up = ((16 * tid + i) & k) == 0;
-      const uint32_t a = v[i], b = v[p];
-      const bool sw = (a > b) == up;
-      v[i] = sw ? b : a;
-      v[p] = sw ? a : b;
-    }
-  }
+__host__ __device__ inline int st_list_cap(int ob) {
+  const int c = kStLdsKeys / (2 * ob);
+  return c < 256 ? c : 256;
 }
 
-// 16 * NT keys in NT threads (v: this thread's 16), ascending.  lds: 16 * NT words, element e
-// at (e % 16) * NT + e / 16 (conflict-free for a fixed i across lanes).
-template <int NT>
-__device__ void block_sort16(uint32_t (&v)[16], uint32_t* lds) {
-  const int tid = threadIdx.x;
-  constexpr int P = 16 * NT;
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 1024) {  // partner in another wave
+// ---------------------------------------------------------------- LDS radix select
+// Up to NQ ranks over a key set the workgroup visits with visit(fn): every thread calls fn(key)
+// for the keys it owns.  Query q starts from the known bits qpre[q] / qmask[q] (the masks are
+// whole-bit prefixes; queries may share a prefix, and then share a histogram).  On return
+// qpre[q] is the key of rank qrank[q] (in the set restricted to the starting prefix).
+// Needs blockDim.x >= 64 * NQ; qpre / qmask / qrank / hist in LDS.
+// Histograms hold kStCopies copies of every bin (lane & 7 picks the copy): the keys of a digit
+// pass usually fall into a handful of bins, and same-address LDS atomics of one instruction
+// serialise, so the copies cut that serialisation 8-fold.  hist: [NQ][256][kStCopies].
+constexpr int kStCopies = 8;
+template <int NQ, class Visit>
+__device__ void st_radix_select(uint32_t* qpre, uint32_t* qmask, uint32_t* qrank, Visit visit, uint32_t* hist) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    const uint32_t dm = 0xffu << shift;
+    uint32_t pre[NQ], msk[NQ];
+    int rep[NQ];
+    bool act[NQ], any = false;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) lds[i * NT + tid] = v[i];
-        __syncthreads();
-        const int pt = tid ^ (j >> 4);
+    for (int q = 0; q < NQ; ++q) {
+      pre[q] = qpre[q];
+      msk[q] = qmask[q];
+      act[q] = (msk[q] & dm) != dm;
+      any |= act[q];
+      rep[q] = q;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int e = 16 * tid + i;
-          const uint32_t o = lds[i * NT + pt];
-          const bool keep_min = (e < (e ^ j)) == ((e & k) == 0);
-          v[i] = keep_min ? min(v[i], o) : max(v[i], o);
+      for (int p = 0; p < q; ++p)
+        if (rep[q] == q && pre[p] == pre[q] && msk[p] == msk[q]) rep[q] = rep[p];
+    }
+    if (!any) continue;  // uniform: every thread read the same state
+    for (int i = tid; i < NQ * 256 * kStCopies; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    uint32_t* hl = hist + (lane & (kStCopies - 1));
+    visit([&](uint32_t k) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        if (act[q] && rep[q] == q && (k & msk[q]) == pre[q])
+          atomicAdd(&hl[(q * 256 + ((k >> shift) & 255)) * kStCopies], 1u);
+    });
+    __syncthreads();
+    if (w < NQ && act[w]) {
+      const uint4* hh = reinterpret_cast<const uint4*>(hist + (rep[w] * 256 + 4 * lane) * kStCopies);
+      uint32_t c4[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 a = hh[2 * j], b = hh[2 * j + 1];
+        c4[j] = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+        sum += c4[j];
+      }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      const uint32_t excl = incl - sum, r = qrank[w];
+      const bool mine = r >= excl && r < incl;
+      const bool none = __ballot(mine) == 0ull;  // rank past the set (inconsistent input): last bin
+      if (mine || (none && lane == 63)) {
+        uint32_t acc = excl;
+        int d = 4 * lane + 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (acc + c4[j] > r) {
+            d = 4 * lane + j;
+            break;
+          }
+          acc += c4[j];
         }
-        __syncthreads();
-      } else if (j >= 16) {  // partner lane of the same wave
-        const int lm = j >> 4;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int e = 16 * tid + i;
-          const uint32_t o = __shfl_xor(v[i], lm, 64);
-          const bool keep_min = (e < (e ^ j)) == ((e & k) == 0);
-          v[i] = keep_min ? min(v[i], o) : max(v[i], o);
-        }
-      } else if (j == 8) {
-        bitonic_in_thread<8>(v, tid, k);
-      } else if (j == 4) {
-        bitonic_in_thread<4>(v, tid, k);
-      } else if (j == 2) {
-        bitonic_in_thread<2>(v, tid, k);
-      } else {
-        bitonic_in_thread<1>(v, tid, k);
+        qpre[w] = (pre[w] & ~dm) | ((uint32_t)d << shift);
+        qmask[w] = msk[w] | dm;
+        qrank[w] = r - acc;
       }
     }
+    __syncthreads();
   }
 }
 
-// bounds[(c*2 + t)*2 + {0,1}] = {lo, hi} keys of target t (0: 99th, 1: 1st percentile), from
-// the S-row stride sample rows ((2s + 1) len) / (2S) (all rows when S == len).
-// NT threads sort S <= 16 NT keys: 256 (S = 4096) up to 2M live rows, 1024 (S = 16384) beyond, so
-// the bracket (~0.8 / sqrt(S) of the rows) keeps the candidate lists within their capacity.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_st_bracket(ReplayDev r, int64_t len, int S, uint32_t* __restrict__ bounds) {
-  __shared__ uint32_t sk[16 * NT];
-  const int c = blockIdx.x, tid = threadIdx.x, ob = r.ob;
-  uint32_t v[16];
+// ---------------------------------------------------------------- sample bracket
+// k_st_sample: the S-row stride sample rows ((2s + 1) len) / (2S) (all rows when S == len), one
+// sample row per thread over a grid of workgroups (a random-row gather needs many CUs' worth of
+// outstanding misses), written column-major as keys: samp[c][s].
+__global__ __launch_bounds__(256) void k_st_sample(ReplayDev r, int64_t len, int S, uint32_t* __restrict__ samp) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const int ob = r.ob;
+  const double step = (double)len / (2.0 * (double)S);  // exact enough for a sample; row s when S == len
+  const int64_t row = min((int64_t)((double)(2 * s + 1) * step), len - 1);
+  const float* x = r.obs + r.obs_idx[row] * ob;
+  for (int c0 = 0; c0 < ob; c0 += 16) {
+    float v[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int j = 16 * tid + i;
-    uint32_t k = 0xffffffffu;  // padding sorts last
-    if (j < S) {
-      const int64_t row = ((2 * (int64_t)j + 1) * len) / (2 * (int64_t)S);
-      k = fkey(r.obs[r.obs_idx[row] * ob + c]);
+    for (int i = 0; i < 16; ++i) v[i] = c0 + i < ob ? x[c0 + i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (c0 + i < ob) samp[(int64_t)(c0 + i) * S + s] = fkey(v[i]);
+  }
+}
+
+// bounds[(c*2 + t)*2 + {0,1}] = {lo, hi} keys of target t (0: 99th, 1: 1st percentile) from the
+// column's S sample keys (KPT per thread, coalesced reads of samp[c][:]).
+template <int KPT>
+__global__ __launch_bounds__(1024) void k_st_bracket(const uint32_t* __restrict__ samp, int S,
+                                                      uint32_t* __restrict__ bounds) {
+  __shared__ __attribute__((aligned(16))) uint32_t hist[4 * 256 * kStCopies];
+  __shared__ uint32_t qpre[4], qmask[4], qrank[4];
+  __shared__ int qn;
+  __shared__ int qt[4];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  uint32_t v[KPT];
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const int j = i * 1024 + tid;
+    v[i] = samp[(int64_t)c * S + (j < S ? j : S - 1)];
+  }
+  if (tid == 0) {
+    int n = 0;
+    for (int t = 0; t < 2; ++t) {
+      const double p = t == 0 ? 0.99 : 0.01;
+      const int64_t f = (int64_t)floor(p * (double)(S - 1));
+      const int m = (int)ceil(4.0 * sqrt((double)S * p * (1.0 - p))) + 4;
+      const int64_t lo_i = f - m, hi_i = f + 1 + m;
+      // a bracket touching the sample's end extends to the key range's end (nothing outside)
+      if (lo_i <= 0) {
+        bounds[(c * 2 + t) * 2 + 0] = 0u;
+      } else {
+        qt[n] = (c * 2 + t) * 2 + 0;
+        qrank[n] = (uint32_t)lo_i;
+        ++n;
+      }
+      if (hi_i >= S - 1) {
+        bounds[(c * 2 + t) * 2 + 1] = 0xffffffffu;
+      } else {
+        qt[n] = (c * 2 + t) * 2 + 1;
+        qrank[n] = (uint32_t)hi_i;
+        ++n;
+      }
     }
-    v[i] = k;
+    for (int q = 0; q < 4; ++q) {
+      qpre[q] = 0;
+      qmask[q] = q < n ? 0u : 0xffffffffu;  // unused slots: fully known (inactive)
+    }
+    qn = n;
   }
-  block_sort16<NT>(v, sk);
   __syncthreads();
+  if (qn == 0) return;
+  st_radix_select<4>(
+      qpre, qmask, qrank,
+      [&](auto&& fn) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) sk[16 * tid + i] = v[i];
-  __syncthreads();
-  if (tid < 2) {
-    const double p = tid == 0 ? 0.99 : 0.01;
-    const int64_t f = (int64_t)floor(p * (double)(S - 1));
-    const int m = (int)ceil(4.0 * sqrt((double)S * p * (1.0 - p))) + 4;
-    const int64_t lo_i = f - m, hi_i = f + 1 + m;
-    // a bracket touching the sample's end extends to the key range's end (nothing outside)
-    bounds[(c * 2 + tid) * 2 + 0] = lo_i <= 0 ? 0u : sk[lo_i];
-    bounds[(c * 2 + tid) * 2 + 1] = hi_i >= S - 1 ? 0xffffffffu : sk[hi_i];
-  }
+        for (int i = 0; i < KPT; ++i)
+          if (i * 1024 + tid < S) fn(v[i]);
+      },
+      hist);
+  if (tid < qn) bounds[qt[tid]] = qpre[tid];
 }
 
 // ---------------------------------------------------------------- the data pass
@@ -147,255 +219,250 @@ struct StPassArgs {
   const uint32_t* bounds;  // [ob][2][2]
   const float* pivot;      // [ob] or null (first live row)
   double* part;            // [nblk][ob][2]       moment partials
-  uint32_t* cpart;         // [nblk][ob][2][3]    count partials: outside, == lo, == hi
-  uint32_t* wgl;           // [nblk][ob][2][kStWgCap]  per-workgroup candidate lists
-  uint32_t* wgn;           // [nblk][ob][2]            keys in each list (<= kStWgCap)
-  uint32_t* ovf;           // [ob][2][kStOvfCap]  keys past a lane's slots or a list's capacity
-  uint32_t* ovf_n;         // [ob][2]             (zeroed before the pass)
+  uint32_t* cpart;         // [nblk][ob][6]       count partials: per target outside, == lo, == hi
+  uint32_t* wgl;           // [nblk][ob][2][cap]  per-workgroup candidate lists
+  uint32_t* wgn;           // [nblk][ob][2]       keys in each list (<= cap)
+  uint32_t* ovf;           // [ob][2][kStOvfCap]  keys past a list's capacity
+  uint32_t* ovf_n;         // [ob][2]             (zero on entry; k_st_select re-zeroes)
+  int cap;                 // st_list_cap(ob)
 };
 
-__global__ __launch_bounds__(kStPassThreads) void k_st_pass(StPassArgs a) {
+// WIDE: ob > 64 (two column halves per lane).  OFF32: the obs ring is < 4 GiB, so every load is a
+// uniform 64-bit base plus ONE 32-bit per-lane byte offset (saddr form: 1 VGPR per address).
+template <bool WIDE, bool OFF32>
+__global__ __launch_bounds__(kStPassThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_st_pass(StPassArgs a) {
   constexpr int W = kStPassThreads / 64;
-  __shared__ double rs[W][64][2][2];   // per lane: [j][s1, s2]
-  __shared__ uint32_t rcn[W][64][2][6];  // per lane: [j][t * 3 + (outside, == lo, == hi)]
-  __shared__ uint32_t lst[W][64][2][2][kStLaneK];  // per lane candidate slots
-  __shared__ uint8_t lfill[W][64][2][2];
-  const int ob = a.r.ob, G = st_groups(ob);
+  constexpr int U = WIDE ? kStUnroll / 2 : kStUnroll;  // row groups per iteration (2 loads each if WIDE)
+  __shared__ uint32_t lst[kStLdsKeys];   // [ob][2][cap]
+  __shared__ uint32_t lcnt[256];         // [ob][2] list cursors
+  __shared__ uint32_t ccnt[128 * 6];     // [ob][6] counts
+  __shared__ double rs[W * 64][2][2];    // per lane: [j][s1, s2]
+  const int ob = a.r.ob, G = st_groups(ob), cap = a.cap;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < 2 * ob; i += kStPassThreads) lcnt[i] = 0;
+  for (int i = tid; i < 6 * ob; i += kStPassThreads) ccnt[i] = 0;
   const int64_t wv = (int64_t)blockIdx.x * W + w, nw = (int64_t)gridDim.x * W;
   const int g = ob <= 64 ? lane / ob : 0;
-  const int col[2] = {st_col(ob, lane, 0), st_col(ob, lane, 1)};
+  const int col[2] = {st_col(ob, lane, 0), WIDE ? st_col(ob, lane, 1) : -1};
   const float* p0 = a.pivot ? a.pivot : a.r.obs + a.r.obs_idx[0] * ob;
-  float piv[2];
+  double piv[2];
   uint32_t lo[2][2], hi[2][2];
   double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
   uint32_t cout[2][2] = {{0, 0}, {0, 0}}, ceq[2][2] = {{0, 0}, {0, 0}};  // ceq: == lo | == hi << 16
-  uint32_t fill[2][2] = {{0, 0}, {0, 0}};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = col[j] < 0 ? 0 : col[j];
-    piv[j] = p0[c];
+    piv[j] = (double)p0[c];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       lo[j][t] = a.bounds[(c * 2 + t) * 2 + 0];
       hi[j][t] = a.bounds[(c * 2 + t) * 2 + 1];
     }
   }
-  const int64_t ngroups = (a.len + G - 1) / G;
-  // the obs_idx of the next iteration's rows are requested before this iteration's data is
-  // used: the dependent index -> row load pair overlaps across iterations
-  int nidx[kStUnroll];  // ring slots < capacity < 2^31
-#pragma unroll
-  for (int u = 0; u < kStUnroll; ++u) {
-    const int64_t row = (wv + u * nw) * G + g;
-    nidx[u] = (row < a.len && col[0] >= 0) ? (int)a.r.obs_idx[row] : -1;
-  }
-  for (int64_t rg0 = wv; rg0 < ngroups; rg0 += nw * kStUnroll) {
-    int64_t base[kStUnroll];
-    bool ok[kStUnroll];
-#pragma unroll
-    for (int u = 0; u < kStUnroll; ++u) {
-      ok[u] = nidx[u] >= 0;
-      base[u] = ok[u] ? (int64_t)nidx[u] * ob : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < kStUnroll; ++u) {
-      const int64_t row = (rg0 + (kStUnroll + u) * nw) * G + g;
-      nidx[u] = (row < a.len && col[0] >= 0) ? (int)a.r.obs_idx[row] : -1;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j == 1 && ob <= 64) break;
-      float x[kStUnroll];
-#pragma unroll
-      for (int u = 0; u < kStUnroll; ++u) x[u] = (ok[u] && col[j] >= 0) ? a.r.obs[base[u] + col[j]] : 0.f;
-#pragma unroll
-      for (int u = 0; u < kStUnroll; ++u) {
-        if (!(ok[u] && col[j] >= 0)) continue;
-        const double d = (double)x[u] - (double)piv[j];
-        s1[j] += d;
-        s2[j] += d * d;
-        const uint32_t key = fkey(x[u]);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const uint32_t l = lo[j][t], h = hi[j][t];
-          cout[j][t] += (uint32_t)(t ? key < l : key > h);
-          ceq[j][t] += (uint32_t)(key == l) | ((uint32_t)(key == h && h != l) << 16);
-          if (key > l && key < h) {
-            const uint32_t f = fill[j][t]++;
-            if (f < (uint32_t)kStLaneK) {
-              lst[w][lane][j][t][f] = key;
-            } else {
-              const int ct = col[j] * 2 + t;
-              const uint32_t o = atomicAdd(&a.ovf_n[ct], 1u);
-              if (o < (uint32_t)kStOvfCap) a.ovf[(int64_t)ct * kStOvfCap + o] = key;
-            }
-          }
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) lfill[w][lane][j][t] = (uint8_t)(fill[j][t] < (uint32_t)kStLaneK ? fill[j][t] : kStLaneK);
-  // lane partials -> LDS -> one partial per (workgroup, column)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    rs[w][lane][j][0] = s1[j];
-    rs[w][lane][j][1] = s2[j];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      rcn[w][lane][j][3 * t + 0] = cout[j][t];
-      rcn[w][lane][j][3 * t + 1] = ceq[j][t] & 0xffffu;
-      rcn[w][lane][j][3 * t + 2] = ceq[j][t] >> 16;
-    }
-  }
   __syncthreads();
-  for (int c = tid; c < ob; c += blockDim.x) {
-    double m1 = 0.0, m2 = 0.0;
-    uint32_t cn[6] = {0, 0, 0, 0, 0, 0};
-    const int j = ob <= 64 ? 0 : c / 64;
-    for (int q = 0; q < W; ++q)
-      for (int gg = 0; gg < G; ++gg) {
-        const int l = ob <= 64 ? gg * ob + c : c - 64 * j;
-        m1 += rs[q][l][j][0];
-        m2 += rs[q][l][j][1];
+  const int64_t ngroups = (a.len + G - 1) / G;
+  // Software pipeline over iterations of U row groups: iteration i+1's rows are
+  // requested (their obs_idx came one iteration earlier) and iteration i+2's obs_idx issued
+  // before iteration i's keys are classified, so the data pass overlaps its own compute.
+  // Every load is unconditional (clamped row / column), so none sits in a branch with its wait.
+  const int64_t last = a.len - 1;
+  const int c0 = col[0] < 0 ? 0 : col[0], c1 = col[1] < 0 ? 0 : col[1];
+  const int64_t it_rows = nw * U;  // row groups per iteration (all waves)
+  const char* obs_b = reinterpret_cast<const char*>(a.r.obs);
+  const char* idx_b = reinterpret_cast<const char*>(a.r.obs_idx);
+  auto ld_idx = [&](int64_t row) -> int {  // ring slots < capacity < 2^31
+    if constexpr (OFF32) return *reinterpret_cast<const int*>(idx_b + (uint32_t)row * 8u);  // low word
+    else return (int)a.r.obs_idx[row];
+  };
+  auto ld_x = [&](int slot, int c) -> float {
+    if constexpr (OFF32) return *reinterpret_cast<const float*>(obs_b + ((uint32_t)slot * (uint32_t)ob + (uint32_t)c) * 4u);
+    else return a.r.obs[(int64_t)slot * ob + c];
+  };
+  // validity is kept apart from the loaded slot (a select on the loaded value lets the compiler
+  // sink the load into a branch with its own wait)
+  auto idx_load = [&](int64_t rg0, int (&n)[U], uint32_t& vm) {
+    vm = 0;
 #pragma unroll
-        for (int f = 0; f < 6; ++f) cn[f] += rcn[q][l][j][f];
-      }
-    a.part[((int64_t)blockIdx.x * ob + c) * 2 + 0] = m1;
-    a.part[((int64_t)blockIdx.x * ob + c) * 2 + 1] = m2;
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = (rg0 + u * nw) * G + g;
+      n[u] = ld_idx(min(row, last));
+      vm |= (uint32_t)(row < a.len && col[0] >= 0) << u;
+    }
+  };
+  auto x_load = [&](const int (&n)[U], float (&x)[2][U]) {
 #pragma unroll
-    for (int f = 0; f < 6; ++f) a.cpart[((int64_t)blockIdx.x * ob + c) * 6 + f] = cn[f];
-  }
-  // the lanes' candidate slots -> this workgroup's list per (column, target)
-  for (int ct = tid; ct < 2 * ob; ct += blockDim.x) {
-    const int c = ct >> 1, t = ct & 1;
-    const int j = ob <= 64 ? 0 : c / 64;
-    uint32_t* dst = a.wgl + ((int64_t)blockIdx.x * ob * 2 + ct) * kStWgCap;
-    uint32_t n = 0;
-    for (int q = 0; q < W; ++q)
-      for (int gg = 0; gg < G; ++gg) {
-        const int l = ob <= 64 ? gg * ob + c : c - 64 * j;
-        const int m = lfill[q][l][j][t];
-        for (int i = 0; i < m; ++i) {
-          const uint32_t key = lst[q][l][j][t][i];
-          if (n < (uint32_t)kStWgCap) {
-            dst[n++] = key;
+    for (int u = 0; u < U; ++u) x[0][u] = ld_x(n[u], c0);
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[1][u] = ld_x(n[u], c1);
+    }
+  };
+  // one key: moments, far-side counts; the rare keys inside a bracket take the slow path
+  auto proc = [&](int j, float xv, bool v) {
+    const double d = v ? (double)xv - piv[j] : 0.0;
+    s1[j] += d;
+    s2[j] = fma(d, d, s2[j]);
+    const uint32_t key = fkey(xv);
+    cout[j][0] += (uint32_t)(v && key > hi[j][0]);
+    cout[j][1] += (uint32_t)(v && key < lo[j][1]);
+    const bool in0 = v && key >= lo[j][0] && key <= hi[j][0];
+    const bool in1 = v && key >= lo[j][1] && key <= hi[j][1];
+    if (in0 || in1) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (!(t ? in1 : in0)) continue;
+        const uint32_t l = lo[j][t], h = hi[j][t];
+        if (key == l) {
+          ceq[j][t] += 1u;
+        } else if (key == h) {
+          ceq[j][t] += 1u << 16;
+        } else {
+          const int ct = col[j] * 2 + t;
+          const uint32_t f = atomicAdd(&lcnt[ct], 1u);
+          if (f < (uint32_t)cap) {
+            lst[ct * cap + f] = key;
           } else {
             const uint32_t o = atomicAdd(&a.ovf_n[ct], 1u);
             if (o < (uint32_t)kStOvfCap) a.ovf[(int64_t)ct * kStOvfCap + o] = key;
           }
         }
       }
-    a.wgn[(int64_t)blockIdx.x * ob * 2 + ct] = n;
+    }
+  };
+  // the next iteration's obs_idx are requested before this iteration's rows are used
+  int nA[U];
+  uint32_t vA;
+  idx_load(wv, nA, vA);
+  for (int64_t rg0 = wv; rg0 < ngroups; rg0 += it_rows) {
+    float xA[2][U];
+    x_load(nA, xA);
+    const uint32_t v = vA;
+    idx_load(rg0 + it_rows, nA, vA);
+#pragma unroll
+    for (int u = 0; u < U; ++u) proc(0, xA[0][u], (v >> u) & 1u);
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) proc(1, xA[1][u], ((v >> u) & 1u) && col[1] >= 0);
+    }
   }
+  // lane partials -> LDS -> one partial per (workgroup, column)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    rs[tid][j][0] = s1[j];
+    rs[tid][j][1] = s2[j];
+    if (col[j] >= 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (cout[j][t]) atomicAdd(&ccnt[col[j] * 6 + 3 * t + 0], cout[j][t]);
+        if (ceq[j][t] & 0xffffu) atomicAdd(&ccnt[col[j] * 6 + 3 * t + 1], ceq[j][t] & 0xffffu);
+        if (ceq[j][t] >> 16) atomicAdd(&ccnt[col[j] * 6 + 3 * t + 2], ceq[j][t] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < ob; c += kStPassThreads) {
+    double m1 = 0.0, m2 = 0.0;
+    const int j = ob <= 64 ? 0 : c / 64;
+    for (int q = 0; q < W; ++q)
+      for (int gg = 0; gg < G; ++gg) {
+        const int l = 64 * q + (ob <= 64 ? gg * ob + c : c - 64 * j);
+        m1 += rs[l][j][0];
+        m2 += rs[l][j][1];
+      }
+    a.part[((int64_t)blockIdx.x * ob + c) * 2 + 0] = m1;
+    a.part[((int64_t)blockIdx.x * ob + c) * 2 + 1] = m2;
+  }
+  for (int i = tid; i < 6 * ob; i += kStPassThreads) a.cpart[(int64_t)blockIdx.x * ob * 6 + i] = ccnt[i];
+  for (int i = tid; i < 2 * ob; i += kStPassThreads)
+    a.wgn[(int64_t)blockIdx.x * ob * 2 + i] = min(lcnt[i], (uint32_t)cap);
+  uint32_t* dst = a.wgl + (int64_t)blockIdx.x * ob * 2 * cap;
+  for (int i = tid; i < 2 * ob * cap; i += kStPassThreads)
+    if ((uint32_t)(i % cap) < lcnt[i / cap]) dst[i] = lst[i];
+}
+
+inline void st_launch_pass(const StPassArgs& pa, int nblk, hipStream_t st) {
+  const bool wide = pa.r.ob > 64;
+  const bool off32 = (uint64_t)pa.r.cap * (uint64_t)pa.r.ob * 4u < (1ull << 32) && pa.len < ((int64_t)1 << 29);
+  if (wide && off32) hipLaunchKernelGGL((k_st_pass<true, true>), dim3(nblk), dim3(kStPassThreads), 0, st, pa);
+  else if (wide) hipLaunchKernelGGL((k_st_pass<true, false>), dim3(nblk), dim3(kStPassThreads), 0, st, pa);
+  else if (off32) hipLaunchKernelGGL((k_st_pass<false, true>), dim3(nblk), dim3(kStPassThreads), 0, st, pa);
+  else hipLaunchKernelGGL((k_st_pass<false, false>), dim3(nblk), dim3(kStPassThreads), 0, st, pa);
 }
 
 // ---------------------------------------------------------------- select
-// Radix select (8-bit digits) of up to 2 ranks over a key set that the workgroup visits with
-// visit(fn): every thread calls fn(key) for the keys it owns.  Each query starts from
-// qpre / qmask: the bits known in advance (the candidates' common prefix: counting those
-// digits would put every key into one bin).
-template <class Visit>
-__device__ void st_radix_select(int nq, uint32_t* qpre, uint32_t* qmask, uint32_t* qrank, Visit visit,
-                                uint32_t (*hist)[256]) {
-  const int tid = threadIdx.x;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    const uint32_t dm = 0xffu << shift;
-    bool any = false;
-    for (int q = 0; q < nq; ++q) any |= (qmask[q] & dm) != dm;
-    if (!any) continue;
-    for (int i = tid; i < 2 * 256; i += blockDim.x) hist[i >> 8][i & 255] = 0;
-    __syncthreads();
-    const uint32_t m0 = qmask[0], p0 = qpre[0], m1 = nq > 1 ? qmask[1] : 0u, p1 = nq > 1 ? qpre[1] : 1u;
-    const bool a0 = (m0 & dm) != dm, a1 = nq > 1 && (m1 & dm) != dm;
-    visit([&](uint32_t k) {
-      if (a0 && (k & m0) == p0) atomicAdd(&hist[0][(k >> shift) & 255], 1u);
-      if (a1 && (k & m1) == p1) atomicAdd(&hist[1][(k >> shift) & 255], 1u);
-    });
-    __syncthreads();
-    if (tid < nq && (qmask[tid] & dm) != dm) {
-      const uint32_t fixed = qpre[tid] & dm;
-      uint32_t acc = 0, r = qrank[tid];
-      int bin = 255;
-      for (int d = 0; d < 256; ++d) {
-        if ((((uint32_t)d << shift) & qmask[tid] & dm) != fixed) continue;  // outside the known bits
-        if (acc + hist[tid][d] > r) {
-          bin = d;
-          break;
-        }
-        acc += hist[tid][d];
-      }
-      qpre[tid] = (qpre[tid] & ~dm) | ((uint32_t)bin << shift);
-      qmask[tid] |= dm;
-      qrank[tid] = r - acc;
-    }
-    __syncthreads();
-  }
-}
-
 struct StSelArgs {
   ReplayDev r;
   int64_t len;
-  int nblk;
+  int nblk, cap;
   const double* part;
   const uint32_t* cpart;
   const uint32_t* bounds;
   const uint32_t* wgl;
   const uint32_t* wgn;
   const uint32_t* ovf;
-  const uint32_t* ovf_n;
+  uint32_t* ovf_n;
   const float* pivot;
   float *mean, *std, *max_out, *min_out;
   int first_update;
 };
 
-constexpr int kStSelThreads = 1024;
-
 __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
   constexpr int T = kStSelThreads;
-  __shared__ double rd[2][T / 64];
-  __shared__ uint32_t rc[4][T / 64];
-  __shared__ uint32_t hist[2][256];
+  constexpr int NW = T / 64;
+  __shared__ uint32_t cand[kStSelKeys];
+  __shared__ double rd[2][NW];
+  __shared__ uint32_t rc[4][NW];
+  __shared__ __attribute__((aligned(16))) uint32_t hist[2 * 256 * kStCopies];
   __shared__ uint32_t vals[2], qpre[2], qmask[2], qrank[2];
-  __shared__ int qslot[2], nq, mode;  // mode: 0 candidates, 1 raw column
+  __shared__ int qslot[2], nq, mode;  // mode: 0 candidates in LDS, 1 raw column, 2 global lists
   const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, ob = a.r.ob;
   const int lane = tid & 63, wv = tid >> 6;
   const int ct = c * 2 + t;
-  // ---- moments (target 0), this target's counts, candidate count, over the workgroup partials
+  const int cap = a.cap;
+  // ---- moments (target 0), this target's counts, list lengths: thread b owns workgroup b
+  const int b = tid;
   double m1 = 0.0, m2 = 0.0;
-  uint32_t cc[4] = {0, 0, 0, 0};
-  for (int k = tid; k < a.nblk; k += T) {
+  uint32_t cc[3] = {0, 0, 0}, nb = 0;
+  if (b < a.nblk) {
     if (t == 0) {
-      m1 += a.part[((int64_t)k * ob + c) * 2 + 0];
-      m2 += a.part[((int64_t)k * ob + c) * 2 + 1];
+      m1 = a.part[((int64_t)b * ob + c) * 2 + 0];
+      m2 = a.part[((int64_t)b * ob + c) * 2 + 1];
     }
 #pragma unroll
-    for (int f = 0; f < 3; ++f) cc[f] += a.cpart[((int64_t)k * ob + c) * 6 + 3 * t + f];
-    cc[3] += a.wgn[(int64_t)k * ob * 2 + ct];
+    for (int f = 0; f < 3; ++f) cc[f] = a.cpart[((int64_t)b * ob + c) * 6 + 3 * t + f];
+    nb = a.wgn[(int64_t)b * ob * 2 + ct];
+  }
+  // inclusive wave scan of the list lengths (candidate offsets)
+  uint32_t incl = nb;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
   }
   m1 = wave_sum_d(m1);
   m2 = wave_sum_d(m2);
 #pragma unroll
-  for (int f = 0; f < 4; ++f)
+  for (int f = 0; f < 3; ++f)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cc[f] += __shfl_xor(cc[f], o, 64);
+  if (lane == 63) rc[3][wv] = incl;
   if (lane == 0) {
     rd[0][wv] = m1;
     rd[1][wv] = m2;
 #pragma unroll
-    for (int f = 0; f < 4; ++f) rc[f][wv] = cc[f];
+    for (int f = 0; f < 3; ++f) rc[f][wv] = cc[f];
   }
   __syncthreads();
+  uint32_t woff = 0;
+  for (int q = 0; q < wv; ++q) woff += rc[3][q];
+  const uint32_t off = woff + incl - nb;  // this workgroup list's first slot
   const int64_t n = a.len;
   const uint32_t novf_raw = a.ovf_n[ct];
   const uint32_t novf = min(novf_raw, (uint32_t)kStOvfCap);
   if (tid == 0) {
     double s1 = 0.0, s2 = 0.0;
     int64_t out = 0, eql = 0, eqh = 0, nl = 0;
-    for (int q = 0; q < T / 64; ++q) {
+    for (int q = 0; q < NW; ++q) {
       s1 += rd[0][q];
       s2 += rd[1][q];
       out += rc[0][q];
@@ -450,53 +517,69 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
           qrank[q] = (uint32_t)(start + eql + qrank[q]);
         }
     }
+    for (int q = nqq; q < 2; ++q) qmask[q] = 0xffffffffu;  // inactive
     nq = nqq;
-    mode = raw ? 1 : 0;
+    mode = raw ? 1 : (ncd <= kStSelKeys ? 0 : 2);
   }
   __syncthreads();
-  if (nq > 0) {
-    if (mode == 0) {  // thread i visits workgroup list i, then a stride of the overflow keys
-      const uint32_t* wgl = a.wgl;
-      const uint32_t* wgn = a.wgn;
-      const uint32_t* ovf = a.ovf + (int64_t)ct * kStOvfCap;
-      const int nblk = a.nblk;
-      st_radix_select(nq, qpre, qmask, qrank,
-                      [&](auto&& fn) {
-                        for (int b = tid; b < nblk; b += T) {
-                          const uint32_t* L = wgl + ((int64_t)b * ob * 2 + ct) * kStWgCap;
-                          const uint32_t m = wgn[(int64_t)b * ob * 2 + ct];
-                          for (uint32_t i = 0; i < m; i += 4) {
-                            uint32_t k4[4];
+  const int md = mode;
+  if (nq > 0 && md == 0) {  // gather the candidates into LDS: thread b copies list b
+    const uint32_t* L = a.wgl + ((int64_t)b * ob * 2 + ct) * cap;
+    for (uint32_t i = 0; i < nb; i += 8) {
+      uint32_t k8[8];
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) k4[u] = i + u < m ? L[i + u] : 0u;
+      for (int u = 0; u < 8; ++u) k8[u] = i + u < nb ? L[i + u] : 0u;
 #pragma unroll
-                            for (int u = 0; u < 4; ++u)
-                              if (i + u < m) fn(k4[u]);
-                          }
-                        }
-                        for (uint32_t i = tid; i < novf; i += T) fn(ovf[i]);
-                      },
-                      hist);
-    } else {
-      const ReplayDev r = a.r;
-      st_radix_select(nq, qpre, qmask, qrank,
-                      [&](auto&& fn) {
-                        for (int64_t i0 = tid; i0 < n; i0 += 4 * (int64_t)T) {
-                          uint32_t k4[4];
-#pragma unroll
-                          for (int u = 0; u < 4; ++u) {
-                            const int64_t i = i0 + u * (int64_t)T;
-                            k4[u] = i < n ? fkey(r.obs[r.obs_idx[i] * ob + c]) : 0u;
-                          }
-#pragma unroll
-                          for (int u = 0; u < 4; ++u)
-                            if (i0 + u * (int64_t)T < n) fn(k4[u]);
-                        }
-                      },
-                      hist);
+      for (int u = 0; u < 8; ++u)
+        if (i + u < nb) cand[off + i + u] = k8[u];
     }
-    if (tid < nq) vals[qslot[tid]] = qpre[tid];
+    uint32_t tot = 0;
+    for (int q = 0; q < NW; ++q) tot += rc[3][q];
+    const uint32_t* ovf = a.ovf + (int64_t)ct * kStOvfCap;
+    for (uint32_t i = tid; i < novf; i += T) cand[tot + i] = ovf[i];
+    __syncthreads();
+    const uint32_t ncd = tot + novf;
+    st_radix_select<2>(qpre, qmask, qrank,
+                       [&](auto&& fn) {
+                         for (uint32_t i = tid; i < ncd; i += T) fn(cand[i]);
+                       },
+                       hist);
+  } else if (nq > 0 && md == 2) {  // too many candidates for LDS: visit the global lists
+    const uint32_t* wgl = a.wgl;
+    const uint32_t* ovf = a.ovf + (int64_t)ct * kStOvfCap;
+    st_radix_select<2>(qpre, qmask, qrank,
+                       [&](auto&& fn) {
+                         const uint32_t* L = wgl + ((int64_t)b * ob * 2 + ct) * cap;
+                         for (uint32_t i = 0; i < nb; i += 4) {
+                           uint32_t k4[4];
+#pragma unroll
+                           for (int u = 0; u < 4; ++u) k4[u] = i + u < nb ? L[i + u] : 0u;
+#pragma unroll
+                           for (int u = 0; u < 4; ++u)
+                             if (i + u < nb) fn(k4[u]);
+                         }
+                         for (uint32_t i = tid; i < novf; i += T) fn(ovf[i]);
+                       },
+                       hist);
+  } else if (nq > 0) {
+    const ReplayDev r = a.r;
+    st_radix_select<2>(qpre, qmask, qrank,
+                       [&](auto&& fn) {
+                         for (int64_t i0 = tid; i0 < n; i0 += 4 * (int64_t)T) {
+                           uint32_t k4[4];
+#pragma unroll
+                           for (int u = 0; u < 4; ++u) {
+                             const int64_t i = i0 + u * (int64_t)T;
+                             k4[u] = i < n ? fkey(r.obs[r.obs_idx[i] * ob + c]) : 0u;
+                           }
+#pragma unroll
+                           for (int u = 0; u < 4; ++u)
+                             if (i0 + u * (int64_t)T < n) fn(k4[u]);
+                         }
+                       },
+                       hist);
   }
+  if (nq > 0 && tid < nq) vals[qslot[tid]] = qpre[tid];
   __syncthreads();
   if (tid == 0) {
     const double vi = (double)(n - 1) * (t ? 0.01 : 0.99);
@@ -507,6 +590,7 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
     const float res = (float)(g >= 0.5 ? x1 - diff * (1.0 - g) : x0 + diff * g);  // numpy _lerp
     if (t == 0) a.max_out[c] = a.first_update ? res : fmaxf(res, a.max_out[c]);
     else a.min_out[c] = a.first_update ? res : fminf(res, a.min_out[c]);
+    a.ovf_n[ct] = 0;  // every reader of this counter is past the barrier above
   }
 }
 

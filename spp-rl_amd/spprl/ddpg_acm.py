@@ -160,9 +160,10 @@ class DDPG_AcM(OffPolicyLoop):
     def collect_params_dict(self):
         rb = self.replay_buffer
         return {"actor": self.net_state(_lib.SPP_NET_ACTOR), "critic": self.net_state(_lib.SPP_NET_CRITIC1),
-                "acm": self.net_state(_lib.SPP_NET_ACM), "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
+                "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
                 "min_obs": rb.min_obs.cpu() if rb._have_minmax else None,
-                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None}
+                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None,
+                "acm": self.net_state(_lib.SPP_NET_ACM)}
 
     def apply_params_dict(self, d):
         for k in ("actor", "critic", "acm"):

@@ -268,6 +268,29 @@ class PPO_AcM:
         rb = self.replay_buffer
         return {"actor": _nets.state_dict(self.nets.params[0], actor_layout(self.ob_dim, self.ob_dim)),
                 "critic": _nets.state_dict(self.nets.params[1], critic_layout(self.ob_dim)),
-                "acm": self.acm.net_state(5), "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
+                "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
                 "min_obs": rb.min_obs.cpu() if rb._have_minmax else None,
-                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None}
+                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None,
+                "acm": self.acm.net_state(5)}
+
+    def apply_params_dict(self, d):  # rl.py:263-279 + ACM (acm/on_policy.py)
+        from .onpolicy import actor_layout, critic_layout
+        from . import nets as _nets
+
+        for i, (k, lay) in enumerate((("actor", actor_layout(self.ob_dim, self.ob_dim)),
+                                      ("critic", critic_layout(self.ob_dim)))):
+            _nets.load_state(self.nets.params[i], lay, d[k])
+        self.acm.apply_params_dict({"actor": self.acm.net_state(0), "critic_1": self.acm.net_state(1),
+                                    "critic_2": self.acm.net_state(2), "acm": d["acm"], "obs_mean": d["obs_mean"],
+                                    "obs_std": d["obs_std"], "min_obs": d.get("min_obs"),
+                                    "max_obs": d.get("max_obs")})
+
+    def save(self, path):  # rl.py:281-292
+        from .checkpoint import save_params
+
+        save_params(path, self.collect_params_dict())
+
+    def load(self, path):  # rl.py:294-301
+        from .checkpoint import load_params
+
+        self.apply_params_dict(load_params(path))

@@ -249,11 +249,13 @@ class SAC_AcM(OffPolicyLoop):
     # ------------------------------------------------------------------ checkpoints (rl.py:263-301)
     def collect_params_dict(self):
         rb = self.replay_buffer
+        # key order of the reference's dict (sac.py:287-296 + acm/off_policy/sac_acm.py collect_params_dict)
         return {"actor": self.net_state(_lib.SPP_NET_ACTOR), "critic_1": self.net_state(_lib.SPP_NET_CRITIC1),
-                "critic_2": self.net_state(_lib.SPP_NET_CRITIC2), "acm": self.net_state(_lib.SPP_NET_ACM),
+                "critic_2": self.net_state(_lib.SPP_NET_CRITIC2),
                 "obs_mean": rb.obs_mean.cpu(), "obs_std": rb.obs_std.cpu(),
                 "min_obs": rb.min_obs.cpu() if rb._have_minmax else None,
-                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None}
+                "max_obs": rb.max_obs.cpu() if rb._have_minmax else None,
+                "acm": self.net_state(_lib.SPP_NET_ACM)}
 
     def apply_params_dict(self, d):
         for k, net in (("actor", _lib.SPP_NET_ACTOR), ("critic_1", _lib.SPP_NET_CRITIC1),

@@ -619,19 +619,16 @@ class OffPolicyLoop:
         call("sppAgentGetTiming", self._h, ms.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p))
         return ms, cnt
 
-    # ---------------------------------------------------------- checkpoints (rl.py:286-301)
+    # ---------------------------------------------------------- checkpoints (rl.py:281-301)
     def save(self, path):
-        import pickle
+        from .checkpoint import save_params
 
-        with open(path, "wb") as f:
-            pickle.dump(self.collect_params_dict(), f)
+        save_params(path, self.collect_params_dict())
 
     def load(self, path):
-        """Our own checkpoints only (never unpickle files that ship with the reference)."""
-        import pickle
+        from .checkpoint import load_params
 
-        with open(path, "rb") as f:
-            self.apply_params_dict(pickle.load(f))
+        self.apply_params_dict(load_params(path))
 
 
 def acm_lr_at(acm_lr, gamma, step, epochs_done):

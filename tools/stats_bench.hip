@@ -1,0 +1,131 @@
+// Standalone timing of the obs-statistics kernels (csrc/stats.hip) without torch: per-kernel
+// HIP-event averages on synthetic N(0,1) rows.  Build + run (GPU box):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o gpurun_out/stats_bench tools/stats_bench.hip
+//   gpurun_out/stats_bench [n] [ob] [reps]
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <random>
+#include <vector>
+
+#include "../spp-rl_amd/csrc/common.h"
+namespace spp {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+}
+const char* get_error() { return ""; }
+}  // namespace spp
+#include "../spp-rl_amd/csrc/replay.hip"
+#include "../spp-rl_amd/csrc/stats.hip"
+
+using namespace spp;
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));     \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
+  const int ob = argc > 2 ? atoi(argv[2]) : 11;
+  const int reps = argc > 3 ? atoi(argv[3]) : 20;
+  std::vector<float> h(n * ob);
+  std::mt19937 g(1);
+  std::normal_distribution<float> nd;
+  for (auto& x : h) x = nd(g);
+  std::vector<int64_t> hi(n);
+  for (int64_t i = 0; i < n; ++i) hi[i] = i;
+  ReplayDev d{};
+  CK(hipMalloc(&d.obs, sizeof(float) * n * ob));
+  CK(hipMalloc(&d.obs_idx, sizeof(int64_t) * n));
+  CK(hipMemcpy(d.obs, h.data(), sizeof(float) * n * ob, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d.obs_idx, hi.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+  d.cap = n;
+  d.ob = ob;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int nblk = std::min(kStNblkMax, 4 * prop.multiProcessorCount);
+  const int cap = st_list_cap(ob);
+  uint32_t* samp;
+  CK(hipMalloc(&samp, sizeof(uint32_t) * (size_t)ob * kStSampBig));
+  uint32_t *bounds, *cpart, *wgl, *wgn, *ovf, *ovf_n;
+  double* part;
+  float *mean, *sd, *mx, *mn;
+  CK(hipMalloc(&bounds, sizeof(uint32_t) * ob * 4));
+  CK(hipMalloc(&part, sizeof(double) * nblk * ob * 2));
+  CK(hipMalloc(&cpart, sizeof(uint32_t) * nblk * ob * 6));
+  CK(hipMalloc(&wgl, sizeof(uint32_t) * (size_t)nblk * ob * 2 * cap));
+  CK(hipMalloc(&wgn, sizeof(uint32_t) * (size_t)nblk * ob * 2));
+  CK(hipMalloc(&ovf, sizeof(uint32_t) * (size_t)ob * 2 * kStOvfCap));
+  CK(hipMalloc(&ovf_n, sizeof(uint32_t) * ob * 2));
+  CK(hipMemset(ovf_n, 0, sizeof(uint32_t) * ob * 2));
+  CK(hipMalloc(&mean, 4 * ob));
+  CK(hipMalloc(&sd, 4 * ob));
+  CK(hipMalloc(&mx, 4 * ob));
+  CK(hipMalloc(&mn, 4 * ob));
+  const bool big = n > kStBigLen;
+  const int ns = (int)std::min<int64_t>(n, big ? kStSampBig : kStSampSmall);
+  StPassArgs pa{d, n, bounds, nullptr, part, cpart, wgl, wgn, ovf, ovf_n, cap};
+  StSelArgs sa{d, n, nblk, cap, part, cpart, bounds, wgl, wgn, ovf, ovf_n, nullptr, mean, sd, mx, mn, 1};
+  auto sample = [&]() { hipLaunchKernelGGL(k_st_sample, dim3(cdiv(ns, 256)), dim3(256), 0, 0, d, n, ns, samp); };
+  auto bracket = [&]() {
+    if (big)
+      hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, 0, samp, ns, bounds);
+    else
+      hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, 0, samp, ns, bounds);
+  };
+  auto pass = [&]() { st_launch_pass(pa, nblk, 0); };
+  auto sel = [&]() { hipLaunchKernelGGL(k_st_select, dim3(ob, 2), dim3(kStSelThreads), 0, 0, sa); };
+  for (int i = 0; i < 3; ++i) {
+    sample();
+    bracket();
+    pass();
+    sel();
+  }
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto timeit = [&](const char* name, auto&& f, double bytes) {
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    printf("%-10s %8.4f ms", name, ms);
+    if (bytes > 0) printf("  %7.1f GB/s (%.3f of 8 TB/s)", bytes / ms / 1e6, bytes / ms / 1e6 / 8000.0);
+    printf("\n");
+  };
+  const double bytes = (double)n * (4.0 * ob + 8.0);
+  timeit("sample", sample, 0);
+  timeit("bracket", bracket, 0);
+  timeit("pass", pass, bytes);
+  timeit("select", sel, 0);
+  timeit("all", [&]() { sample(); bracket(); pass(); sel(); }, bytes);
+  // parity spot check against a host sort of column 0
+  std::vector<float> m(ob), M(ob);
+  CK(hipMemcpy(M.data(), mx, 4 * ob, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> cnt(ob * 2);
+  std::vector<float> col(n);
+  for (int64_t i = 0; i < n; ++i) col[i] = h[i * ob];
+  std::sort(col.begin(), col.end());
+  const double vi = (double)(n - 1) * 0.99;
+  const int64_t k0 = (int64_t)floor(vi);
+  const double gg = vi - floor(vi);
+  const double x0 = col[k0], x1 = col[std::min(k0 + 1, n - 1)];
+  const float ref = (float)(gg >= 0.5 ? x1 - (x1 - x0) * (1.0 - gg) : x0 + (x1 - x0) * gg);
+  printf("p99 col0: gpu %.9g ref %.9g %s\n", M[0], ref, M[0] == ref ? "OK" : "MISMATCH");
+  return M[0] == ref ? 0 : 2;
+}

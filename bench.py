@@ -102,6 +102,10 @@ def parse():
                     help="concurrent 1-thread reference-loop processes (default: the host's CPU share, max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic null)")
+    ap.add_argument("--host-env", action="store_true",
+                    help="step the envs on the host CPU (HostSynthEnv: vectorised numpy SynthEnv behind pinned "
+                         "staging + side-stream copies, the update overlapping the host step): the PCIe-inclusive "
+                         "host-simulator rate, not the metric")
     a = ap.parse_args()
     st, wu = DEFAULT_STEPS.get(a.config, (200, 10))
     a.steps = st if a.steps is None else a.steps
@@ -446,8 +450,11 @@ def main():
         sched = "fused"
     if sched == "fused" and vanilla:
         B = int(round(rho * E))
+    env = None
+    if args.host_env:
+        env = spprl.HostSynthEnv(E, ob, ac, max_episode_steps=1000, seed=seed, device=dev)
     ag = Agent(env_name=cfg["env"], buffer_size=cap, max_batch=max(B, BA, 128), device=dev, seed=0, n_envs=E,
-               schedule=sched, random_frames=0, batch_size=batch_size, iterations=10 ** 9, loop_seed=seed,
+               schedule=sched, random_frames=0, batch_size=batch_size, iterations=10 ** 9, loop_seed=seed, env=env,
                **({} if vanilla else dict(acm_epochs=1)), **a)
     rb = ag.replay_buffer
     if sched == "fused":
@@ -540,11 +547,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16 MFMA MLP, fp32 accumulate / targets / optimizer" if bf16 else "fp32",
-        "data": "synthetic: SynthEnv linear-tanh dynamics (%s shapes ob=%d, ac=%d), random-init networks, replay "
-                "pre-filled with N(0,1) transitions" % (cfg["env"], ob, ac),
+        "data": "synthetic: SynthEnv linear-tanh dynamics (%s shapes ob=%d, ac=%d)%s, random-init networks, replay "
+                "pre-filled with N(0,1) transitions" % (cfg["env"], ob, ac, ", stepped on the HOST (HostSynthEnv, "
+                                                        "numpy) behind pinned H2D/D2H side-stream copies"
+                                                        if args.host_env else ""),
         "config": {"workload": cfg["workload"] % E if "%d" in cfg["workload"] else cfg["workload"],
                    "envs_per_gpu": E, "update_batch": B, "acm_batch": BA, "rho": rho, "sigma": sigma,
                    "schedule": sched, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world,
+                   "env": "host (HostSynthEnv, PCIe-inclusive)" if args.host_env else "device (SynthVecEnv)",
                    "obs_stats": "%s rate: %d passes over %d timed steps (one per %d frames)" % (
                        args.stats_rate, stats["passes"], args.steps, batch_size)},
         "roofline": {"bound": "mfma", "kernel": "%s (critic targets + critic fwd/bwd)" % kname,

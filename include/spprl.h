@@ -31,7 +31,8 @@ enum {
   SPP_E_SHAPE = 2,
   SPP_E_OOM = 3,
   SPP_E_HIP = 4,
-  SPP_E_STATE = 5
+  SPP_E_STATE = 5,
+  SPP_E_RCCL = 6
 };
 
 /* Text of the last error raised on this thread ("" if none). */
@@ -110,6 +111,17 @@ typedef struct {
   uint8_t* end;        /* [capacity]        */
 } sppReplayView;
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);
+/* The SURVEY §8b constructor: n_envs sizes the per-step metadata ring up front; compat_mode must
+ * be 1 (the reference obs-index ring with the Q6 wrap -- the only ring rltoolkit has);
+ * store_fp64 must be 0 (the reference's float64 arrays only ever receive float32 values, so
+ * float32 storage is exact, Q5).  Other values return SPP_E_INVALID_ARG. */
+sppStatus sppReplayCreateEx(sppReplayHandle* out, int64_t capacity, int ob, int aout, int ac, int n_envs,
+                            int compat_mode, int store_fp64, int device);
+/* BufferAcMOffPolicy.last_rollout (replay_buffer.py:335-383) with last_end (:170-177): the last
+ * complete episode is the *length timesteps first, first+1, ... (cyclic over [0, current_len))
+ * ending at the last end flag at or before ts_idx - 1.  Synchronous; SPP_E_STATE if the buffer
+ * holds no episode end. */
+sppStatus sppReplayLastRollout(sppReplayHandle h, int64_t* first, int64_t* length, void* stream);
 
 /* ------------------------------------------------------------------ agent */
 /* SPP_ALGO_SAC: vanilla SAC (rltoolkit/algorithms/sac/sac.py:138-280), BASELINE configs[0]: no ACM,
@@ -219,6 +231,24 @@ sppStatus sppDdpgAcmCriticGrads(sppAgentHandle h, const sppBatch* batch, float* 
 sppStatus sppDdpgAcmCriticApply(sppAgentHandle h, void* stream);
 sppStatus sppDdpgAcmActorGrads(sppAgentHandle h, float* losses_dev, void* stream);
 sppStatus sppDdpgAcmActorApply(sppAgentHandle h, void* stream);
+
+/* ------------------------------------------------------------------ data-parallel exchange (§8e)
+ * RCCL communicator for C/C++ hosts without torch.distributed (librccl resolved at run time).
+ * Rank 0 fills a SPP_COMM_ID_BYTES unique id, the host ships it to every rank by any channel,
+ * each rank calls sppCommInitRank on its device.  Replaces torch.distributed.all_reduce in the
+ * Python DP path (spprl/dp.py); on ROCm both are RCCL over xGMI. */
+#define SPP_COMM_ID_BYTES 128
+sppStatus sppCommGetUniqueId(void* uid_out);
+sppStatus sppCommInitRank(void** comm_out, int nranks, const void* uid, int rank, int device);
+sppStatus sppCommDestroy(void* comm);
+/* In-place average over the communicator's `world` ranks (ncclSum then x 1/world) of one gradient
+ * bucket, stream-ordered between the *Grads and *Apply halves of an update:
+ *   SPP_BUCKET_CRITIC  critic_1 (+ critic_2) grads          (after *CriticGrads)
+ *   SPP_BUCKET_ACTOR   actor grads (+ the SAC alpha operand)  (after *ActorGrads)
+ *   SPP_BUCKET_ACM     ACM grads                            (after sppAcmRegressGrads)
+ *   SPP_BUCKET_ALL     all of them. */
+enum { SPP_BUCKET_CRITIC = 0, SPP_BUCKET_ACTOR = 1, SPP_BUCKET_ACM = 2, SPP_BUCKET_ALL = 3 };
+sppStatus sppAllReduceGrads(sppAgentHandle h, int bucket, int world, void* rccl_comm, void* stream);
 
 /* AcMTrainer.batch_update (rltoolkit/acm/acm.py:246-258): x [B][2ob], y [B][ac]
  * -> MSE loss (device float) and one Adam step on the bound ACM net. */

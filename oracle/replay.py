@@ -9,6 +9,7 @@ Restates rltoolkit/buffer/replay_buffer.py (reference @ v0):
   BufferAcMOffPolicy.sample_batch     :385-398 + acm actions
   rbuffer_sample_acm                  :404-430
   MetaReplayBuffer.update_obs_mean_std :83-96  fp64 mean, std (ddof=0), percentile 99/1, running max/min
+  last_end / last_rollout             :170-218, :335-383  the last complete episode, walked backwards
 Storage is float64 as in the reference (Q5); every stored value comes from a
 float32 tensor so fp32 round-trips are exact.
 """
@@ -76,6 +77,35 @@ class OracleReplay:
         idx = mt.randint(len(self), B)
         o, no, _, _, _, acm = self.gather(idx)
         return (o, no, acm), idx
+
+    def last_end(self, idx):  # :170-177 (python indexing: -1 is the array's last element)
+        end = self._end[idx]
+        while not end:
+            idx -= 1
+            if idx < 0:
+                idx = self.current_len - 1
+            end = self._end[idx]
+        return idx
+
+    def last_rollout(self):  # :335-383 -> (obs [T+1], actions, rewards, dones, actions_acm, ts indices)
+        i = self.last_end(self.ts_idx - 1)  # -1 stays python's last element, as in the reference
+        obs, actions, rewards, dones, acms, ts = [], [], [], [], [], []
+        last_obs = self._obs[self._next_obs_idx[i]].astype(np.float32)
+        next_end = False
+        while not next_end:
+            obs.insert(0, self._obs[self._obs_idx[i]].astype(np.float32))
+            actions.insert(0, self._actions[i].astype(np.float32))
+            rewards.insert(0, self._rewards[i])
+            dones.insert(0, self._end[i])
+            acms.insert(0, self._actions_acm[i].astype(np.float32))
+            ts.insert(0, i % self.size)
+            i -= 1
+            if i < 0:
+                i = self.current_len - 1
+            next_end = self._end[i]
+        obs.append(last_obs)
+        return (np.stack(obs), np.stack(actions), np.array(rewards, np.float32), np.array(dones), np.stack(acms),
+                np.array(ts))
 
     def live_obs(self):
         return self._obs[self._obs_idx[: self.current_len]]

@@ -1,4 +1,5 @@
 // libspprl C-ABI implementation (unity build: kernels included below).
+#include <dlfcn.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -225,19 +226,27 @@ sppStatus sppReplayAddObs(sppReplayHandle h, const float* obs, int E, int64_t* s
   return SPP_OK;
 }
 
+// pinned host / device metadata ring of the per-step (prev, next, ts) uploads, >= E entries
+static sppStatus ring_reserve(sppReplayHandle h, int E) {
+  if (E <= h->ring_cap) return SPP_OK;
+  hipDeviceSynchronize();
+  for (int i = 0; i < sppReplay::kRing; ++i) {
+    if (h->pinned[i]) hipHostFree(h->pinned[i]);
+    if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
+    h->pinned[i] = nullptr;
+    h->dev_meta[i] = nullptr;
+    SPP_CHECK_HIP(hipHostMalloc(&h->pinned[i], sizeof(int64_t) * 3 * E));
+    SPP_CHECK_HIP(hipMalloc(&h->dev_meta[i], sizeof(int64_t) * 3 * E));
+  }
+  h->ring_cap = E;
+  return SPP_OK;
+}
+
 sppStatus sppReplayAddStep(sppReplayHandle h, const int64_t* prev, const int64_t* next, int E, const float* act,
                            const float* acm, const float* rew, const uint8_t* done, const uint8_t* end, void* stream) {
   SPP_REQUIRE(h && prev && next && E > 0 && rew && done && end, SPP_E_INVALID_ARG, "add_step: bad args");
-  if (E > h->ring_cap) {
-    hipDeviceSynchronize();
-    for (int i = 0; i < sppReplay::kRing; ++i) {
-      if (h->pinned[i]) hipHostFree(h->pinned[i]);
-      if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
-      SPP_CHECK_HIP(hipHostMalloc(&h->pinned[i], sizeof(int64_t) * 3 * E));
-      SPP_CHECK_HIP(hipMalloc(&h->dev_meta[i], sizeof(int64_t) * 3 * E));
-    }
-    h->ring_cap = E;
-  }
+  sppStatus rs = ring_reserve(h, E);
+  if (rs) return rs;
   const int slot = h->ring_pos;
   h->ring_pos = (h->ring_pos + 1) % sppReplay::kRing;
   SPP_CHECK_HIP(hipEventSynchronize(h->ev[slot]));  // the copy that last used this slot is done
@@ -299,6 +308,65 @@ sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* v) {
   v->rew = h->d.rew;
   v->done = h->d.done;
   v->end = h->d.end;
+  return SPP_OK;
+}
+
+// §8b form of the constructor.  n_envs sizes the pinned per-step metadata ring up front;
+// compat_mode 1 is the reference obs-index ring with the Q6 wrap rule (the only ring the
+// reference has); store_fp64 0: the reference's float64 arrays only ever receive float32
+// values (torch float32 obs, actions and rewards), so float32 storage is exact (Q5).
+sppStatus sppReplayCreateEx(sppReplayHandle* out, int64_t cap, int ob, int aout, int ac, int n_envs,
+                            int compat_mode, int store_fp64, int device) {
+  SPP_REQUIRE(compat_mode == 1, SPP_E_INVALID_ARG,
+              "replay create: compat_mode %d (only 1, the reference obs-index ring with the Q6 wrap, exists)",
+              compat_mode);
+  SPP_REQUIRE(store_fp64 == 0, SPP_E_INVALID_ARG,
+              "replay create: store_fp64 %d (float32 storage is exact for every value the reference stores, Q5)",
+              store_fp64);
+  SPP_REQUIRE(n_envs > 0, SPP_E_INVALID_ARG, "replay create: n_envs %d", n_envs);
+  sppStatus s = sppReplayCreate(out, cap, ob, aout, ac, device);
+  if (s) return s;
+  s = ring_reserve(*out, n_envs);
+  if (s) {
+    sppReplayDestroy(*out);
+    *out = nullptr;
+  }
+  return s;
+}
+
+// BufferAcMOffPolicy.last_rollout (replay_buffer.py:335-383): the last complete episode is the
+// *length timesteps first, first+1, ... (cyclic over [0, current_len)) ending at the last `end`
+// at or before ts_idx - 1 (last_end, :170-177).  Synchronous (returns host values).
+sppStatus sppReplayLastRollout(sppReplayHandle h, int64_t* first, int64_t* length, void* stream) {
+  SPP_REQUIRE(h && first && length, SPP_E_INVALID_ARG, "last_rollout: null");
+  const int64_t len = h->len;
+  SPP_REQUIRE(len > 0, SPP_E_STATE, "last_rollout: empty buffer");
+  hipStream_t st = S(stream);
+  if (h->ts_idx == 0 && len == h->d.cap) {
+    // python index ts_idx - 1 = -1 is the array's last element; when it is an end, the reference's
+    // walk wraps to that same element at once (i = -2 -> current_len - 1) and stops: a 1-step rollout
+    uint8_t e = 0;
+    SPP_CHECK_HIP(hipMemcpyAsync(&e, h->d.end + (len - 1), 1, hipMemcpyDeviceToHost, st));
+    SPP_CHECK_HIP(hipStreamSynchronize(st));
+    if (e) {
+      *first = len - 1;
+      *length = 1;
+      return SPP_OK;
+    }
+  }
+  const int64_t p = h->ts_idx > 0 ? std::min(h->ts_idx - 1, len - 1) : len - 1;
+  int64_t* d = nullptr;
+  SPP_CHECK_HIP(hipMallocAsync((void**)&d, 2 * sizeof(int64_t), st));
+  hipLaunchKernelGGL(k_replay_last_rollout, dim3(1), dim3(1024), 0, st, (const uint8_t*)h->d.end, len, p, d);
+  int64_t hb[2] = {-1, -1};
+  SPP_CHECK_HIP(hipMemcpyAsync(hb, d, sizeof(hb), hipMemcpyDeviceToHost, st));
+  SPP_CHECK_HIP(hipFreeAsync(d, st));
+  SPP_CHECK_HIP(hipStreamSynchronize(st));
+  SPP_REQUIRE(hb[0] >= 0 && hb[1] >= 0, SPP_E_STATE, "last_rollout: no episode end in the buffer");
+  int64_t T = (hb[0] - hb[1]) % len;
+  if (T <= 0) T += len;
+  *first = (hb[1] + 1) % len;
+  *length = T;
   return SPP_OK;
 }
 
@@ -2051,6 +2119,130 @@ sppStatus sppOnpAct(sppOnPolicyHandle o, const float* x, int N, const float* eps
   OnpArgs p = onp_args(o, N);
   p.X = x; p.EPS = eps; p.ACT_OUT = act_out; p.LP_OUT = logp_out;
   hipLaunchKernelGGL(o->ks.act, dim3(onp_grid(o, N)), dim3(256), 0, st, p);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// ---------------------------------------------------------------- RCCL exchange (§8e)
+// librccl is resolved at run time (the one torch already loaded, if any), so the library has no
+// link-time RCCL dependency and a C/C++ host can run data parallelism without torch.distributed.
+namespace {
+struct RcclUid {
+  char internal[SPP_COMM_ID_BYTES];
+};
+struct Rccl {
+  int (*get_uid)(RcclUid*) = nullptr;
+  int (*init_rank)(void**, int, RcclUid, int) = nullptr;
+  int (*destroy)(void*) = nullptr;
+  int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*group_start)() = nullptr;
+  int (*group_end)() = nullptr;
+  const char* (*err)(int) = nullptr;
+  bool ok = false;
+};
+Rccl& rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r;
+  tried = true;
+  void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) lib = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) return r;
+  r.get_uid = (int (*)(RcclUid*))dlsym(lib, "ncclGetUniqueId");
+  r.init_rank = (int (*)(void**, int, RcclUid, int))dlsym(lib, "ncclCommInitRank");
+  r.destroy = (int (*)(void*))dlsym(lib, "ncclCommDestroy");
+  r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(lib, "ncclAllReduce");
+  r.group_start = (int (*)())dlsym(lib, "ncclGroupStart");
+  r.group_end = (int (*)())dlsym(lib, "ncclGroupEnd");
+  r.err = (const char* (*)(int))dlsym(lib, "ncclGetErrorString");
+  r.ok = r.get_uid && r.init_rank && r.destroy && r.all_reduce && r.group_start && r.group_end && r.err;
+  return r;
+}
+constexpr int kNcclFloat32 = 7, kNcclSum = 0;
+}  // namespace
+
+#define SPP_CHECK_RCCL(expr)                                                                   \
+  do {                                                                                         \
+    const int r_ = (expr);                                                                     \
+    if (r_ != 0) {                                                                             \
+      ::spp::set_error("%s:%d %s -> rccl %d (%s)", __FILE__, __LINE__, #expr, r_, rccl().err(r_)); \
+      return SPP_E_RCCL;                                                                       \
+    }                                                                                          \
+  } while (0)
+
+__global__ void k_scale(float* x, int64_t n, float s) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= s;
+}
+
+sppStatus sppCommGetUniqueId(void* uid_out) {
+  SPP_REQUIRE(uid_out, SPP_E_INVALID_ARG, "comm uid: null");
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  RcclUid u;
+  SPP_CHECK_RCCL(rccl().get_uid(&u));
+  memcpy(uid_out, &u, sizeof(u));
+  return SPP_OK;
+}
+
+sppStatus sppCommInitRank(void** comm_out, int nranks, const void* uid, int rank, int device) {
+  SPP_REQUIRE(comm_out && uid && nranks > 0 && rank >= 0 && rank < nranks, SPP_E_INVALID_ARG,
+              "comm init: nranks %d rank %d", nranks, rank);
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  SPP_CHECK_HIP(hipSetDevice(device));
+  RcclUid u;
+  memcpy(&u, uid, sizeof(u));
+  void* c = nullptr;
+  SPP_CHECK_RCCL(rccl().init_rank(&c, nranks, u, rank));
+  *comm_out = c;
+  return SPP_OK;
+}
+
+sppStatus sppCommDestroy(void* comm) {
+  SPP_REQUIRE(comm, SPP_E_INVALID_ARG, "comm destroy: null");
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  SPP_CHECK_RCCL(rccl().destroy(comm));
+  return SPP_OK;
+}
+
+// In-place average of one exchange bucket over the communicator (ncclSum, then x 1/world: the same
+// arithmetic as spprl.dp.make_allreduce), stream-ordered between *Grads and *Apply.
+sppStatus sppAllReduceGrads(sppAgentHandle h, int bucket, int world, void* rccl_comm, void* stream) {
+  SPP_REQUIRE(h && rccl_comm && world > 0 && bucket >= SPP_BUCKET_CRITIC && bucket <= SPP_BUCKET_ALL,
+              SPP_E_INVALID_ARG, "allreduce grads: bucket %d world %d", bucket, world);
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  hipStream_t st = S(stream);
+  std::vector<std::pair<float*, int64_t>> bufs;
+  auto add = [&](int net) {
+    if (h->net[net].g && h->nsize[net] > 0) bufs.push_back({h->net[net].g, h->nsize[net]});
+  };
+  const bool all = bucket == SPP_BUCKET_ALL;
+  if (all || bucket == SPP_BUCKET_CRITIC) {
+    add(SPP_NET_CRITIC1);
+    if (!h->ddpg) add(SPP_NET_CRITIC2);
+  }
+  if (all || bucket == SPP_BUCKET_ACTOR) {
+    add(SPP_NET_ACTOR);
+    if (!h->ddpg) bufs.push_back({h->alpha_grad, 1});
+  }
+  if ((all || bucket == SPP_BUCKET_ACM) && !h->plain) add(SPP_NET_ACM);
+  SPP_REQUIRE(!bufs.empty(), SPP_E_STATE, "allreduce grads: no gradient buffer bound for bucket %d", bucket);
+  SPP_CHECK_RCCL(rccl().group_start());
+  for (auto& b : bufs) {
+    const int r = rccl().all_reduce(b.first, b.first, (size_t)b.second, kNcclFloat32, kNcclSum, rccl_comm, st);
+    if (r != 0) {
+      rccl().group_end();
+      set_error("ncclAllReduce -> rccl %d (%s)", r, rccl().err(r));
+      return SPP_E_RCCL;
+    }
+  }
+  SPP_CHECK_RCCL(rccl().group_end());
+  if (world > 1) {
+    const float inv = 1.0f / (float)world;
+    for (auto& b : bufs)
+      hipLaunchKernelGGL(k_scale, dim3(std::max(1, std::min(cdiv(b.second, 256), 1024))), dim3(256), 0, st, b.first,
+                         b.second, inv);
+  }
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

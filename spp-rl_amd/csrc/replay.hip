@@ -98,6 +98,45 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm(ReplayDev r, const int6
   stage_rows(r.acm, rt, r.ac, valid, stg, AENV, Bp, b0);
 }
 
+// last_end (replay_buffer.py:170-177) and the walk of last_rollout (:335-383): out[0] = the first
+// index at distance 0, 1, ... back from p (cyclic over [0, len)) with end set; out[1] = the first
+// one at distance 1 .. len back from out[0] (itself when it is the only end).  -1: none.
+__global__ __launch_bounds__(1024) void k_replay_last_rollout(const uint8_t* __restrict__ end, int64_t len, int64_t p,
+                                                              int64_t* out) {
+  __shared__ int best;
+  __shared__ int64_t at;
+  const int tid = threadIdx.x;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int64_t from = pass == 0 ? p : at;
+    const int64_t k0 = pass, k1 = pass == 0 ? len : len + 1;  // distance range [k0, k1)
+    if (tid == 0) best = 0x7fffffff;
+    __syncthreads();
+    for (int64_t base = k0; base < k1; base += 1024) {
+      const int64_t k = base + tid;
+      if (k < k1) {
+        int64_t i = (from - k) % len;
+        if (i < 0) i += len;
+        if (end[i]) atomicMin(&best, (int)(k - base));
+      }
+      __syncthreads();
+      const int b = best;
+      __syncthreads();
+      if (b != 0x7fffffff) {
+        if (tid == 0) {
+          int64_t i = (from - (base + b)) % len;
+          at = i < 0 ? i + len : i;
+        }
+        break;
+      }
+      if (base + 1024 >= k1 && tid == 0) at = -1;
+    }
+    __syncthreads();
+    if (tid == 0) out[pass] = at;
+    if (at < 0) return;  // uniform (read after the barrier)
+    __syncthreads();
+  }
+}
+
 // rbuffer_sample_acm (:404-430) + AcMTrainer.acm_cat (acm.py:260-264): row-major
 // x[b] = [obs | next_obs], y[b] = acm action; kStageTile samples per workgroup,
 // consecutive lanes read and write consecutive floats of one row.

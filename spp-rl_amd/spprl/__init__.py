@@ -11,6 +11,6 @@ from .sac_acm import SAC_AcM  # noqa: F401
 from .sac import SAC  # noqa: F401
 from .ddpg_acm import DDPG_AcM  # noqa: F401
 from .ppo_acm import PPO_AcM  # noqa: F401
-from .trainer import HostVecEnv, SynthVecEnv  # noqa: F401
+from .trainer import HostSynthEnv, HostVecEnv, SynthVecEnv  # noqa: F401
 
-__all__ = ["SAC", "SAC_AcM", "DDPG_AcM", "PPO_AcM", "SynthVecEnv", "HostVecEnv", "BufferAcMOffPolicy", "ReplayBuffer", "SppError", "load"]
+__all__ = ["SAC", "SAC_AcM", "DDPG_AcM", "PPO_AcM", "SynthVecEnv", "HostVecEnv", "HostSynthEnv", "BufferAcMOffPolicy", "ReplayBuffer", "SppError", "load"]

@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("SPPRL_LIB") or os.path.join(HERE, "libspprl.so")
 (SPP_NET_ACTOR, SPP_NET_CRITIC1, SPP_NET_CRITIC2, SPP_NET_CRITIC1_TARG, SPP_NET_CRITIC2_TARG, SPP_NET_ACM,
  SPP_NET_ACTOR_TARG) = range(7)
 SPP_ALGO_SAC_ACM, SPP_ALGO_DDPG_ACM, SPP_ALGO_SAC = 1, 2, 3
+SPP_BUCKET_CRITIC, SPP_BUCKET_ACTOR, SPP_BUCKET_ACM, SPP_BUCKET_ALL = range(4)
+SPP_COMM_ID_BYTES = 128
 NUM_LOSSES = 8
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
@@ -70,6 +72,12 @@ _SIGS = {
                                 c_void_p, c_void_p]),
     "sppReplayObsStats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "sppReplayGetView": (c_int, [c_void_p, P(ReplayView)]),
+    "sppReplayCreateEx": (c_int, [P(c_void_p), c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "sppReplayLastRollout": (c_int, [c_void_p, P(c_int64), P(c_int64), c_void_p]),
+    "sppCommGetUniqueId": (c_int, [c_void_p]),
+    "sppCommInitRank": (c_int, [P(c_void_p), c_int, c_void_p, c_int, c_int]),
+    "sppCommDestroy": (c_int, [c_void_p]),
+    "sppAllReduceGrads": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sppAgentCreate": (c_int, [P(c_void_p), P(AgentConfig), c_int]),
     "sppAgentDestroy": (c_int, [c_void_p]),
     "sppAgentNetSize": (c_int, [c_void_p, c_int, P(c_int64)]),

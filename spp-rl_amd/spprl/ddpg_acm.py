@@ -80,7 +80,8 @@ class DDPG_AcM(OffPolicyLoop):
         m_lim = np.full(ac, float(ac_high), np.float32)  # unused by BasicAcM (its scale is t1)
         call("sppAgentSetLimits", self._h, a_lim.ctypes.data_as(ctypes.c_void_p), m_lim.ctypes.data_as(ctypes.c_void_p))
         self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
-                                                min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
+                                                min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm,
+                                                n_envs=int(unused.get("n_envs", 1)))
         rb = self.replay_buffer
         call("sppAgentBindNormalizer", self._h, ptr(rb.min_obs), ptr(rb.max_obs), ptr(rb.obs_mean), ptr(rb.obs_std))
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)

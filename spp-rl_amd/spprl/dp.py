@@ -64,3 +64,44 @@ def shard_batch(B, world):
     if B % world:
         raise ValueError("global batch %d not divisible by world size %d" % (B, world))
     return B // world
+
+
+class NativeComm:
+    """An RCCL communicator owned by libspprl (sppCommGetUniqueId / sppCommInitRank), for hosts
+    that run the §8e exchange through the C-ABI (sppAllReduceGrads) rather than
+    torch.distributed.  ``share_uid(buf)`` ships rank 0's 128-byte id to every rank (any channel,
+    e.g. a gloo broadcast) and returns it."""
+
+    def __init__(self, rank, world, device, share_uid):
+        import ctypes
+
+        from . import _lib
+
+        self.rank, self.world = int(rank), int(world)
+        uid = ctypes.create_string_buffer(_lib.SPP_COMM_ID_BYTES)
+        if self.rank == 0:
+            _lib.call("sppCommGetUniqueId", uid)
+        raw = share_uid(bytes(uid.raw))
+        uid = ctypes.create_string_buffer(bytes(raw), _lib.SPP_COMM_ID_BYTES)
+        self.comm = ctypes.c_void_p()
+        _lib.call("sppCommInitRank", ctypes.byref(self.comm), self.world, uid, self.rank, int(device))
+
+    def allreduce_for(self, agent):
+        """``allreduce(bucket)`` over the agent's exchange buckets (bucket_critic / _actor / _acm),
+        averaged in place on the current stream by sppAllReduceGrads."""
+        from . import _lib
+
+        ids = {id(agent.bucket_critic): _lib.SPP_BUCKET_CRITIC, id(agent.bucket_actor): _lib.SPP_BUCKET_ACTOR,
+               id(agent.bucket_acm): _lib.SPP_BUCKET_ACM}
+
+        def allreduce(bucket):
+            _lib.call("sppAllReduceGrads", agent._h, ids[id(bucket)], self.world, self.comm, _lib.stream_handle())
+
+        return allreduce
+
+    def close(self):
+        from . import _lib
+
+        if self.comm:
+            _lib.call("sppCommDestroy", self.comm)
+            self.comm = None

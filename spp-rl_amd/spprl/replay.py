@@ -13,9 +13,59 @@ from . import _lib
 from ._lib import call, ptr, stream_handle
 
 
+class Memory:
+    """What rltoolkit's last_rollout returns (buffer/memory.py:131-270 Memory / MemoryAcM, one
+    rollout): ``obs`` [T, ob] and ``next_obs`` [T, ob] of the episode, ``actions`` [T, aout],
+    ``rewards`` [T], ``done`` / ``end`` [T] (the end flags; the last is set), ``actions_acm`` [T, ac]
+    and the buffer's normaliser state (``normalize`` / ``denormalize`` as the buffer's)."""
+
+    def __init__(self, obs_all, actions, rewards, end, actions_acm, buffer):
+        self._obs_all = obs_all  # [T + 1, ob]: the episode's observations and the final next_obs
+        self.actions, self.rewards, self.actions_acm = actions, rewards, actions_acm
+        self.done = self.end = end
+        self.min_max_denormalize = buffer.min_max_denormalize
+        self.obs_mean, self.obs_std = buffer.obs_mean.clone(), buffer.obs_std.clone()
+        self.min_obs, self.max_obs = buffer.min_obs.clone(), buffer.max_obs.clone()
+        self._buffer = buffer
+
+    @property
+    def obs(self):
+        return self._obs_all[:-1]
+
+    @property
+    def next_obs(self):
+        return self._obs_all[1:]
+
+    @property
+    def norm_obs(self):
+        return self._buffer.normalize(self.obs, force=True)
+
+    @property
+    def norm_next_obs(self):
+        return self._buffer.normalize(self.next_obs, force=True)
+
+    def __len__(self):
+        return int(self.rewards.shape[0])
+
+    @property
+    def returns_rollouts(self):  # memory.py:202-212
+        return np.array([float(self.rewards.double().sum())])
+
+    @property
+    def rollouts_no(self):  # memory.py:214-216
+        return int(self.end.sum())
+
+    @property
+    def average_returns_per_rollout(self):
+        return float(self.returns_rollouts.sum()) / self.rollouts_no
+
+
 class BufferAcMOffPolicy:
+    HAS_ACM = True
+
     def __init__(self, size, obs_shape, act_shape, acm_act_shape, device="cuda", min_max_denormalize=False,
-                 obs_mean=None, obs_std=None, max_obs=None, min_obs=None, obs_norm=False, dtype=torch.float32):
+                 obs_mean=None, obs_std=None, max_obs=None, min_obs=None, obs_norm=False, dtype=torch.float32,
+                 n_envs=1):
         _lib.load()
         self.size, self.obs_shape, self.act_shape, self.acm_act_shape = int(size), obs_shape, act_shape, acm_act_shape
         self.device = torch.device(device)
@@ -24,7 +74,8 @@ class BufferAcMOffPolicy:
         self.min_max_denormalize = min_max_denormalize
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = ctypes.c_void_p()
-        call("sppReplayCreate", ctypes.byref(h), self.size, obs_shape, act_shape, acm_act_shape, dev)
+        call("sppReplayCreateEx", ctypes.byref(h), self.size, obs_shape, act_shape, acm_act_shape, int(n_envs), 1, 0,
+             dev)
         self._h = h
         z = lambda v: None if v is None else torch.as_tensor(v, dtype=torch.float32, device=self.device)  # noqa
         # ReplayBuffer.__init__ :113-115: identity z-score normaliser until the first stats update
@@ -123,6 +174,22 @@ class BufferAcMOffPolicy:
             obs, nobs = self.normalize(obs), self.normalize(nobs)
         return [obs, nobs, act, rew, done, acm]
 
+    def last_rollout(self):
+        """BufferAcMOffPolicy.last_rollout (:335-383): the last complete episode (device search for
+        the end flags, one gather of its transitions)."""
+        first, length = ctypes.c_int64(), ctypes.c_int64()
+        call("sppReplayLastRollout", self._h, ctypes.byref(first), ctypes.byref(length), stream_handle())
+        T, n = length.value, len(self)
+        idx = (first.value + torch.arange(T, dtype=torch.int64)) % n
+        norm, self.obs_norm = self.obs_norm, False  # raw observations (make_obs_memory_tensor)
+        try:
+            obs, nobs, act, rew, _, acm = BufferAcMOffPolicy.gather(self, idx)
+        finally:
+            self.obs_norm = norm
+        end = torch.zeros(T, dtype=torch.bool, device=self.device)
+        end[-1] = True
+        return Memory(torch.cat([obs, nobs[-1:]]), act, rew, end, acm if self.HAS_ACM else None, self)
+
     def sample_batch(self, batch_size=64, device=None):
         """idx = np.random.randint(0, len, B) from numpy's global stream (replay_buffer.py:234)."""
         idx = np.random.randint(0, len(self), batch_size)
@@ -205,6 +272,7 @@ class BufferAcMOffPolicy:
 class ReplayBuffer(BufferAcMOffPolicy):
     """ReplayBuffer (rltoolkit/buffer/replay_buffer.py:99-261): the same HBM obs-index ring
     without the ACM action; ``sample_batch`` returns (obs, next_obs, action, reward, done)."""
+    HAS_ACM = False
 
     def __init__(self, size, obs_shape, act_shape, device="cuda", **kw):
         super().__init__(size, obs_shape, act_shape, act_shape, device=device, **kw)

@@ -120,14 +120,16 @@ class SAC_AcM(OffPolicyLoop):
         if vanilla:
             if obs_norm:
                 raise NotImplementedError("vanilla SAC with obs_norm=True is not on the device path")
-            self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=False)
+            self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=False,
+                                              n_envs=int(unused.get("n_envs", 1)))
             # identity denormalisation of the actor output: min-max over [-1, 1] is 0 + x * 1, exact
             self._ident = torch.stack([-torch.ones(ob), torch.ones(ob), torch.zeros(ob), torch.ones(ob)]).to(self.device)
             call("sppAgentBindNormalizer", self._h, ptr(self._ident[0]), ptr(self._ident[1]), ptr(self._ident[2]),
                  ptr(self._ident[3]))
         else:
             self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
-                                                    min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm)
+                                                    min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm,
+                                                    n_envs=int(unused.get("n_envs", 1)))
             self.bind_normalizer(self.replay_buffer)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
         self._init_loop(update_batch_size=update_batch_size, **unused)

@@ -148,11 +148,14 @@ class HostVecEnv:
     def __init__(self, envs, device="cuda", env_fn=None, n_stage=4):
         self.env_fn = env_fn
         self.envs = list(envs)
-        self.n = len(self.envs)
         e0 = self.envs[0]
-        self.ob = int(np.prod(e0.observation_space.shape))
-        self.ac = int(np.prod(e0.action_space.shape))
-        self._max_episode_steps = getattr(e0, "_max_episode_steps", None)
+        self._init_staging(len(self.envs), int(np.prod(e0.observation_space.shape)),
+                           int(np.prod(e0.action_space.shape)), getattr(e0, "_max_episode_steps", None), device,
+                           n_stage)
+
+    def _init_staging(self, n, ob, ac, max_episode_steps, device, n_stage):
+        self.n, self.ob, self.ac = int(n), int(ob), int(ac)
+        self._max_episode_steps = max_episode_steps
         self.device = torch.device(device)
         self.side = torch.cuda.Stream(device=self.device)
         pin = dict(pin_memory=True)
@@ -196,11 +199,23 @@ class HostVecEnv:
 
     def reset(self, mask=None):
         h_obs, _, _ = self._writable(carry=mask is not None)
-        idx = range(self.n) if mask is None else np.flatnonzero(mask)
-        for e in idx:
-            h_obs[e] = torch.as_tensor(np.asarray(self.envs[e].reset(), np.float32).reshape(-1))
+        idx = np.arange(self.n) if mask is None else np.flatnonzero(mask)
+        self._reset_rows(idx, h_obs)
         self._upload()
         return self.obs
+
+    def _reset_rows(self, idx, h_obs):
+        for e in idx:
+            h_obs[e] = torch.as_tensor(np.asarray(self.envs[e].reset(), np.float32).reshape(-1))
+
+    def _step_rows(self, act, h_obs, h_rew):
+        end = np.zeros(self.n, bool)
+        for e, env in enumerate(self.envs):
+            o, r, d, _ = env.step(act[e])
+            h_obs[e] = torch.as_tensor(np.asarray(o, np.float32).reshape(-1))
+            h_rew[e] = float(r)
+            end[e] = bool(d)
+        return end
 
     def send(self, action):
         """Start the D2H copy of the actions (non-blocking)."""
@@ -216,12 +231,7 @@ class HostVecEnv:
         self._pending = False
         act = self.h_act.numpy()
         h_obs, h_rew, h_end = self._writable(carry=False)
-        end = np.zeros(self.n, bool)
-        for e, env in enumerate(self.envs):
-            o, r, d, _ = env.step(act[e])
-            h_obs[e] = torch.as_tensor(np.asarray(o, np.float32).reshape(-1))
-            h_rew[e] = float(r)
-            end[e] = bool(d)
+        end = self._step_rows(act, h_obs, h_rew)
         h_end.copy_(torch.from_numpy(end.astype(np.uint8)))
         self._upload()
         return self.obs, self.rew, end, self.end_dev
@@ -241,6 +251,48 @@ class HostVecEnv:
         return out
 
 
+class HostSynthEnv(HostVecEnv):
+    """E SynthEnv instances (SURVEY.md Appendix A dynamics, as SynthVecEnv) stepped on the HOST in
+    one vectorised numpy call per step -- the stand-in for a CPU simulator pool (MuJoCo is not in
+    this image) behind HostVecEnv's pinned staging and side-stream copies, so the loop measures the
+    host-env boundary: D2H actions, the host step overlapped with the queued update, H2D obs."""
+
+    def __init__(self, n_envs, ob, ac, max_episode_steps=1000, ac_high=1.0, seed=0, dyn_seed=1234, device="cuda",
+                 n_stage=4):
+        self.envs, self.env_fn = [], None
+        self._init_staging(n_envs, ob, ac, int(max_episode_steps), device, n_stage)
+        g = torch.Generator(device="cpu").manual_seed(dyn_seed)
+        self.A = (torch.randn(ob, ob, generator=g) * 0.05).numpy()
+        self.ac_high = float(ac_high)
+        self._rng = np.random.RandomState(seed)
+        self._s = np.zeros((self.n, ob), np.float32)
+        self._t = np.zeros(self.n, np.int64)
+        self._seed = seed
+
+    def _reset_rows(self, idx, h_obs):
+        self._s[idx] = self._rng.randn(len(idx), self.ob).astype(np.float32)
+        self._t[idx] = 0
+        h_obs.numpy()[idx] = self._s[idx]
+
+    def _step_rows(self, act, h_obs, h_rew):
+        a = np.asarray(act, np.float32)  # s'_i = tanh(A_i . s) + 0.1 a[i % ac] (k_synth_env)
+        s = np.tanh(self._s @ self.A.T) + np.float32(0.1) * a[:, np.arange(self.ob) % self.ac]
+        self._s = s.astype(np.float32)
+        h_obs.numpy()[:] = self._s
+        h_rew.numpy()[:] = -(a * a).sum(1) + self._s[:, 0]
+        self._t += 1
+        return self._t >= self._max_episode_steps
+
+    def spawn(self, n_envs, seed):
+        return HostSynthEnv(n_envs, self.ob, self.ac, self._max_episode_steps, self.ac_high, seed=seed,
+                            device=self.device)
+
+    def sample_actions(self, out):
+        out.copy_(torch.from_numpy(self._rng.uniform(-self.ac_high, self.ac_high, (self.n, self.ac)).astype(
+            np.float32)))
+        return out
+
+
 # ---------------------------------------------------------------- loop
 
 
@@ -255,7 +307,8 @@ class OffPolicyLoop:
                    acm_update_batches=config.ACM_UPDATE_BATCHES, acm_pre_train_samples=config.ACM_PRE_TRAIN_SAMPLES,
                    acm_pre_train_epochs=config.ACM_PRE_TRAIN_N_EPOCHS, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
                    acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=config.ACM_KEEP_PRE_TRAIN,
-                   n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, **unused):
+                   n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, tensorboard_dir=None,
+                   debug_mode=False, **unused):
         if max_frames is not None and max_frames > iterations * batch_size:
             raise AssertionError("max_frames should be smaller or equal than iterations * batch_size")  # rl.py:166
         self.iterations, self.batch_size, self.stats_freq = int(iterations), int(batch_size), int(stats_freq)
@@ -270,6 +323,13 @@ class OffPolicyLoop:
         self._acm_sched_epochs = 0  # StepLR.last_epoch
         self.iteration = 0
         self.stats_logger = StatsLogger()
+        # rl.py:67-83: a TensorBoard writer when tensorboard_dir is given (scalar panels, spprl/tb.py)
+        self.tensorboard_dir, self.debug_mode = tensorboard_dir, bool(debug_mode)
+        self.tensorboard_writer = None
+        if tensorboard_dir is not None:
+            from .tb import TensorboardWriter
+
+            self.tensorboard_writer = TensorboardWriter(tensorboard_dir)
         ob, ac = self.ob_dim, self.ac_dim
         if env is None:
             spec = getattr(self, "env_spec", None) or config.ENV_SPECS.get(self.env_name, (ob, ac, 1.0, 1000))
@@ -334,12 +394,26 @@ class OffPolicyLoop:
         self.logs_after_iteration(ret, done=True)
         return self.stats_logger.running_return
 
-    def logs_after_iteration(self, ret, done=False):
+    def logs_after_iteration(self, ret, done=False):  # rl.py:320-368
         if self.test_episodes:
             self.stats_logger.test_return = self.test()
+        loss = dict(self.loss)
         self.stats_logger.stats.append({"iteration": self.iteration, "frames": self.stats_logger.frames,
                                         "running_return": self.stats_logger.running_return,
-                                        "test_return": self.stats_logger.test_return, "loss": dict(self.loss)})
+                                        "test_return": self.stats_logger.test_return, "loss": loss})
+        w = self.tensorboard_writer
+        if w is not None:  # add_tensorboard_logs (rl.py:344-368): the scalar panels
+            sl = self.stats_logger
+            if sl.running_return is not None:
+                w.log_running_return(self.iteration, sl.frames, sl.rollouts, sl.running_return)
+            if self.test_episodes:
+                w.log_test_return(self.iteration, sl.frames, sl.rollouts, sl.test_return)
+            w.log_loss(self.iteration, loss)
+            if self.debug_mode and hasattr(self, "current_alpha"):  # sac.py:233-236
+                w.log_sac_alpha(self.iteration, self.current_alpha())
+            w.flush()
+            if done:
+                w.close()
 
     # ---------------------------------------------------------- DDPG.perform_iteration (ddpg.py:159-170)
     def perform_iteration(self):

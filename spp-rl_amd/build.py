@@ -56,22 +56,71 @@ def _stale(src):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+
+
+def _resources(text):
+    """{kernel: {vgpr, agpr, vgpr_spill, sgpr_spill, lds}} from -Rpass-analysis=kernel-resource-usage."""
+    import re
+
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+(VGPRs|AGPRs|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur is not None:
+            key = {"VGPRs": "vgpr", "AGPRs": "agpr", "VGPRs Spill": "vgpr_spill", "SGPRs Spill": "sgpr_spill",
+                   "LDS Size [bytes/block]": "lds"}[m.group(1)]
+            cur[key] = int(m.group(2))
+    return out
+
+
 def _compile(src, verbose):
     obj = _obj(src)
-    cmd = [HIPCC] + FLAGS + ["-c", "-o", obj, src]
+    cmd = [HIPCC] + FLAGS + ["-Rpass-analysis=kernel-resource-usage", "-c", "-o", obj, src]
     t0 = time.time()
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stdout[-8000:]))
+    import json
+
+    with open(obj + ".res.json", "w") as f:
+        json.dump(_resources(r.stdout), f, indent=0)
     if verbose:
         print("  %-22s %5.0fs" % (os.path.basename(src), time.time() - t0), flush=True)
     return obj
+
+
+# Phase kernels whose VGPRs spill to scratch have produced wrong results (DESIGN.md §8:
+# the round-1 fragment prefetch, the DDPG Ant actor phase before its heads were parked): the
+# build lists every kernel with VGPR scratch spills (build/kernel_resources.json) so a spill
+# introduced by a change is seen at build time; the GPU parity tests cover each such kernel.
+def report_spills(objs, verbose=True):
+    import json
+
+    allres = {}
+    for o in objs:
+        try:
+            with open(o + ".res.json") as f:
+                allres.update(json.load(f))
+        except OSError:
+            pass
+    with open(os.path.join(OBJ, "kernel_resources.json"), "w") as f:
+        json.dump(allres, f, indent=1, sort_keys=True)
+    spills = {k: v["vgpr_spill"] for k, v in allres.items() if v.get("vgpr_spill", 0) > 0}
+    if verbose and spills:
+        print("kernels with VGPR scratch spills:")
+        for k, n in sorted(spills.items(), key=lambda kv: -kv[1]):
+            print("  %4d  %s" % (n, k[:150]))
+    return spills
 
 
 def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, nodense=False):
     if prof:  # region-timing variant (never the default library): single TU
         out = os.path.join(HERE, "spprl", "libspprl_prof.so")
         extra = (["-DSPP_ONLY_HOPPER"] if hopper_only else []) + (["-DSPP_PROF_NODENSE"] if nodense else []) + (
+            ["-DSPP_ONLY_BF16"] if "--bf16-only" in sys.argv else []) + (
             ["-DSPP_PROF_DRAIN"] if "--drain" in sys.argv else [])
         cmd = [HIPCC] + FLAGS + ["-shared", "-DSPP_PROF", "-DSPP_SINGLE_TU"] + extra + [
             "-o", out, os.path.join(CSRC, "api.hip")]
@@ -91,6 +140,7 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(lambda s: _compile(s, verbose), todo))
     objs = [_obj(s) for s in srcs]
+    report_spills(objs, verbose)
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs)
     os.replace(OUT + ".tmp", OUT)
     if verbose:

@@ -24,11 +24,16 @@
 #include "kset.h"
 #ifdef SPP_SINGLE_TU  // profiling / development builds: everything in one TU
 #include "ks_sac_hopper.hip"
+#if defined(SPP_ONLY_BF16)  // region-profiling builds of the bf16 sets: Hopper fp32 + bf16 only
+#define SPP_ONLY_HOPPER
+#include "ks_sac_bf16.hip"
+#endif
 #ifndef SPP_ONLY_HOPPER
 #include "ks_sac_hcheetah.hip"
 #include "ks_sac_ant.hip"
 #include "ks_sac_small.hip"
 #include "ks_ddpg.hip"
+#include "ks_ddpg_ant.hip"
 #include "ks_sac_bf16.hip"
 #include "ks_sac_vanilla.hip"
 #endif
@@ -670,7 +675,7 @@ struct DwSet {
 // compiled in parallel by build.py and linked into libspprl.so.
 static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, KernelSet* ks) {
   if (bf16) {
-#ifndef SPP_ONLY_HOPPER
+#if !defined(SPP_ONLY_HOPPER) || defined(SPP_ONLY_BF16)
     return algo == SPP_ALGO_SAC_ACM && kset_sac_bf16(ob, aout, ac, acmc, ks);
 #else
     return false;
@@ -691,6 +696,7 @@ static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, 
     if (kset_sac_small(ob, aout, ac, acmc, ks)) return true;
   } else if (algo == SPP_ALGO_DDPG_ACM) {
     if (kset_ddpg(ob, aout, ac, acmc, ks)) return true;
+    if (kset_ddpg_ant(ob, aout, ac, acmc, ks)) return true;
 #endif
   }
   return false;
@@ -739,6 +745,8 @@ struct sppAgent {
   float *AH1 = nullptr, *AH2 = nullptr, *AD1 = nullptr, *AD2 = nullptr, *ADH = nullptr;
   float *Z1 = nullptr, *Z2 = nullptr, *T3 = nullptr, *part = nullptr;
   float *aux = nullptr;  // [4] alpha grad operand (all-reduced in DP)
+  float* GAD = nullptr;       // wide-head actor phase: d a_d hand-over [aout][Bp]
+  uint64_t* MASK = nullptr;   // and the trunk's ReLU masks [tile][4][64]
   // ACM regression scratch
   float *RX = nullptr, *RZ1 = nullptr, *RZ2 = nullptr, *RP1 = nullptr, *RP2 = nullptr, *RP3 = nullptr;
   // weight-gradient job sets: [0] SAC (critic phase, actor phase), [1] ACM regression
@@ -1266,6 +1274,8 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   const int64_t oRX = take(2 * ob), oRZ1 = take(dd ? 128 : 64), oRZ2 = take(dd ? 64 : 32), oRP1 = take(dd ? 128 : 64),
                 oRP2 = take(dd ? 64 : 32), oRP3 = take(ac);
   const int64_t oRS21 = dd ? take(64) : 0, oRPZ21 = dd ? take(64) : 0;
+  // wide-head actor phase hand-over: d a_d [aout][Bp], ReLU masks (4 x u64 per lane = 16 floats per sample)
+  const int64_t oGAD = take(aout), oMASK = take(16);
   const int64_t oPart = total;
   total += ntiles * kBParts + 64;
   const int64_t oAux = total;
@@ -1284,6 +1294,8 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   }
   a->AH1 = b + oAH1; a->AH2 = b + oAH2; a->AD1 = b + oAD1; a->AD2 = b + oAD2; a->ADH = b + oADH;
   a->Z1 = b + oZ1; a->Z2 = b + oZ2; a->T3 = b + oT3;
+  a->GAD = b + oGAD;
+  a->MASK = reinterpret_cast<uint64_t*>(b + oMASK);
   a->RX = b + oRX; a->RZ1 = b + oRZ1; a->RZ2 = b + oRZ2; a->RP1 = b + oRP1; a->RP2 = b + oRP2; a->RP3 = b + oRP3;
   if (dd) {
     a->bz = BAcmScratch{a->Z1, a->Z2, a->T3};
@@ -1446,10 +1458,11 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   // repack the updated critics
   launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), st);
   SacArgs p = make_args(a, B);
-  AcmScratch z{a->Z1, a->Z2, a->T3};
+  AcmScratch z{a->Z1, a->Z2, a->T3, a->GAD, a->MASK};
   const int grid = phase_grid(a, p.Bp);
   tmark(a, 1, st);
   hipLaunchKernelGGL(a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
+  if (a->ks.actor_heads) hipLaunchKernelGGL(a->ks.actor_heads, dim3(grid), dim3(256), 0, st, p, z);
   tmark(a, 1, st);
   SPP_CHECK_HIP(hipGetLastError());
   tmark(a, 2, st);

@@ -172,7 +172,7 @@ __device__ __forceinline__ void ddpg_head(const SacArgs& p, const Lane& L, f32x1
       const bool ok = j < C::AOUT;
       if (BRF || ok) {  // BRF: no per-unit branch around the table loads (one round trip each)
         const int jj = ok ? j : 0;
-        const float ad = denorm<(C::NB_AOUT <= 2)>(p, L.tbl, jj, fmul_rn(tanhf(u[ib][q]), actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, jj)));
+        const float ad = denorm<true>(p, L.tbl, jj, fmul_rn(tanhf(u[ib][q]), actor_lim<true>(p, L.tbl, jj)));
         if (ok) L.bl[ur * 32] = ad;
       }
     }
@@ -267,6 +267,19 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
     actor_trunk<C, true, C::NB_AOUT, C::AOUT>(p.actor, p.S, C::OB * L.ld4, L, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
     f32x16 u[C::NB_AOUT];
     ddpg_head<C>(p, L, u);
+    // Wide heads (Ant): park the fc3 pre-activation in the ADH rows the heads backward overwrites
+    // (same lane, same element) instead of keeping NB_AOUT tiles live through the critic section.
+    constexpr bool kParkHeads = C::NB_AOUT > 2;
+    const rsrc_t adhr = rsrc(p.ADH);
+    if constexpr (kParkHeads) {
+#pragma unroll
+      for (int ib = 0; ib < C::NB_AOUT; ++ib)
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) {
+          const int ur = 32 * ib + ru(q2);
+          if (ur + L.h4 < C::AOUT) fm_st(adhr, ur, L.ld4, L.vo, u[ib][q2]);
+        }
+    }
     // ---- critic input [s | ACM(s, a_d)] or [s | a_d]   (:128-132)
     f32x16 cin[C::NB_CIN];
     if constexpr (C::ACMC) {
@@ -321,8 +334,14 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
     const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
     // Branch-free over the units, loads through array-bounded resources (rows >= AOUT read 0),
     // stores after the loop: per-unit branches or interleaved stores cost a round trip per unit.
-    const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4), adhr = rsrc(p.ADH);
+    const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4);
     const bool closs = p.custom_loss != 0.f;
+    if constexpr (kParkHeads) {
+#pragma unroll
+      for (int ib = 0; ib < C::NB_AOUT; ++ib)
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) u[ib][q2] = fm_ld(adhr, 32 * ib + ru(q2), L.ld4, L.vo);
+    }
 #pragma unroll
     for (int ib = 0; ib < C::NB_AOUT; ++ib)
 #pragma unroll
@@ -332,22 +351,22 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_actor_phase(SacArgs p, BAcmScra
         const int jj = ok ? j : 0;
         const float s2 = closs ? fm_ldb(s2r, ur, L.ld4, L.vo) : 0.f;
         const float t = tanhf(u[ib][q2]);
-        const float lim = actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, jj);
+        const float lim = actor_lim<true>(p, L.tbl, jj);
         const float a = fmul_rn(t, lim);
         float g_ad = L.bl[ur * 32];
         float g_a = 0.f;
         if (closs) {
           if (p.norm_closs) {
-            const float df = fsub_rn(a, normalize<(C::NB_AOUT <= 2)>(p, L.tbl, jj, s2));
+            const float df = fsub_rn(a, normalize<true>(p, L.tbl, jj, s2));
             g_a += cl_scale * df;
             dist_part += (valid && ok) ? df * df : 0.f;
           } else {
-            const float df = fsub_rn(denorm<(C::NB_AOUT <= 2)>(p, L.tbl, jj, a), s2);
+            const float df = fsub_rn(denorm<true>(p, L.tbl, jj, a), s2);
             g_ad += cl_scale * df;
             dist_part += (valid && ok) ? df * df : 0.f;
           }
         }
-        g_a += g_ad * denorm_scale<(C::NB_AOUT <= 2)>(p, L.tbl, jj);
+        g_a += g_ad * denorm_scale<true>(p, L.tbl, jj);
         u[ib][q2] = ok ? g_a * lim * (1.f - t * t) : 0.f;
       }
 #pragma unroll
@@ -413,7 +432,7 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_policy_act(SacArgs p, ActArgs a
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ib + ru(q), j = ur + L.h4;
         if (j < C::AOUT) {
-          const float lim = actor_lim<(C::NB_AOUT <= 2)>(p, L.tbl, j);
+          const float lim = actor_lim<true>(p, L.tbl, j);
           float act;
           if (a.mode == 0) {
             act = valid ? lim * a.eps[er * C::AOUT + j] : 0.f;
@@ -422,7 +441,7 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_policy_act(SacArgs p, ActArgs a
             if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
             act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);
           }
-          if (a.denorm_out) act = denorm<(C::NB_AOUT <= 2)>(p, L.tbl, j, act);
+          if (a.denorm_out) act = denorm<true>(p, L.tbl, j, act);
           L.bl[ur * 32] = act;
           if (valid) a.target_out[er * C::AOUT + j] = act;
         }

@@ -10,6 +10,7 @@ namespace spp {
 struct KernelSet {
   void (*critic)(SacArgs);
   void (*actor)(SacArgs, AcmScratch);
+  void (*actor_heads)(SacArgs, AcmScratch);  // wide heads: second kernel of the actor phase
   void (*act)(SacArgs, ActArgs);
   void (*acmreg)(SacArgs, AcmRegArgs);
   // DDPG_AcM
@@ -22,13 +23,15 @@ struct KernelSet {
 template <int OB, int AOUT, int AC, bool ACMC, bool BF = false>
 KernelSet make_kset() {
   using C = Cfg<OB, AOUT, AC, ACMC, BF>;
-  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, k_policy_act<C>, k_acm_regress<C>,
+  void (*heads)(SacArgs, AcmScratch) = nullptr;
+  if constexpr (C::NB_PAIR > 2) heads = k_sac_actor_heads<C>;
+  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, heads, k_policy_act<C>, k_acm_regress<C>,
           nullptr, nullptr, nullptr, nullptr};
 }
 template <int OB, int AOUT, int AC, bool ACMC>
 KernelSet make_dkset() {
   using D = DCfg<OB, AOUT, AC, ACMC>;
-  return {nullptr, nullptr, nullptr, nullptr,
+  return {nullptr, nullptr, nullptr, nullptr, nullptr,
           k_ddpg_critic_phase<D>, k_ddpg_actor_phase<D>, k_ddpg_policy_act<D>, k_bacm_regress<D>};
 }
 
@@ -43,6 +46,7 @@ bool kset_sac_hcheetah(int ob, int aout, int ac, bool acmc, KernelSet* ks);  // 
 bool kset_sac_ant(int ob, int aout, int ac, bool acmc, KernelSet* ks);       // ks_sac_ant.hip
 bool kset_sac_small(int ob, int aout, int ac, bool acmc, KernelSet* ks);     // ks_sac_small.hip
 bool kset_ddpg(int ob, int aout, int ac, bool acmc, KernelSet* ks);          // ks_ddpg.hip
+bool kset_ddpg_ant(int ob, int aout, int ac, bool acmc, KernelSet* ks);      // ks_ddpg_ant.hip
 bool kset_sac_bf16(int ob, int aout, int ac, bool acmc, KernelSet* ks);      // ks_sac_bf16.hip
 bool kset_sac_vanilla(int ob, int aout, int ac, bool acmc, KernelSet* ks);   // ks_sac_vanilla.hip
 

@@ -86,9 +86,9 @@ __device__ __forceinline__ bool getbit(uint64_t lo, uint64_t hi, int ob, int q) 
 
 // memory.py:107-121 (denormalize) and :76-87 / utils.py:62-73 (normalize, force=True)
 // TB: read the kernel's LDS table T (make_args puts the limits at t_lim / t_alim and the
-// normaliser vectors at t_n0 / t_n1) instead of the global arrays.  Narrow-head kernels use the
-// table (per-slot global loads are one round trip each there); the wide-head (Ant) kernels keep
-// the global reads.
+// normaliser vectors at t_n0 / t_n1) instead of the global arrays (per-slot global loads are one
+// round trip each).  Every kernel set reads the table (TB = true); the global form stays for
+// reference.
 template <bool TB>
 __device__ __forceinline__ float nv0(const SacArgs& p, const float* T, int j) {
   if constexpr (TB) return T[p.t_n0 + j];
@@ -302,7 +302,7 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int u = ru(q) + L.h4;
-    limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, u < C::AC ? u : 0);
+    limv[q] = acm_lim<true>(p, L.tbl, u < C::AC ? u : 0);
   }
   dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, L.tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {
 #pragma unroll
@@ -372,10 +372,10 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
     for (int r = 0; r < 8; ++r) ev[ib][r] = fm_ldb(er, 16 * ib + r, L.ld4, L.vp);
-  // BRF, narrow heads: no per-slot branch (a branch holding a table load and its use costs one
-  // round trip per slot); slots j >= AOUT compute on index 0 and are dropped.  The actor phase
-  // keeps the branches: the branch-free form's live ranges spill there.
-  constexpr bool kBranchFree = BRF && C::NB_PAIR <= 2;
+  // BRF (critic phase): no per-slot branch (a branch holding a table load and its use costs one
+  // LDS round trip per slot); slots j >= AOUT compute on index 0 and are dropped.  The actor
+  // phase keeps the branches (its branch-free live ranges spill).
+  constexpr bool kBranchFree = BRF;
 #pragma unroll
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
@@ -396,8 +396,8 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         const float cj = 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
         lp += ok ? lpj : 0.f;
         corr += ok ? cj : 0.f;
-        const float a = fmul_rn(tanhf(u), actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, jj));
-        const float ad = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, jj, a);
+        const float a = fmul_rn(tanhf(u), actor_lim<true>(p, L.tbl, jj));
+        const float ad = denorm<true>(p, L.tbl, jj, a);
         if (ok) L.pl[j0 * 32] = ad;
       }
     }
@@ -516,6 +516,10 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
 // Scratch for the frozen-ACM backward (feature-major, same-lane re-read).
 struct AcmScratch {
   float *Z1, *Z2, *T3;
+  // wide heads (NB_PAIR > 2): the actor phase runs as two kernels; the first hands the second
+  // d loss / d a_d [AOUT][Bp] (GAD) and the trunk's ReLU masks [tile][4][64 lanes] (MASK)
+  float* GAD;
+  uint64_t* MASK;
 };
 
 template <class C>
@@ -630,7 +634,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       for (int q = 0; q < 16; ++q) {
         const int u = ru(q) + L.h4;
         t3v[q] = fm_ldb(t3r, ru(q), L.ld4, L.vo);
-        limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, u < C::AC ? u : 0);
+        limv[q] = acm_lim<true>(p, L.tbl, u < C::AC ? u : 0);
       }
       if constexpr (kPre) {
 #pragma unroll
@@ -699,59 +703,37 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         }
     }
     SPP_TP(16);  // ACM backward
+    if constexpr (kParkHeads) {
+      // Wide heads: the heads and trunk backward run in k_sac_actor_heads (a second kernel with
+      // the whole register file: in one kernel the live ranges spill to scratch, and spilled
+      // phase kernels have returned wrong results).  Hand over d a_d and the masks.
+      const rsrc_t gr = rsrc(z.GAD);
+#pragma unroll
+      for (int ib = 0; ib < C::NB_AOUT; ++ib)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int ur = 32 * ib + ru(q);
+          if (ur + L.h4 < C::AOUT) fm_st(gr, ur, L.ld4, L.vo, L.bl[ur * 32]);
+        }
+      uint64_t* mk = z.MASK + (int64_t)tile * 4 * 64 + lane;
+      mk[0] = a1lo;
+      mk[64] = a1hi;
+      mk[128] = a2lo;
+      mk[192] = a2hi;
+      const float ps = wave_sum((valid && L.h == 0) ? fsub_rn(alpha * lp, qmin) : 0.f);
+      const float pl = wave_sum((valid && L.h == 0) ? lp : 0.f);
+      if (lane == 0) {
+        p.part[tile * kParts + 2] = ps;
+        p.part[tile * kParts + 4] = pl;
+      }
+      continue;
+    }
     // ---- heads backward in the pairing layout (squash, denorm, custom loss, logpi)
     float sac_part = (valid && L.h == 0) ? fsub_rn(alpha * lp, qmin) : 0.f;
     float dist_part = 0.f;
     const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
     const int h8 = 8 * L.h;
-    if constexpr (kParkHeads) {
-      // wide heads: per-slot form (the branch-free form's batched loads exceed the registers)
-#pragma unroll
-      for (int ib = 0; ib < C::NB_PAIR; ++ib)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int j0 = 16 * ib + r;
-          const int j = j0 + h8;
-          float gmu = 0.f, gls = 0.f;
-          if (j < C::AOUT) {
-            const float mu = fm_ld(rsrc(p.ADH), j0, L.ld4, L.vp);
-            const float lsr = fm_ld(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp);
-            const float ls = fminf(fmaxf(lsr, -20.f), 2.f);
-            const float sc = expf(ls);
-            const float e = fm_ld(rsrc(p.EPS2), j0, L.ld4, L.vp);
-            const float u = fadd_rn(mu, fmul_rn(e, sc));
-            const float d = fsub_rn(u, mu);
-            const float t = tanhf(u);
-            const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, j);
-            const float a = fmul_rn(t, lim);
-            float g_ad = L.pl[j0 * 32];
-            float g_a = 0.f;
-            if (p.custom_loss != 0.f) {
-              const float s2 = fm_ld(rsrc(p.S2), j0, L.ld4, L.vp);
-              if (p.norm_closs) {
-                const float df = fsub_rn(a, normalize<(C::NB_PAIR <= 2)>(p, L.tbl, j, s2));
-                g_a += cl_scale * df;
-                dist_part += valid ? df * df : 0.f;
-              } else {
-                const float df = fsub_rn(denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, a), s2);
-                g_ad += cl_scale * df;
-                dist_part += valid ? df * df : 0.f;
-              }
-            }
-            g_a += g_ad * denorm_scale<(C::NB_PAIR <= 2)>(p, L.tbl, j);
-            const float var = fmul_rn(sc, sc);
-            const float sig_m2u = 1.f / (1.f + expf(2.f * u));
-            const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
-            gmu = gu + g_lp * d / var;
-            const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
-            gls = (lsr >= -20.f && lsr <= 2.f) ? gsc * sc : 0.f;
-            fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, gmu);
-            fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, gls);
-          }
-          hd[ib][r] = gmu;
-          hd[ib][r + 8] = gls;
-        }
-    } else {
+    {
       // Branch-free over the pairing slots: every lane loads through resources bounded to the
       // arrays (slots j >= AOUT read 0) and computes; results of those slots are dropped.  Per-slot
       // branches would put each load and its use in one block, i.e. one round trip per slot.
@@ -776,22 +758,22 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           const float u = fadd_rn(mu, fmul_rn(e, sc));
           const float d = fsub_rn(u, mu);
           const float t = tanhf(u);
-          const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, jj);
+          const float lim = actor_lim<true>(p, L.tbl, jj);
           const float a = fmul_rn(t, lim);
           float g_ad = L.pl[j0 * 32];  // from the critics through the ACM
           float g_a = 0.f;
           if (closs) {
             if (p.norm_closs) {
-              const float df = fsub_rn(a, normalize<(C::NB_PAIR <= 2)>(p, L.tbl, jj, s2));
+              const float df = fsub_rn(a, normalize<true>(p, L.tbl, jj, s2));
               g_a += cl_scale * df;
               dist_part += (valid && ok) ? df * df : 0.f;
             } else {
-              const float df = fsub_rn(denorm<(C::NB_PAIR <= 2)>(p, L.tbl, jj, a), s2);
+              const float df = fsub_rn(denorm<true>(p, L.tbl, jj, a), s2);
               g_ad += cl_scale * df;
               dist_part += (valid && ok) ? df * df : 0.f;
             }
           }
-          g_a += g_ad * denorm_scale<(C::NB_PAIR <= 2)>(p, L.tbl, jj);
+          g_a += g_ad * denorm_scale<true>(p, L.tbl, jj);
           const float var = fmul_rn(sc, sc);
           const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
           const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
@@ -844,6 +826,129 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
   SPP_TP_FLUSH();
 }
 
+// ============================================================================ actor phase, wide heads
+// k_sac_actor_heads: the heads backward (squash, denormalisation, custom loss, logpi, in the
+// pairing layout) and the trunk backward of the actor phase for wide heads (Ant), after
+// k_sac_actor_phase handed over d loss / d a_d (z.GAD) and the trunk's ReLU masks (z.MASK).  One
+// pairing block at a time: the block's parked heads, eps, targets and d a_d are requested together
+// (one round trip per block), the limit / normaliser vectors come from the LDS table, and the
+// results stay in registers (the WhT layer's input tile) until every load has been issued.
+template <class C>
+__global__ __launch_bounds__(256, 1) void k_sac_actor_heads(SacArgs p, AcmScratch z) {
+  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  SPP_TP_INIT();
+  load_table(p, tbl);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* big = smem + w * kLdsPerWave;
+  float* small = big + kSmallRow * 32;
+  const int ntiles = p.Bp / 32;
+  const int ld = p.Bp;
+  const float alpha = *p.alpha;
+  for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
+    const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
+    const bool valid = L.b < p.B;
+    const float g_lp = valid ? alpha * p.inv_B : 0.f;
+    const uint64_t* mk = z.MASK + (int64_t)tile * 4 * 64 + lane;
+    const uint64_t a1lo = mk[0], a1hi = mk[64], a2lo = mk[128], a2hi = mk[192];
+    float dist_part = 0.f;
+    const float cl_scale = valid ? p.custom_loss * 2.f * p.inv_B / (float)C::AOUT : 0.f;
+    const rsrc_t adhr = rsrc_n(p.ADH, 2 * C::AOUT * L.ld4);
+    const rsrc_t epsr = rsrc_n(p.EPS2, C::AOUT * L.ld4);
+    const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4);
+    const rsrc_t gr = rsrc_n(z.GAD, C::AOUT * L.ld4);
+    const bool closs = p.custom_loss != 0.f;
+    const int h8 = 8 * L.h;
+    // one pairing block per iteration (not unrolled: a block's loads and math stay within the
+    // iteration); results go to the LDS image in the pairing layout (rows j / AOUT + j)
+#pragma unroll 1
+    for (int ib = 0; ib < C::NB_PAIR; ++ib) {
+      float mu[8], lsr[8], ev[8], s2v[8], gv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j0 = 16 * ib + r;
+        mu[r] = fm_ldb(adhr, j0, L.ld4, L.vp);
+        lsr[r] = fm_ldb(adhr, C::AOUT + j0, L.ld4, L.vp);
+        ev[r] = fm_ldb(epsr, j0, L.ld4, L.vp);
+        s2v[r] = closs ? fm_ldb(s2r, j0, L.ld4, L.vp) : 0.f;
+        gv[r] = fm_ldb(gr, j0, L.ld4, L.vp);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j0 = 16 * ib + r;
+        const int j = j0 + h8;
+        const bool ok = j < C::AOUT;
+        const int jj = ok ? j : 0;
+        const float e = ev[r];
+        const float ls = fminf(fmaxf(lsr[r], -20.f), 2.f);
+        const float sc = expf(ls);
+        const float u = fadd_rn(mu[r], fmul_rn(e, sc));
+        const float d = fsub_rn(u, mu[r]);
+        const float t = tanhf(u);
+        const float lim = actor_lim<true>(p, L.tbl, jj);
+        const float a = fmul_rn(t, lim);
+        float g_ad = gv[r];  // from the critics through the ACM
+        float g_a = 0.f;
+        if (closs) {
+          if (p.norm_closs) {
+            const float df = fsub_rn(a, normalize<true>(p, L.tbl, jj, s2v[r]));
+            g_a += cl_scale * df;
+            dist_part += (valid && ok) ? df * df : 0.f;
+          } else {
+            const float df = fsub_rn(denorm<true>(p, L.tbl, jj, a), s2v[r]);
+            g_ad += cl_scale * df;
+            dist_part += (valid && ok) ? df * df : 0.f;
+          }
+        }
+        g_a += g_ad * denorm_scale<true>(p, L.tbl, jj);
+        const float var = fmul_rn(sc, sc);
+        const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
+        const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
+        const float gmu = gu + g_lp * d / var;
+        const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
+        const float gls = (lsr[r] >= -20.f && lsr[r] <= 2.f) ? gsc * sc : 0.f;
+        if (ok) {  // slot j >= AOUT would land on row AOUT + j' of a valid slot's log-std
+          L.pl[j0 * 32] = gmu;
+          L.pl[(C::AOUT + j0) * 32] = gls;
+        }
+      }
+    }
+    f32x16 hd[C::NB_PAIR];
+    load_pair<C>(hd, big);
+    // the heads' gradient operands (dW of fc_prob / fc_scale), after every load above
+#pragma unroll
+    for (int ib = 0; ib < C::NB_PAIR; ++ib)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int j0 = 16 * ib + r;
+        if (j0 + h8 < C::AOUT) {
+          fm_st(rsrc(p.ADH), j0, L.ld4, L.vp, hd[ib][r]);
+          fm_st(rsrc(p.ADH), C::AOUT + j0, L.ld4, L.vp, hd[ib][r + 8]);
+        }
+      }
+    SPP_TP(17);  // heads backward
+    // ---- dh2 = Wh^T dheads * relu'(h2); dh1 = W2^T dh2 * relu'(h1)
+    dense<C::NB_PAIR, C::RV_PAIR, C::BF>(p.actor.WhT, 8, hd, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ur = 32 * ob + ru(q);
+        const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
+        L.bl[ur * 32] = v;
+        fm_st(rsrc(p.AD2), ur, L.ld4, L.vo, v);
+      }
+    });
+    dense_lds<8, C::BF>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
+    });
+    SPP_TP(18);  // trunk backward
+    const float pd = wave_sum(dist_part);
+    if (lane == 0) p.part[tile * kParts + 3] = pd;
+  }
+  SPP_TP_FLUSH();
+}
+
 // ============================================================================ rollout action
 struct ActArgs {
   int E, mode, denorm_out;
@@ -883,7 +988,7 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
         const int j0 = 16 * ib + r;
         const int j = j0 + h8;
         if (j < C::AOUT) {
-          const float lim = actor_lim<(C::NB_PAIR <= 2)>(p, L.tbl, j);
+          const float lim = actor_lim<true>(p, L.tbl, j);
           float act;
           if (a.plain && (a.mode == 0 || a.mode == 3)) {
             act = valid ? a.eps[er * C::AOUT + j] : 0.f;  // action_space.sample() drawn by the caller (ddpg.py:178-180)
@@ -912,7 +1017,7 @@ __global__ __launch_bounds__(256, 1) void k_policy_act(SacArgs p, ActArgs a) {
             if (a.mode == 1 && a.noise) act += fmul_rn(a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f), lim);
             act = fminf(fmaxf(act, -1.1f * lim), 1.1f * lim);  // ddpg_acm.py:43-45
           }
-          if (a.denorm_out && !a.plain) act = denorm<(C::NB_PAIR <= 2)>(p, L.tbl, j, act);
+          if (a.denorm_out && !a.plain) act = denorm<true>(p, L.tbl, j, act);
           L.pl[j0 * 32] = act;
           if (valid) a.target_out[er * C::AOUT + j] = act;
           if (valid && a.plain) a.env_out[er * C::AOUT + j] = act;  // process_action: identity (ddpg.py:371-384)
@@ -1001,7 +1106,7 @@ __global__ __launch_bounds__(256, 1) void k_acm_regress(SacArgs p, AcmRegArgs g)
     for (int q = 0; q < 16; ++q) {
       const int u = ru(q) + L.h4;
       const int uu = u < C::AC ? u : 0;
-      limv[q] = acm_lim<(C::NB_PAIR <= 2)>(p, L.tbl, uu);
+      limv[q] = acm_lim<true>(p, L.tbl, uu);
       yv[q] = g.y[br * C::AC + uu];
     }
     dense<1, C::RV_Z2, C::BF>(p.acm.W3, 1, z2, tbl + p.acm.tb3, [&](int ob, const f32x16& acc) {

@@ -96,10 +96,16 @@ def check_sac(ag, o, ol, grad_tol, loss_tol, params_check=True, params0=None):
     ("Hopper-v2", 11, 3, 409600, False),
     ("Ant-v2", 111, 8, 65536, True),
     ("Ant-v2", 111, 8, 409600, True),
+    ("Ant-v2", 111, 8, 4096, False),    # fp32 Ant (bench config sac_ant): the widest phase kernels
+    ("Ant-v2", 111, 8, 65536, False),
+    ("Ant-v2", 111, 8, 4096, "acmc0"),  # fp32 Ant, critics on [s | a_d] (acm_critic=False)
+    ("Ant-v2", 111, 8, 4096, "bf16_acmc0"),
 ])
 def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
     rng = np.random.RandomState(B % 1000 + ob)
-    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=True, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
+    acmc = bf16 not in ("acmc0", "bf16_acmc0")
+    bf16 = bf16 in (True, "bf16_acmc0")
+    ag = spprl.SAC_AcM(env_name=env_name, acm_critic=acmc, custom_loss=0.2, norm_closs=False, min_max_denormalize=True,
                        denormalize_actor_out=True, gamma=0.99, max_batch=B, buffer_size=128, device=DEV, seed=3,
                        mlp_bf16=bf16)
     params = snapshot(ag, SAC_NETS)
@@ -108,7 +114,7 @@ def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
     e1, e2 = rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32)
     ag.update(*batch, eps_next=e1, eps_cur=e2)
     torch.cuda.synchronize()
-    o = OracleSacAcm(ob, ob, ac, acm_critic=True, custom_loss=0.2, norm_closs=False, norm=norm, actor_lim=1.0,
+    o = OracleSacAcm(ob, ob, ac, acm_critic=acmc, custom_loss=0.2, norm_closs=False, norm=norm, actor_lim=1.0,
                      acm_lim=np.ones(ac, np.float32), gamma=0.99, params=params, dtype=F64)
     ol = o.update(*batch, e1, e2)
     if bf16:

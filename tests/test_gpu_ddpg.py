@@ -107,3 +107,38 @@ def test_basic_acm_regression_matches_torch():
     got = ag.grads[_lib.SPP_NET_ACM].cpu().numpy()
     assert relerr(got, gflat) < 2e-4, relerr(got, gflat)
     np.testing.assert_allclose(got[:1 + ac], gflat[:1 + ac], rtol=1e-3, atol=1e-6)  # t, t1
+
+
+@pytest.mark.parametrize("B", [96, 4000])
+def test_ddpg_acm_ant_dims_match_oracle(B):
+    """SPP-DDPG Ant (train/spp_ddpg_ant.py: ob 111, ac 8, BasicAcM(222, 8)) kernel set: two updates
+    and the policy act against the oracle from the agent's own initial parameters (no reference fixture
+    exists at these dims: parity pinned through the oracle, which the HalfCheetah fixture pins)."""
+    ob, ac = 111, 8
+    ag = spprl.DDPG_AcM(env_name="Ant-v2", gamma=0.99, actor_lr=5e-4, critic_lr=5e-4, acm_critic=True,
+                        custom_loss=1.0, norm_closs=False, min_max_denormalize=True, denormalize_actor_out=True,
+                        max_batch=B, buffer_size=64, device=DEV, seed=11)
+    params = {k: {n: v.numpy() for n, v in ag.net_state(net).items()} for k, net in NAMES.items()}
+    rng = np.random.RandomState(B)
+    lo = -rng.uniform(0.5, 2, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2, ob).astype(np.float32)
+    rb = ag.replay_buffer
+    rb.min_obs.copy_(torch.from_numpy(lo))
+    rb.max_obs.copy_(torch.from_numpy(hi))
+    rb._have_minmax = True
+    norm = onets.Norm(True, torch.from_numpy(lo), torch.from_numpy(hi))
+    o = OracleDdpgAcm(ob, ob, ac, norm=norm, actor_lim=np.ones(ob, np.float32), gamma=0.99, tau=0.005,
+                      params=params, dtype=torch.float64)  # float64: the oracle's own summation error negligible
+    for _ in range(2):
+        batch = (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
+                 rng.uniform(-1, 1, (B, ob)).astype(np.float32), rng.randn(B).astype(np.float32),
+                 (rng.rand(B) < 0.1).astype(np.int8), rng.uniform(-1, 1, (B, ac)).astype(np.float32))
+        ag.update(*batch)
+        ol = o.update(*batch)
+        torch.cuda.synchronize()
+        for k, net in (("critic", _lib.SPP_NET_CRITIC1), ("actor", _lib.SPP_NET_ACTOR)):
+            e = relerr(ag.grads[net].cpu().numpy(), o.last["grads"][k])
+            assert e < 2e-4, (k, e)
+        gl = ag.loss
+        for k in ("critic", "actor", "ddpg", "dist"):
+            assert gl[k] == pytest.approx(ol[k], rel=1e-4, abs=1e-6), k

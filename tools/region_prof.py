@@ -25,17 +25,20 @@ NAMES = {0: "tile start", 1: "actor L1", 2: "actor L2", 3: "actor heads", 4: "sq
 
 
 def main():
+    """argv[1]: hopper (default) | ant_bf16 (build with --prof --bf16-only)"""
     dev = torch.device("cuda", 0)
     E, B = 4096, 409600
-    ag = spprl.SAC_AcM(env_name="Hopper-v2", acm_critic=True, custom_loss=0.2, norm_closs=False,
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "hopper"
+    env, ob, ac, bf = {"hopper": ("Hopper-v2", 11, 3, False), "ant_bf16": ("Ant-v2", 111, 8, True)}[cfg]
+    ag = spprl.SAC_AcM(env_name=env, acm_critic=True, custom_loss=0.2, norm_closs=False,
                        min_max_denormalize=True, denormalize_actor_out=True, max_batch=B, buffer_size=200_000,
-                       device=dev, seed=0)
+                       device=dev, seed=0, mlp_bf16=bf)
     rb = ag.replay_buffer
     n = 150_000
-    slots = rb.add_obs_batch(torch.randn(n + 1, 11, device=dev))
-    rb.add_timestep_batch(slots[:n], slots[1:], torch.randn(n, 11, device=dev), torch.randn(n, device=dev),
+    slots = rb.add_obs_batch(torch.randn(n + 1, ob, device=dev))
+    rb.add_timestep_batch(slots[:n], slots[1:], torch.randn(n, ob, device=dev), torch.randn(n, device=dev),
                           torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
-                          torch.rand(n, 3, device=dev) * 2 - 1)
+                          torch.rand(n, ac, device=dev) * 2 - 1)
     rb.update_obs_mean_std()
     idx = torch.randint(0, n, (B,), device=dev)
     buf = (ctypes.c_ulonglong * 64)()
@@ -48,7 +51,7 @@ def main():
     t = np.array(buf[:32], np.float64)
     tiles = 3 * (B // 32)
     tot = t.sum()
-    print("both phases, cycles per tile (%d tiles per phase): total %.0f" % (tiles, tot / tiles))
+    print("%s: both phases, cycles per tile (%d tiles per phase): total %.0f" % (cfg, tiles, tot / tiles))
     for k in [k for k in NAMES if t[k] > 0]:
         print("  %2d %-20s %9.0f  %5.1f%%" % (k, NAMES[k], t[k] / tiles, 100 * t[k] / tot))
 

@@ -137,6 +137,30 @@ __device__ __forceinline__ float softplus_t(float x) {  // torch softplus(beta=1
   return x > 20.f ? x : log1pf(expf(x));
 }
 
+// Transcendentals of the squash / log-prob epilogues.  F (the bf16 kernel sets, BASELINE configs[4]:
+// bf16 MLP): the hardware forms (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp), far inside the bf16
+// tolerance; these epilogues are VALU-latency bound on the 111-wide Ant heads.  fp32 sets: libm.
+template <bool F>
+__device__ __forceinline__ float t_exp(float x) {
+  if constexpr (F) return __expf(x);
+  else return expf(x);
+}
+template <bool F>
+__device__ __forceinline__ float t_rcp(float x) {
+  if constexpr (F) return __builtin_amdgcn_rcpf(x);
+  else return 1.f / x;
+}
+template <bool F>
+__device__ __forceinline__ float t_tanh(float x) {
+  if constexpr (F) return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * x) + 1.f);
+  else return tanhf(x);
+}
+template <bool F>
+__device__ __forceinline__ float t_softplus(float x) {
+  if constexpr (F) return x > 20.f ? x : __logf(1.f + __expf(x));
+  else return softplus_t(x);
+}
+
 // Pairing-layout tile of the actor heads from the LDS image rows [0, 2*AOUT)
 // pairing layout: block ib, register r<8 (mu) / r+8 (logsig), half h -> j = 16*ib + 8*h + r
 template <class C>
@@ -385,18 +409,24 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
       const bool ok = j < C::AOUT;
       if (kBranchFree || ok) {
         const int jj = ok ? j : 0;
+        constexpr bool F = C::BF;
         const float mu = hd[ib][r];
         const float ls = fminf(fmaxf(hd[ib][r + 8], -20.f), 2.f);
-        const float sc = expf(ls);
+        const float sc = t_exp<F>(ls);
         const float e = ev[ib][r];
         const float u = fadd_rn(mu, fmul_rn(e, sc));
-        const float d = fsub_rn(u, mu);
-        const float var = fmul_rn(sc, sc);
-        const float lpj = fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(d, d), 2.f * var), logf(sc)), kLogSqrt2Pi);
-        const float cj = 2.f * fsub_rn(fsub_rn(kLog2, u), softplus_t(-2.f * u));
+        float lpj;
+        if constexpr (F) {  // Normal(mu, sc).log_prob(u) with u - mu = e sc, log sc = ls
+          lpj = -0.5f * e * e - ls - kLogSqrt2Pi;
+        } else {  // the reference's operation order
+          const float d = fsub_rn(u, mu);
+          const float var = fmul_rn(sc, sc);
+          lpj = fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(d, d), 2.f * var), logf(sc)), kLogSqrt2Pi);
+        }
+        const float cj = 2.f * fsub_rn(fsub_rn(kLog2, u), t_softplus<F>(-2.f * u));
         lp += ok ? lpj : 0.f;
         corr += ok ? cj : 0.f;
-        const float a = fmul_rn(tanhf(u), actor_lim<true>(p, L.tbl, jj));
+        const float a = fmul_rn(t_tanh<F>(u), actor_lim<true>(p, L.tbl, jj));
         const float ad = denorm<true>(p, L.tbl, jj, a);
         if (ok) L.pl[j0 * 32] = ad;
       }
@@ -879,12 +909,13 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_heads(SacArgs p, AcmScratc
         const int j = j0 + h8;
         const bool ok = j < C::AOUT;
         const int jj = ok ? j : 0;
+        constexpr bool F = C::BF;
         const float e = ev[r];
         const float ls = fminf(fmaxf(lsr[r], -20.f), 2.f);
-        const float sc = expf(ls);
+        const float sc = t_exp<F>(ls);
         const float u = fadd_rn(mu[r], fmul_rn(e, sc));
         const float d = fsub_rn(u, mu[r]);
-        const float t = tanhf(u);
+        const float t = t_tanh<F>(u);
         const float lim = actor_lim<true>(p, L.tbl, jj);
         const float a = fmul_rn(t, lim);
         float g_ad = gv[r];  // from the critics through the ACM
@@ -902,10 +933,11 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_heads(SacArgs p, AcmScratc
         }
         g_a += g_ad * denorm_scale<true>(p, L.tbl, jj);
         const float var = fmul_rn(sc, sc);
-        const float sig_m2u = 1.f / (1.f + expf(2.f * u));  // sigmoid(-2u)
-        const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d / var + 2.f - 4.f * sig_m2u);
-        const float gmu = gu + g_lp * d / var;
-        const float gsc = gu * e + g_lp * (d * d / (var * sc) - 1.f / sc);
+        const float ivar = t_rcp<F>(var), isc = t_rcp<F>(sc);
+        const float sig_m2u = t_rcp<F>(1.f + t_exp<F>(2.f * u));  // sigmoid(-2u)
+        const float gu = g_a * lim * (1.f - t * t) + g_lp * (-d * ivar + 2.f - 4.f * sig_m2u);
+        const float gmu = gu + g_lp * d * ivar;
+        const float gsc = gu * e + g_lp * (d * d * ivar * isc - isc);
         const float gls = (lsr[r] >= -20.f && lsr[r] <= 2.f) ? gsc * sc : 0.f;
         if (ok) {  // slot j >= AOUT would land on row AOUT + j' of a valid slot's log-std
           L.pl[j0 * 32] = gmu;

@@ -47,7 +47,9 @@ def _stale(src):
     obj = _obj(src)
     if not os.path.exists(obj):
         return True
-    if os.path.basename(src).startswith("ks_"):
+    if os.path.basename(src) == "ks_dw.hip":
+        deps = [src] + [os.path.join(CSRC, d) for d in ("dw.hip", "internal.h", "common.h", "mlp.h")]
+    elif os.path.basename(src).startswith("ks_"):
         deps = [src] + [os.path.join(CSRC, d) for d in KSET_DEPS]
     else:
         deps = [f for f in glob.glob(os.path.join(CSRC, "*")) if not os.path.basename(f).startswith("ks_")]

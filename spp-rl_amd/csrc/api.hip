@@ -14,7 +14,6 @@
 #include "replay.h"
 #include "sac_kernels.h"
 
-#include "dw.hip"
 #include "optim.hip"
 #include "ppo.hip"
 #include "replay.hip"
@@ -23,6 +22,7 @@
 #include "ddpg.hip"
 #include "kset.h"
 #ifdef SPP_SINGLE_TU  // profiling / development builds: everything in one TU
+#include "ks_dw.hip"
 #include "ks_sac_hopper.hip"
 #if defined(SPP_ONLY_BF16)  // region-profiling builds of the bf16 sets: Hopper fp32 + bf16 only
 #define SPP_ONLY_HOPPER
@@ -668,6 +668,7 @@ struct DwSet {
   int B = -1;
   int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
   int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
+  bool bf16 = false;              // bf16 MFMA job set (k_dw<true>)
   void release() { slab.release(); jobs.release(); items.release(); }
 };
 
@@ -1031,6 +1032,9 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
   SPP_CHECK_HIP(hipMemcpy(D.jobs.ptr, jobs.data(), sizeof(DwJob) * jobs.size(), hipMemcpyHostToDevice));
   SPP_CHECK_HIP(hipMemcpy(D.items.ptr, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
   D.B = B;
+  D.bf16 = !jobs.empty() && jobs[0].bf16;
+  for (const DwJob& j : jobs)
+    if ((j.bf16 != 0) != D.bf16) return SPP_E_STATE;
   return SPP_OK;
 }
 
@@ -1041,6 +1045,12 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
   const int ca = a->cfg.acm_critic ? ac : aout, cin = ob + ca;
   std::vector<DwJob> jobs;
+  // bf16 SAC kernel sets write these operand arrays as bf16 (op_st, sac.hip)
+  std::vector<const float*> b16;
+  if (a->cfg.mlp_bf16 && !a->ddpg && set == 0)
+    b16 = {a->H1[0], a->H1[1], a->H2[0], a->H2[1], a->D1[0], a->D1[1], a->D2[0], a->D2[1],
+           a->AH1, a->AH2, a->AD1, a->AD2};
+  auto is16 = [&](const float* p) { return p && std::find(b16.begin(), b16.end(), p) != b16.end(); };
   // rows >= nrow2 of a job go to (dW2, db2)
   auto J = [&](const float* A, int N, const float* X0, int K0, const float* X1, int K1, float* dW, float* db,
                int nrow2 = -1, float* dW2 = nullptr, float* db2 = nullptr) {
@@ -1050,7 +1060,9 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     j.dW2 = dW2; j.db2 = db2;
     j.slab_stride = round_up((int64_t)N * (K0 + K1) + N, 4);
     j.bf16 = a->cfg.mlp_bf16 ? 1 : 0;
-    jobs.push_back(j);
+    j.a_bf = is16(A) ? 1 : 0;
+    j.x_bf = is16(X0) ? 1 : 0;
+    jobs.push_back(j);  // (an X1 segment is always staged fp32 input, like X0)
   };
   DwSet& D = a->dws[set];
   int nph = 0;
@@ -1128,8 +1140,7 @@ static void launch_dw_set(DwSet& D, int ph, hipStream_t st) {
   const int* ij = D.items.ptr + D.ioff[ph];
   const int* is = ij + D.nitems[ph];
   const DwJob* jobs = D.jobs.ptr + D.j0[ph];
-  hipLaunchKernelGGL(k_dw, dim3(D.nitems[ph]), dim3(kDwThreads), 0, st, jobs, ij, is);
-  hipLaunchKernelGGL(k_dw_reduce, dim3(cdiv(D.max_elems[ph], 256), D.nj[ph]), dim3(256), 0, st, jobs);
+  launch_dw_kernels(jobs, ij, is, D.nitems[ph], D.nj[ph], D.max_elems[ph], D.bf16, st);
 }
 static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) { launch_dw_set(a->dws[set], ph, st); }
 

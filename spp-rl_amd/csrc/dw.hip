@@ -13,6 +13,12 @@
 // through an R-deep register ring (loads for step t+R-1 issued before step
 // t's MFMAs; R from dw_ring, deeper for thin tile sets).  Partial slabs are
 // summed in a fixed order by k_dw_reduce (deterministic, no atomics).
+//
+// Operand element types are per job (DwJob::a_bf / x_bf): the bf16 kernel sets store the
+// activations and deltas they hand to this kernel as bf16 [rows][Bp] (half the bytes written
+// and read back; the bf16 MFMA rounds fp32 operands to bf16 with the same conversion), while
+// staged inputs (s, a), the per-sample dq and the head deltas stay fp32.  A bf16 operand
+// row-step is one 16-B load of the lane half's 8 samples, fed to the MFMA as is.
 #include "common.h"
 #include "internal.h"
 
@@ -20,14 +26,16 @@ namespace spp {
 
 constexpr int kDwThreads = 256;
 
-// Steps (16 samples each) in flight for an NI x NJ tile set: the R-1 steps ahead carry
-// NI*NJ*8 MFMAs (64 cycles) each, enough to cover >= ~8K cycles of HBM latency, within
-// ~200 VGPRs of operand ring.  4x4: 2 (one 8K-cycle step ahead); thin tiles go deeper.
-template <int NI, int NJ>
+// Steps (16 samples each) in flight for an NI x NJ tile set: the R-1 steps ahead should carry
+// >= ~8K cycles of MFMA work (HBM latency under load), within ~168 VGPRs of operand ring.
+// fp32: 8 x 64-cycle 32x32x2 MFMAs per block pair and step (4x4: R = 2); bf16: one 32-cycle
+// 32x32x16 per block pair and step, so the ring runs as deep as the registers allow (bf16
+// operand rows take one float4 per step, fp32 rows two).
+template <int NI, int NJ, bool BF = false, bool ABF = false, bool XBF = false>
 constexpr int dw_ring() {
-  constexpr int mf = NI * NJ * 8;
-  constexpr int want = 1 + (128 + mf - 1) / mf;
-  constexpr int cap = 200 / ((NI + NJ) * 8);
+  constexpr int cyc = NI * NJ * (BF ? 32 : 512);
+  constexpr int want = 1 + (8192 + cyc - 1) / cyc;
+  constexpr int cap = 168 / (4 * (NI * (ABF ? 1 : 2) + NJ * (XBF ? 1 : 2)));
   constexpr int r = want < cap ? want : cap;
   return r < 2 ? 2 : (r > 8 ? 8 : r);
 }
@@ -44,10 +52,23 @@ __device__ __forceinline__ bf16x8 pack8(const float4& a, const float4& b) {
 
 // BF: one v_mfma_f32_32x32x16_bf16 per (row block, column block) per 16-sample step: lane half
 // h's 8 samples are exactly the MFMA's k = 8h + j slots on both operands (bf16 agents, mlp_bf16).
-template <int NI, int NJ, bool DB, bool BF = false>
+__device__ __forceinline__ bf16x8 as_bf8(const float4& a) { return __builtin_bit_cast(bf16x8, a); }
+// sum of the 8 bf16 of a 16-B operand word (the bias gradient of a bf16 delta row)
+__device__ __forceinline__ float sum_bf8(const float4& a) {
+  const uint32_t w[4] = {__builtin_bit_cast(uint32_t, a.x), __builtin_bit_cast(uint32_t, a.y),
+                         __builtin_bit_cast(uint32_t, a.z), __builtin_bit_cast(uint32_t, a.w)};
+  float s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    s[i] = __builtin_bit_cast(float, w[i] << 16) + __builtin_bit_cast(float, w[i] & 0xffff0000u);
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+// ABF / XBF: the A / X operand rows are bf16 (BF only); row pointers are then __bf16* cast to float*.
+template <int NI, int NJ, bool DB, bool BF = false, bool ABF = false, bool XBF = false>
 __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
                                         f32x16 (&acc)[4][4], float (&bs)[4]) {
-  constexpr int R = dw_ring<NI, NJ>();
+  constexpr int R = dw_ring<NI, NJ, BF, ABF, XBF>();
   float4 ra[R][NI][2], rx[R][NJ][2];
   const float* a0[NI];
   const float* x0[NJ];
@@ -56,12 +77,20 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
   auto load = [&](auto SL, int t) {
     constexpr int sl = decltype(SL)::value;
     static_for<0, NI>([&](auto I) {
-      ra[sl][I][0] = *reinterpret_cast<const float4*>(a0[I] + 16 * t);
-      ra[sl][I][1] = *reinterpret_cast<const float4*>(a0[I] + 16 * t + 4);
+      if constexpr (ABF) {
+        ra[sl][I][0] = *reinterpret_cast<const float4*>(reinterpret_cast<const __bf16*>(a0[I]) + 16 * t);
+      } else {
+        ra[sl][I][0] = *reinterpret_cast<const float4*>(a0[I] + 16 * t);
+        ra[sl][I][1] = *reinterpret_cast<const float4*>(a0[I] + 16 * t + 4);
+      }
     });
     static_for<0, NJ>([&](auto J) {
-      rx[sl][J][0] = *reinterpret_cast<const float4*>(x0[J] + 16 * t);
-      rx[sl][J][1] = *reinterpret_cast<const float4*>(x0[J] + 16 * t + 4);
+      if constexpr (XBF) {
+        rx[sl][J][0] = *reinterpret_cast<const float4*>(reinterpret_cast<const __bf16*>(x0[J]) + 16 * t);
+      } else {
+        rx[sl][J][0] = *reinterpret_cast<const float4*>(x0[J] + 16 * t);
+        rx[sl][J][1] = *reinterpret_cast<const float4*>(x0[J] + 16 * t + 4);
+      }
     });
   };
   static_for<0, R - 1>([&](auto S) {
@@ -78,12 +107,17 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (BF) {
         static_for<0, NI>([&](auto I) {
-          if constexpr (DB) {
+          if constexpr (DB && ABF) {
+            bs[I] += sum_bf8(ra[u][I][0]);
+          } else if constexpr (DB) {
             const float4 a0 = ra[u][I][0], a1 = ra[u][I][1];
             bs[I] += ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
           }
-          const bf16x8 av = pack8(ra[u][I][0], ra[u][I][1]);
-          static_for<0, NJ>([&](auto J) { acc[I][J] = mfma16(av, pack8(rx[u][J][0], rx[u][J][1]), acc[I][J]); });
+          const bf16x8 av = ABF ? as_bf8(ra[u][I][0]) : pack8(ra[u][I][0], ra[u][I][1]);
+          static_for<0, NJ>([&](auto J) {
+            const bf16x8 xv = XBF ? as_bf8(rx[u][J][0]) : pack8(rx[u][J][0], rx[u][J][1]);
+            acc[I][J] = mfma16(av, xv, acc[I][J]);
+          });
         });
       } else {
         static_for<0, NI>([&](auto I) {
@@ -104,6 +138,9 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
   }
 }
 
+// BFK: the bf16 job sets (every job of a launch has the agent's bf16 flag); one kernel per
+// precision so each gets its own register allocation.
+template <bool BFK>
 __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ jobs, const int* __restrict__ item_job,
                                                       const int* __restrict__ item_split) {
   const int item = blockIdx.x;
@@ -145,14 +182,18 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   // clamped to row 0 (their outputs are never stored)
   const float* ap[4];
   const float* xp[4];
+  const int esa = J.a_bf ? 2 : 4, esx = J.x_bf ? 2 : 4;  // operand element sizes
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int n = 32 * (nb0 + i) + c;
     n = n < N ? n : 0;
-    ap[i] = J.A + (int64_t)n * ld + b_begin + 8 * h;
+    ap[i] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(J.A) +
+                                           esa * ((int64_t)n * ld + b_begin + 8 * h));
     int k = 32 * (kb0 + i) + c;
     k = k < K ? k : 0;
-    xp[i] = (k < J.K0 ? J.X0 + (int64_t)k * ld : J.X1 + (int64_t)(k - J.K0) * ld) + b_begin + 8 * h;
+    const float* xr = k < J.K0 ? J.X0 : J.X1;
+    const int64_t kr = k < J.K0 ? k : k - J.K0;
+    xp[i] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(xr) + esx * (kr * ld + b_begin + 8 * h));
   }
   f32x16 acc[4][4];
 #pragma unroll
@@ -160,23 +201,42 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  // operand types: 0 fp32 MFMA; bf16 MFMA with (A, X) element types fp32/fp32, bf16/fp32,
+  // bf16/bf16, fp32/bf16.  The bf16 forms instantiate 1, 2 and 4 blocks per side only (a 3-block
+  // side runs as 4 with its last row block clamped to row 0 and never stored): 4 x 9 shapes.
+  const int mode = BFK ? 1 + J.a_bf + 2 * J.x_bf : 0;
+#define SPP_DW_T(I, J_, ...)                                                    \
+  if (db) dw_tile<I, J_, true, ##__VA_ARGS__>(ap, xp, nsteps, acc, bs);         \
+  else dw_tile<I, J_, false, ##__VA_ARGS__>(ap, xp, nsteps, acc, bs);
 #define SPP_DW_CASE(I, J_)                                                      \
+  case (I) * 8 + (J_): SPP_DW_T(I, J_) break;
+#define SPP_DW_CASE16(I, J_)                                                    \
   case (I) * 8 + (J_):                                                          \
-    if (J.bf16) {                                                               \
-      if (db) dw_tile<I, J_, true, true>(ap, xp, nsteps, acc, bs);              \
-      else dw_tile<I, J_, false, true>(ap, xp, nsteps, acc, bs);                \
-    } else {                                                                    \
-      if (db) dw_tile<I, J_, true>(ap, xp, nsteps, acc, bs);                    \
-      else dw_tile<I, J_, false>(ap, xp, nsteps, acc, bs);                      \
+    switch (mode) {                                                             \
+      case 1: SPP_DW_T(I, J_, true) break;                                      \
+      case 2: SPP_DW_T(I, J_, true, true) break;                                \
+      case 4: SPP_DW_T(I, J_, true, true, true) break;                          \
+      default: SPP_DW_T(I, J_, true, false, true) break;                        \
     }                                                                           \
     break;
-  switch (ni * 8 + nj) {
-    SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)
-    SPP_DW_CASE(2, 1) SPP_DW_CASE(2, 2) SPP_DW_CASE(2, 3) SPP_DW_CASE(2, 4)
-    SPP_DW_CASE(3, 1) SPP_DW_CASE(3, 2) SPP_DW_CASE(3, 3) SPP_DW_CASE(3, 4)
-    SPP_DW_CASE(4, 1) SPP_DW_CASE(4, 2) SPP_DW_CASE(4, 3) SPP_DW_CASE(4, 4)
+  if constexpr (!BFK) {
+    switch (ni * 8 + nj) {
+      SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)
+      SPP_DW_CASE(2, 1) SPP_DW_CASE(2, 2) SPP_DW_CASE(2, 3) SPP_DW_CASE(2, 4)
+      SPP_DW_CASE(3, 1) SPP_DW_CASE(3, 2) SPP_DW_CASE(3, 3) SPP_DW_CASE(3, 4)
+      SPP_DW_CASE(4, 1) SPP_DW_CASE(4, 2) SPP_DW_CASE(4, 3) SPP_DW_CASE(4, 4)
+    }
+  } else {
+    const int ni4 = ni == 3 ? 4 : ni, nj4 = nj == 3 ? 4 : nj;
+    switch (ni4 * 8 + nj4) {
+      SPP_DW_CASE16(1, 1) SPP_DW_CASE16(1, 2) SPP_DW_CASE16(1, 4)
+      SPP_DW_CASE16(2, 1) SPP_DW_CASE16(2, 2) SPP_DW_CASE16(2, 4)
+      SPP_DW_CASE16(4, 1) SPP_DW_CASE16(4, 2) SPP_DW_CASE16(4, 4)
+    }
   }
 #undef SPP_DW_CASE
+#undef SPP_DW_CASE16
+#undef SPP_DW_T
   // partial (or final) result; rows >= nrow2 go to the second output (dW2/db2)
   const bool direct = J.nsplit * J.wsplit == 1;
   float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + part) * J.slab_stride;

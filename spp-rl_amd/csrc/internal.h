@@ -20,7 +20,14 @@ struct DwJob {
   int split_len, nsplit, nrow2;
   int wsplit;       // 4: output <= 128x128, the 4 waves of an item split its samples (one slab each); else 1
   int bf16;         // 1: bf16 MFMA (operands rounded to bf16 in registers, fp32 accumulation)
+  int a_bf, x_bf;   // (bf16 only) A / X rows hold bf16 elements ([rows][Bp] __bf16), else fp32
 };
+
+// dw.hip (own translation unit, ks_dw.hip): the split-K weight-gradient launch + fixed-order reduce
+// over nitems work items of jobs[0, njobs); item_job / item_split index the job table; bf16: the
+// set's jobs are bf16 MFMA jobs (DwJob::bf16).
+void launch_dw_kernels(const DwJob* jobs, const int* item_job, const int* item_split, int nitems, int njobs,
+                       int64_t max_elems, bool bf16, hipStream_t st);
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)
 //   L[n][k] = trans ? S[k][coff + n] : S[n][coff + k]; source rows >= split come from W2

@@ -259,7 +259,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
         const int ur = 32 * ob + ru(q);
         const float v = fmaxf(acc[q], 0.f);
         L.bl[ur * 32] = v;
-        if constexpr (ST) fm_st(hr, ur, L.ld4, L.vo, v);
+        if constexpr (ST) op_st<C::BF>(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
       setbits(m1lo, m1hi, ob, bits);
@@ -275,7 +275,7 @@ __device__ __forceinline__ void actor_trunk(const ActorDev& A, const float* X, i
         const int ur = 32 * ob + ru(q);
         const float v = fmaxf(acc[q], 0.f);
         L.bl[ur * 32] = v;
-        if constexpr (ST) fm_st(hr, ur, L.ld4, L.vo, v);
+        if constexpr (ST) op_st<C::BF>(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
       setbits(m2lo, m2hi, ob, bits);
@@ -355,7 +355,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
       const int ur = 32 * ob + ru(q);
       const float v = fmaxf(acc[q], 0.f);
       L.bl[ur * 32] = v;
-      if constexpr (ST) fm_st(h1r, ur, L.ld4, L.vo, v);
+      if constexpr (ST) op_st<C::BF>(h1r, ur, L.ld4, L.vo, v);
       bits |= (uint32_t)(v > 0.f) << q;
     }
     setbits(m1lo, m1hi, ob, bits);
@@ -370,7 +370,7 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = fmaxf(acc[q], 0.f);
-      if constexpr (ST) fm_st(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
+      if constexpr (ST) op_st<C::BF>(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
       qp = fmaf(v, tv[q], qp);
       bits |= (uint32_t)(v > 0.f) << q;
     }
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
           const int ur = 32 * ob + ru(q2);
           const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tv[q2] : 0.f;
           L.bl[ur * 32] = v;
-          fm_st(d2r, ur, L.ld4, L.vo, v);
+          op_st<C::BF>(d2r, ur, L.ld4, L.vo, v);
         }
       }
       SPP_TP(13);
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       dense_lds<8, C::BF>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2)
-          fm_st(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
+          op_st<C::BF>(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
       });
     }
     SPP_TP(14);
@@ -833,14 +833,14 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         const int ur = 32 * ob + ru(q);
         const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
         L.bl[ur * 32] = v;
-        fm_st(rsrc(p.AD2), ur, L.ld4, L.vo, v);
+        op_st<C::BF>(rsrc(p.AD2), ur, L.ld4, L.vo, v);
       }
     });
     {
       dense_lds<8, C::BF>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
+          op_st<C::BF>(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
       });
     }
     SPP_TP(18);  // trunk backward
@@ -966,13 +966,13 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_heads(SacArgs p, AcmScratc
         const int ur = 32 * ob + ru(q);
         const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
         L.bl[ur * 32] = v;
-        fm_st(rsrc(p.AD2), ur, L.ld4, L.vo, v);
+        op_st<C::BF>(rsrc(p.AD2), ur, L.ld4, L.vo, v);
       }
     });
     dense_lds<8, C::BF>(p.actor.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        fm_st(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
+        op_st<C::BF>(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
     });
     SPP_TP(18);  // trunk backward
     const float pd = wave_sum(dist_part);

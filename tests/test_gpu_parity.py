@@ -402,6 +402,54 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     assert steps[3] == K
 
 
+@pytest.mark.parametrize("bs", [100, 160])
+def test_update_acm_epochs_with_step_lr_match_oracle(bs, monkeypatch):
+    """AcMTrainer.update_acm (acm.py:266-303, the pre-train epoch mode): shuffled epochs over every
+    live row in batches of acm_batch_size with a ragged last batch, StepLR(step 1, gamma 0.5) stepped
+    once per epoch, loss['acm'] = the last epoch's mean batch loss.  The oracle replays the same
+    permutations (recorded from the loop's torch.randperm) through AcMTrainer.batch_update with
+    the scheduled lr.  bs = 100 runs the persistent sppAcmSgd launches, bs = 160 the per-batch
+    regress kernels.  Tolerance as for the persistent SGD test, over all 3 x 21 (13) Adam steps."""
+    import spprl.trainer as tr
+
+    n = 2050
+    ag = _filled_agent("Hopper-v2", 11, 3, n, seed=6)
+    ag.acm_batch_size, ag.acm_scheduler_step, ag.acm_scheduler_gamma = bs, 1, 0.5
+    perms = []
+    real = torch.randperm
+
+    def rec(*a, **k):
+        p = real(*a, **k)
+        perms.append(p.clone())
+        return p
+
+    monkeypatch.setattr(tr.torch, "randperm", rec)
+    rb = ag.replay_buffer
+    params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}
+    o = OracleAcmTrainer(22, 3, lr=ag.acm_lr, ac_lim=ag.ac_lim.numpy(), params=params)
+    obs, nobs, _, _, _, acm = (t.cpu().numpy() for t in rb.gather(torch.arange(n, device=DEV)))
+    x_all = np.concatenate([obs, nobs], 1)
+    epochs = 3
+    ag.update_acm(epochs, pretrain=True)
+    torch.cuda.synchronize()
+    assert len(perms) == epochs
+    steps = 0
+    for e, p in enumerate(perms):
+        o.opt.lr = ag.acm_lr * 0.5 ** e
+        p = p.numpy()
+        losses = [o.batch_update(x_all[p[s:s + bs]], acm[p[s:s + bs]]) for s in range(0, n, bs)]
+        steps += len(losses)
+    assert ag.acm_loss == pytest.approx(np.mean(losses), rel=1e-4)
+    got = ag.params[_lib.SPP_NET_ACM].cpu().numpy()
+    ref = o.flat()
+    d = np.abs(got - ref)
+    assert np.mean(d > 1e-5 * np.maximum(1, np.abs(ref))) < 5e-3 and d.max() < 4 * steps * ag.acm_lr
+    assert ag._acm_sched_epochs == epochs
+    ss = np.zeros(4, np.int64)
+    _lib.call("sppAgentGetSteps", ag._h, ss.ctypes.data_as(__import__("ctypes").c_void_p))
+    assert ss[3] == steps
+
+
 @pytest.mark.parametrize("env_name,ob,ac", [("Hopper-v2", 11, 3), ("Ant-v2", 111, 8)])
 def test_sac_acm_update_bf16_mlp_within_bf16_tolerance(env_name, ob, ac):
     """mlp_bf16 (BASELINE configs[4]: bf16 MFMA MLP + fp32 targets): one SAC_AcM update against the

@@ -4,6 +4,6 @@ set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
 mkdir -p gpurun_out
-timeout -k 10 ${TMO:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v -s --timeout ${PER_TEST:-300} --timeout-method thread \
+timeout -k 10 ${TMO:-900} python -u -m pytest ${TESTS:-tests} ${K:+-k "$K"} -m gpu -x -v -s --timeout ${PER_TEST:-300} --timeout-method thread \
   > gpurun_out/gpu_tests.log 2>&1 || { tail -60 gpurun_out/gpu_tests.log; exit 1; }
 grep -E "PASSED|FAILED|ERROR|grad rel err|passed|failed" gpurun_out/gpu_tests.log | tail -80

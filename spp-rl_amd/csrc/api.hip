@@ -275,8 +275,9 @@ sppStatus sppReplayAddStep(sppReplayHandle h, const int64_t* prev, const int64_t
   }
   SPP_CHECK_HIP(hipMemcpyAsync(h->dev_meta[slot], m, sizeof(int64_t) * 3 * E, hipMemcpyHostToDevice, S(stream)));
   SPP_CHECK_HIP(hipEventRecord(h->ev[slot], S(stream)));
-  hipLaunchKernelGGL(k_replay_add_step, dim3(cdiv(E, 256)), dim3(256), 0, S(stream), h->d, h->dev_meta[slot], E, act,
-                     acm, rew, done, end);
+  const int64_t n_el = (int64_t)E * (h->d.aout + h->d.ac + 1);
+  hipLaunchKernelGGL(k_replay_add_step, dim3(cdiv(n_el, 256)), dim3(256), 0, S(stream), h->d, h->dev_meta[slot], E,
+                     act, acm, rew, done, end);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

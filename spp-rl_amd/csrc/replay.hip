@@ -13,20 +13,30 @@ __global__ void k_replay_add_obs(float* obs, int64_t cap, int ob, const float* s
   obs[((base + e) % cap) * ob + f] = src[i];
 }
 
-// add_acm_action (:332-333) + add_timestep (:65-75) + ReplayBuffer.addition (:133-137)
+// add_acm_action (:332-333) + add_timestep (:65-75) + ReplayBuffer.addition (:133-137).
+// One thread per element: [E][aout] action values, then [E][ac] ACM actions, then the E scalar
+// records, so consecutive lanes write consecutive floats of consecutive timestep rows (the
+// rows of one vector step are consecutive slots except at the Q6 wrap).
 __global__ void k_replay_add_step(ReplayDev r, const int64_t* __restrict__ meta /*[3][E]: prev, next, ts*/, int E,
                                   const float* act, const float* acm, const float* rew, const uint8_t* done,
                                   const uint8_t* end) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const int64_t t = meta[2 * E + e];
-  r.obs_idx[t] = meta[e];
-  r.next_idx[t] = meta[E + e];
-  for (int f = 0; f < r.aout; ++f) r.act[t * r.aout + f] = act ? act[(int64_t)e * r.aout + f] : 0.f;
-  for (int f = 0; f < r.ac; ++f) r.acm[t * r.ac + f] = acm ? acm[(int64_t)e * r.ac + f] : 0.f;
-  r.rew[t] = rew[e];
-  r.done[t] = done[e];
-  r.end[t] = end[e];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t na = (int64_t)E * r.aout, nm = (int64_t)E * r.ac;
+  if (i < na) {
+    const int64_t e = i / r.aout, f = i - e * r.aout;
+    r.act[meta[2 * E + e] * r.aout + f] = act ? act[i] : 0.f;
+  } else if (i < na + nm) {
+    const int64_t j = i - na, e = j / r.ac, f = j - e * r.ac;
+    r.acm[meta[2 * E + e] * r.ac + f] = acm ? acm[j] : 0.f;
+  } else if (i < na + nm + E) {
+    const int e = (int)(i - na - nm);
+    const int64_t t = meta[2 * E + e];
+    r.obs_idx[t] = meta[e];
+    r.next_idx[t] = meta[E + e];
+    r.rew[t] = rew[e];
+    r.done[t] = done[e];
+    r.end[t] = end[e];
+  }
 }
 
 // ---------------------------------------------------------------- gathers

@@ -37,7 +37,7 @@ constexpr int64_t kStBigLen = 4000000;
 constexpr int kStLdsKeys = 6144;     // per-workgroup LDS list space (keys), split over 2 ob lists
 constexpr int kStOvfCap = 1 << 18;   // overflow keys per (column, target)
 constexpr int kStPassThreads = 256;
-constexpr int kStUnroll = 8;         // row groups per lane in flight (halved for ob > 64)
+constexpr int kStUnroll = 8;         // row groups per lane and iteration (halved for ob > 64); 2 iterations in flight
 constexpr int kStNblkMax = 1024;     // pass workgroups (<= select threads)
 constexpr int kStSelThreads = 1024;
 constexpr int kStSelKeys = 32768;    // candidates gathered into the select workgroup's LDS
@@ -329,20 +329,31 @@ __global__ __launch_bounds__(kStPassThreads) __attribute__((amdgpu_waves_per_eu(
       }
     }
   };
-  // the next iteration's obs_idx are requested before this iteration's rows are used
+  // Two-deep pipeline: iteration i+1's rows are requested (their obs_idx arrived one iteration
+  // earlier) and iteration i+2's obs_idx issued before iteration i's keys are classified.
   int nA[U];
-  uint32_t vA;
+  uint32_t vA, vX;
+  float xA[2][U];
   idx_load(wv, nA, vA);
+  x_load(nA, xA);
+  vX = vA;
+  idx_load(wv + it_rows, nA, vA);
   for (int64_t rg0 = wv; rg0 < ngroups; rg0 += it_rows) {
-    float xA[2][U];
-    x_load(nA, xA);
-    const uint32_t v = vA;
-    idx_load(rg0 + it_rows, nA, vA);
+    float xB[2][U];
+    x_load(nA, xB);
+    const uint32_t v = vX;
+    vX = vA;
+    idx_load(rg0 + 2 * it_rows, nA, vA);
 #pragma unroll
     for (int u = 0; u < U; ++u) proc(0, xA[0][u], (v >> u) & 1u);
     if constexpr (WIDE) {
 #pragma unroll
       for (int u = 0; u < U; ++u) proc(1, xA[1][u], ((v >> u) & 1u) && col[1] >= 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xA[0][u] = xB[0][u];
+      if constexpr (WIDE) xA[1][u] = xB[1][u];
     }
   }
   // lane partials -> LDS -> one partial per (workgroup, column)

@@ -187,6 +187,46 @@ def cpu_baseline_report(name, seconds, procs):
     return out
 
 
+def _ppo_cpu_worker(_):
+    """One 1-thread process of the reference's PPO_AcM iteration restated (oracle/cpu_loop_ppo.py), over
+    one ACM update cycle (acm_update_freq = 3 iterations of 2000 frames)."""
+    from oracle.cpu_loop_ppo import PpoCpuLoop
+
+    torch.set_num_threads(1)
+    fps, n, el = PpoCpuLoop().run()
+    return {"value": round(fps, 2), "frames": n, "seconds": round(el, 2)}
+
+
+def ppo_cpu_baseline_report(procs):
+    """train/spp_ppo_hcheetah.py's layout: a multiprocessing pool of independent 1-thread runs."""
+    import multiprocessing as mp
+
+    one = _ppo_cpu_worker(0)
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    for k in saved:
+        os.environ[k] = "-1"
+    try:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_ppo_cpu_worker, range(procs))
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    vals = [r["value"] for r in res]
+    return {"value": round(sum(vals), 2), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "per_core": round(sum(vals) / procs, 2), "one_core": one["value"], "cpu_model": _cpu_model(),
+            "cores_note": "the box's CPU share is 16 and at most 16 processes may hold the GPU runtime (this "
+                          "process included), so the pool is 15 single-thread workers",
+            "sample": "%d concurrent 1-thread processes of the reference's PPO_AcM iteration restated on the CPU "
+                      "(oracle/cpu_loop_ppo.py: 2000-frame single-env collection with actor sample + AcM, 10 x 10 "
+                      "full-batch critic steps, the GAE loop, <= 10 clip-loss epochs of 512 with the KL stop, the "
+                      "ACM ring, 5 ACM epochs of 64-sample batches over the 1e5-row ring every 3 iterations, obs "
+                      "stats), one ACM cycle = 3 iterations = %d frames each (%.1f s); one_core = the same alone"
+                      % (procs, res[0]["frames"], res[0]["seconds"])}
+
+
 def default_cpu_procs():
     # The GPU box gives one job a 16-CPU share (os.cpu_count() reports the whole machine there)
     # and counts every process that imports the ROCm torch runtime as a GPU user (at most 16,
@@ -376,9 +416,7 @@ def bench_ppo(args, world, rank, dev):
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = {"value": None, "unit": "env-steps/s", "cores": 0, "kind": "port",
-                               "sample": "not run: the PPO_AcM CPU loop restatement is not built (the oracle pins the "
-                                         "PPO_AcM math per step, tests/test_oracle_golden.py)"}
+        res["cpu_baseline"] = ppo_cpu_baseline_report(args.cpu_procs or default_cpu_procs())
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

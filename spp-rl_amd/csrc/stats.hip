@@ -297,16 +297,28 @@ __global__ __launch_bounds__(kStPassThreads) __attribute__((amdgpu_waves_per_eu(
       for (int u = 0; u < U; ++u) x[1][u] = ld_x(n[u], c1);
     }
   };
-  // one key: moments, far-side counts; the rare keys inside a bracket take the slow path
-  auto proc = [&](int j, float xv, bool v) {
-    const double d = v ? (double)xv - piv[j] : 0.0;
+  // bracket widths: key in [lo, hi]  <=>  key - lo <= hi - lo  (unsigned; lo <= hi by construction)
+  uint32_t wd[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) wd[j][t] = hi[j][t] - lo[j][t];
+  // one key: moments, far-side counts; the rare keys inside a bracket take the slow path.
+  // V: the iteration has rows past len (per-row validity); full iterations skip it.
+  auto proc = [&](auto VC, int j, float xv, bool v) {
+    constexpr bool V = decltype(VC)::value;
+    double d = (double)xv - piv[j];
+    if constexpr (V) d = v ? d : 0.0;
     s1[j] += d;
     s2[j] = fma(d, d, s2[j]);
     const uint32_t key = fkey(xv);
-    cout[j][0] += (uint32_t)(v && key > hi[j][0]);
-    cout[j][1] += (uint32_t)(v && key < lo[j][1]);
-    const bool in0 = v && key >= lo[j][0] && key <= hi[j][0];
-    const bool in1 = v && key >= lo[j][1] && key <= hi[j][1];
+    bool o0 = key > hi[j][0], o1 = key < lo[j][1];
+    bool in0 = key - lo[j][0] <= wd[j][0], in1 = key - lo[j][1] <= wd[j][1];
+    if constexpr (V) {
+      o0 = o0 && v; o1 = o1 && v; in0 = in0 && v; in1 = in1 && v;
+    }
+    cout[j][0] += (uint32_t)o0;
+    cout[j][1] += (uint32_t)o1;
     if (in0 || in1) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -344,11 +356,26 @@ __global__ __launch_bounds__(kStPassThreads) __attribute__((amdgpu_waves_per_eu(
     const uint32_t v = vX;
     vX = vA;
     idx_load(rg0 + 2 * it_rows, nA, vA);
+    // every row of the iteration is live: lanes without a column are masked once, no per-key validity
+    const bool full = (rg0 + (int64_t)(U - 1) * nw) * G + G - 1 < a.len;
+    if (full) {
+      if (col[0] >= 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) proc(0, xA[0][u], (v >> u) & 1u);
-    if constexpr (WIDE) {
+        for (int u = 0; u < U; ++u) proc(IC<0>{}, 0, xA[0][u], true);
+      }
+      if constexpr (WIDE) {
+        if (col[1] >= 0) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) proc(1, xA[1][u], ((v >> u) & 1u) && col[1] >= 0);
+          for (int u = 0; u < U; ++u) proc(IC<0>{}, 1, xA[1][u], true);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) proc(IC<1>{}, 0, xA[0][u], (v >> u) & 1u);
+      if constexpr (WIDE) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) proc(IC<1>{}, 1, xA[1][u], ((v >> u) & 1u) && col[1] >= 0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

@@ -70,10 +70,12 @@ def _resources(text):
         if m:
             cur = out.setdefault(m.group(1), {})
             continue
-        m = re.search(r"remark:\s+(VGPRs|AGPRs|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]): (\d+)", line)
+        m = re.search(r"remark:\s+(VGPRs|AGPRs|VGPRs Spill|SGPRs Spill|LDS Size \[bytes/block\]|"
+                      r"ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)", line)
         if m and cur is not None:
             key = {"VGPRs": "vgpr", "AGPRs": "agpr", "VGPRs Spill": "vgpr_spill", "SGPRs Spill": "sgpr_spill",
-                   "LDS Size [bytes/block]": "lds"}[m.group(1)]
+                   "LDS Size [bytes/block]": "lds", "ScratchSize [bytes/lane]": "scratch",
+                   "Occupancy [waves/SIMD]": "occupancy"}[m.group(1)]
             cur[key] = int(m.group(2))
     return out
 
@@ -111,11 +113,13 @@ def report_spills(objs, verbose=True):
     with open(os.path.join(OBJ, "kernel_resources.json"), "w") as f:
         json.dump(allres, f, indent=1, sort_keys=True)
     spills = {k: v["vgpr_spill"] for k, v in allres.items() if v.get("vgpr_spill", 0) > 0}
+    # a spill with no scratch memory went to free AGPRs of the unified register file
+    mem = {k: n for k, n in spills.items() if allres[k].get("scratch", 1) > 0}
     if verbose and spills:
-        print("kernels with VGPR scratch spills:")
-        for k, n in sorted(spills.items(), key=lambda kv: -kv[1]):
-            print("  %4d  %s" % (n, k[:150]))
-    return spills
+        print("kernels with VGPR spills (scratch bytes/lane; 0 = spilled into AGPRs, no memory):")
+        for k, n in sorted(spills.items(), key=lambda kv: (-(kv[0] in mem), -kv[1])):
+            print("  %4d  %4s  %s" % (n, allres[k].get("scratch", "?"), k[:150]))
+    return mem
 
 
 def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, nodense=False):

@@ -977,6 +977,9 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
       // small jobs: >= 2048 samples per item, and at most ~256 slabs (the fixed-order reduce is
       // serial over slabs)
       int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
+      // small batches (PPO minibatches of 512): at least 4 items, so each wave of an item takes one
+      // 32-sample unit instead of a serial chain over the whole batch
+      if (!is_big(j)) ns = std::max(ns, std::min(cdiv(Bp, 32 * j.wsplit), 4));
       ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
       j.split_len = (int)round_up(cdiv(Bp, ns), 32 * j.wsplit);
       j.nsplit = cdiv(Bp, j.split_len);
@@ -1980,15 +1983,17 @@ static OnpArgs onp_args(sppOnPolicy* o, int N) {
   return p;
 }
 
-static sppStatus onp_ready(sppOnPolicy* o, int N, hipStream_t st) {
+// net 0: repack the actor's weight images (the params may have changed since the last call), 1: the
+// critic's; the other network's images are not touched.
+static sppStatus onp_ready(sppOnPolicy* o, int N, hipStream_t st, int net) {
   SPP_REQUIRE(N > 0 && N <= o->cfg.max_batch, SPP_E_SHAPE, "batch %d outside (0, max_batch=%d]", N, o->cfg.max_batch);
   SPP_REQUIRE(o->lim.ptr, SPP_E_STATE, "actor limits not set");
   if (!o->pk.ptr) {
     sppStatus s = onp_packs(o);
     if (s) return s;
   }
-  hipLaunchKernelGGL(k_pack_matrix, dim3(16, o->npj_actor + o->npj_critic), dim3(256), 0, st,
-                     (const PackJob*)o->d_pj.ptr);
+  const PackJob* pj = (const PackJob*)o->d_pj.ptr + (net == 0 ? 0 : o->npj_actor);
+  hipLaunchKernelGGL(k_pack_matrix, dim3(16, net == 0 ? o->npj_actor : o->npj_critic), dim3(256), 0, st, pj);
   return SPP_OK;
 }
 
@@ -2069,7 +2074,7 @@ sppStatus sppOnpSetLimits(sppOnPolicyHandle o, const float* lim_host) {
 sppStatus sppOnpValue(sppOnPolicyHandle o, const float* x, int N, float* v, void* stream) {
   SPP_REQUIRE(o && x && v, SPP_E_INVALID_ARG, "value: null");
   hipStream_t st = S(stream);
-  sppStatus s = onp_ready(o, N, st);
+  sppStatus s = onp_ready(o, N, st, 1);
   if (s) return s;
   OnpArgs p = onp_args(o, N);
   p.X = x;
@@ -2082,7 +2087,7 @@ sppStatus sppOnpValue(sppOnPolicyHandle o, const float* x, int N, float* v, void
 sppStatus sppOnpCriticGrads(sppOnPolicyHandle o, const float* x, const float* q, int N, float* loss, void* stream) {
   SPP_REQUIRE(o && x && q, SPP_E_INVALID_ARG, "critic grads: null");
   hipStream_t st = S(stream);
-  sppStatus s = onp_ready(o, N, st);
+  sppStatus s = onp_ready(o, N, st, 1);
   if (s) return s;
   if (o->dw[0].B != N && (s = onp_dw(o, 0, N))) return s;
   OnpArgs p = onp_args(o, N);
@@ -2111,7 +2116,7 @@ sppStatus sppOnpActorGrads(sppOnPolicyHandle o, const float* x, const float* act
                            const float* adv, const float* next_obs, int N, float* out4, void* stream) {
   SPP_REQUIRE(o && x && act && lp_old && adv && out4, SPP_E_INVALID_ARG, "actor grads: null");
   hipStream_t st = S(stream);
-  sppStatus s = onp_ready(o, N, st);
+  sppStatus s = onp_ready(o, N, st, 0);
   if (s) return s;
   if (o->dw[1].B != N && (s = onp_dw(o, 1, N))) return s;
   OnpArgs p = onp_args(o, N);
@@ -2139,7 +2144,7 @@ sppStatus sppOnpAct(sppOnPolicyHandle o, const float* x, int N, const float* eps
                     void* stream) {
   SPP_REQUIRE(o && x && act_out, SPP_E_INVALID_ARG, "act: null");
   hipStream_t st = S(stream);
-  sppStatus s = onp_ready(o, N, st);
+  sppStatus s = onp_ready(o, N, st, 0);
   if (s) return s;
   OnpArgs p = onp_args(o, N);
   p.X = x; p.EPS = eps; p.ACT_OUT = act_out; p.LP_OUT = logp_out;

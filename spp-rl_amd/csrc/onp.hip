@@ -334,23 +334,31 @@ __global__ void k_onp_finish_critic(const float* part, int ntiles, int stride, i
   const double l = block_sum(part, ntiles, stride, 0);
   if (threadIdx.x == 0 && out) out[0] = (float)(l / N);
 }
-// out[3] = entropy of Independent(Normal(mu, exp(log_scale))) = sum_j 0.5 + 0.5 log(2 pi) + log_scale_j
+// out[3] = entropy of Independent(Normal(mu, exp(log_scale))) = sum_j 0.5 + 0.5 log(2 pi) + log_scale_j.
+// All 3 + aout partial slots are reduced in one pass (one sync): thread t sums slot t % ns over the
+// tiles t / ns, t / ns + nsub, ...; the nsub sub-sums of a slot are then added in order.
 __global__ void k_onp_finish_actor(const float* part, int ntiles, int stride, int N, int aout, float ent_coef,
                                    const float* log_scale, float* gls, float* out) {
-  const double sm = block_sum(part, ntiles, stride, 0);
-  const double sk = block_sum(part, ntiles, stride, 1);
-  const double sd = block_sum(part, ntiles, stride, 2);
-  if (threadIdx.x == 0 && out) {
+  __shared__ double red[256];
+  const int ns = 3 + aout, nsub = (int)blockDim.x / ns, t = threadIdx.x;
+  const int slot = t % ns, sub = t / ns;
+  double s = 0.0;
+  if (sub < nsub)
+    for (int i = sub; i < ntiles; i += nsub) s += (double)part[(int64_t)i * stride + slot];
+  red[t] = s;
+  __syncthreads();
+  if (t < ns) {
+    double tot = 0.0;
+    for (int k = 0; k < nsub; ++k) tot += red[k * ns + t];
+    if (t == 0 && out) out[0] = (float)(-tot / N);
+    if (t == 1 && out) out[1] = (float)(tot / N);
+    if (t == 2 && out) out[2] = (float)(tot / ((double)N * aout));
+    if (t >= 3) gls[t - 3] = (float)(tot - (double)ent_coef);
+  }
+  if (t == 0 && out) {
     double ent = 0.0;
     for (int j = 0; j < aout; ++j) ent += 0.5 + 0.91893853320467274178 + (double)log_scale[j];
-    out[0] = (float)(-sm / N);
-    out[1] = (float)(sk / N);
-    out[2] = (float)(sd / ((double)N * aout));
     out[3] = (float)ent;
-  }
-  for (int j = 0; j < aout; ++j) {
-    const double g = block_sum(part, ntiles, stride, 3 + j);
-    if (threadIdx.x == 0) gls[j] = (float)(g - (double)ent_coef);
   }
 }
 

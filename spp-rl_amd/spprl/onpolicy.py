@@ -123,10 +123,13 @@ class OnPolicyNets:
             return q - self.value(obs)
 
     # ------------------------------------------------------------------ actor
-    def actor_step(self, x, act, lp_old, adv, next_obs=None):
+    def actor_step(self, x, act, lp_old, adv, next_obs=None, out=None):
+        """One minibatch step; ``out`` (4 floats: actor loss, KL, dist, entropy) is written, not
+        accumulated, so a caller may hand in rows of a preallocated [steps][4] buffer."""
         x, act, lp_old, adv = (self._dev(t) for t in (x, act, lp_old, adv))
         nxt = self._dev(next_obs) if next_obs is not None else None
-        out = torch.zeros(4, device=self.device)
+        if out is None:
+            out = torch.empty(4, device=self.device)
         call("sppOnpActorGrads", self._h, ptr(x), ptr(act), ptr(lp_old.reshape(-1)), ptr(adv.reshape(-1)), ptr(nxt),
              x.shape[0], ptr(out), stream_handle())
         if self.allreduce is not None:  # average the actor gradient and the loss / KL partials
@@ -164,11 +167,13 @@ class OnPolicyNets:
             # one permuted copy per epoch: every minibatch is then a contiguous slice
             o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]
             n_p = nxt[perm] if nxt is not None else None
-            for s in range(0, N, mb):
+            outs = torch.empty(-(-N // mb), 4, device=self.device)  # one row per minibatch step
+            for k, s in enumerate(range(0, N, mb)):
                 e = s + mb
-                out = self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None)
-                sums += out
-            kl = float(out[1].item())  # KL of the epoch's last minibatch (ppo.py:188)
+                self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None,
+                                out=outs[k])
+            sums += outs.sum(0)
+            kl = float(outs[-1, 1].item())  # KL of the epoch's last minibatch (ppo.py:188)
         self.loss.update(actor=float(sums[0]) / (i + 1), entropy=float(sums[3]) / (i + 1), kl=kl)
         return kl
 

@@ -1742,9 +1742,9 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
   AcmSgdArgs g{x, y, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout, loss_sum};
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
-  if (ob == 11 && ac == 3) hipLaunchKernelGGL((k_acm_sgd<22, 3>), dim3(1), dim3(kSgdThreads), 0, st, g);
-  else if (ob == 17 && ac == 6) hipLaunchKernelGGL((k_acm_sgd<34, 6>), dim3(1), dim3(kSgdThreads), 0, st, g);
-  else if (ob == 3 && ac == 1) hipLaunchKernelGGL((k_acm_sgd<6, 1>), dim3(1), dim3(kSgdThreads), 0, st, g);
+  if (ob == 11 && ac == 3) hipLaunchKernelGGL((k_acm_sgd<22, 3, 256>), dim3(1), dim3(256), 0, st, g);
+  else if (ob == 17 && ac == 6) hipLaunchKernelGGL((k_acm_sgd<34, 6, 512>), dim3(1), dim3(512), 0, st, g);
+  else if (ob == 3 && ac == 1) hipLaunchKernelGGL((k_acm_sgd<6, 1, 512>), dim3(1), dim3(512), 0, st, g);
   else SPP_REQUIRE(false, SPP_E_SHAPE, "acm_sgd: no instantiation for ob=%d ac=%d", ob, ac);
   a->steps[3] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());

@@ -38,7 +38,7 @@ struct AcmSgdArgs {
   float* loss_sum;     // += sum of the steps' batch losses (fp32 scalar)
 };
 
-template <int IN, int AC>
+template <int IN, int AC, int TH>
 struct SgdCfg {
   static constexpr int I1P = (IN + 1 + 3) / 4 * 4;
   static constexpr int H1P = 68, H2P = 36;
@@ -46,7 +46,7 @@ struct SgdCfg {
   // parameter tiles (4 rows x 4 columns): layer 1 | layer 2 | layer 3
   static constexpr int T1 = 16 * (I1P / 4), T2 = 8 * (H1P / 4), T3 = (ACP / 4) * (H2P / 4);
   static constexpr int NT = T1 + T2 + T3;
-  static constexpr int RT = (NT + kSgdThreads - 1) / kSgdThreads;  // tiles per thread
+  static constexpr int RT = (NT + TH - 1) / TH;  // tiles per thread
 };
 
 // canonical flat index of augmented (layer, row, col); -1 for padding
@@ -114,9 +114,10 @@ __device__ __forceinline__ void outer4x4(const float* A, int lda, const float* B
   }
 }
 
-template <int IN, int AC>
-__global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
-  using C = SgdCfg<IN, AC>;
+// TH threads (a multiple of 64): 512 (two waves per SIMD) where the per-thread registers fit in 256.
+template <int IN, int AC, int TH>
+__global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
+  using C = SgdCfg<IN, AC, TH>;
   constexpr int I1P = C::I1P, H1P = C::H1P, H2P = C::H2P, ACP = C::ACP, MB = kSgdMaxBatch;
   __shared__ __attribute__((aligned(16))) float W1[64 * I1P];
   __shared__ __attribute__((aligned(16))) float W2[32 * H1P];
@@ -128,56 +129,56 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
   __shared__ __attribute__((aligned(16))) float D2T[32 * MB];
   __shared__ __attribute__((aligned(16))) float D3[MB * ACP];
   __shared__ float Y[MB * AC];
-  __shared__ float lsum[kSgdThreads / 64];
+  __shared__ float lsum[TH / 64];
   const int t = threadIdx.x;
   const int bs = a.bs, bsp = (bs + 3) & ~3;
   // register prefetch of one step's batch: x elements t, t + 256, ... of [bs][IN]; y likewise
-  constexpr int NXP = (MB * IN + kSgdThreads - 1) / kSgdThreads, NYP = (MB * AC + kSgdThreads - 1) / kSgdThreads;
+  constexpr int NXP = (MB * IN + TH - 1) / TH, NYP = (MB * AC + TH - 1) / TH;
   float xp[NXP], yp[NYP];
   auto prefetch = [&](int st) {
     const float* xs = a.x + (int64_t)st * bs * IN;
     const float* ys = a.y + (int64_t)st * bs * AC;
 #pragma unroll
     for (int k = 0; k < NXP; ++k) {
-      const int i = t + kSgdThreads * k;
+      const int i = t + TH * k;
       xp[k] = (st < a.nsteps && i < bs * IN) ? xs[i] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < NYP; ++k) {
-      const int i = t + kSgdThreads * k;
+      const int i = t + TH * k;
       yp[k] = (st < a.nsteps && i < bs * AC) ? ys[i] : 0.f;
     }
   };
   auto stage = [&]() {  // prefetched batch -> X [bsp][I1P] (bias column = 1, zero padding), Y
 #pragma unroll
     for (int k = 0; k < NXP; ++k) {
-      const int i = t + kSgdThreads * k;
+      const int i = t + TH * k;
       if (i < bs * IN) X[(i / IN) * I1P + (i % IN)] = xp[k];
     }
 #pragma unroll
     for (int k = 0; k < NYP; ++k) {
-      const int i = t + kSgdThreads * k;
+      const int i = t + TH * k;
       if (i < bs * AC) Y[i] = yp[k];
     }
-    for (int i = t; i < bsp * (I1P - IN); i += kSgdThreads) {
+    for (int i = t; i < bsp * (I1P - IN); i += TH) {
       const int b = i / (I1P - IN), k = IN + i % (I1P - IN);
       X[b * I1P + k] = (k == IN && b < bs) ? 1.f : 0.f;
     }
-    for (int i = t; i < (bsp - bs) * IN; i += kSgdThreads) X[(bs + i / IN) * I1P + (i % IN)] = 0.f;
+    for (int i = t; i < (bsp - bs) * IN; i += TH) X[(bs + i / IN) * I1P + (i % IN)] = 0.f;
   };
   auto wrow = [&](int layer, int row) -> float* {  // augmented row of a layer's image
     return layer == 0 ? W1 + row * I1P : (layer == 1 ? W2 + row * H1P : W3 + row * H2P);
   };
   // parameters -> augmented LDS images (zero padding)
-  for (int i = t; i < 64 * I1P; i += kSgdThreads) {
+  for (int i = t; i < 64 * I1P; i += TH) {
     const int c = sgd_canon<IN, AC>(0, i / I1P, i % I1P);
     W1[i] = c >= 0 ? a.params[c] : 0.f;
   }
-  for (int i = t; i < 32 * H1P; i += kSgdThreads) {
+  for (int i = t; i < 32 * H1P; i += TH) {
     const int c = sgd_canon<IN, AC>(1, i / H1P, i % H1P);
     W2[i] = c >= 0 ? a.params[c] : 0.f;
   }
-  for (int i = t; i < ACP * H2P; i += kSgdThreads) {
+  for (int i = t; i < ACP * H2P; i += TH) {
     const int c = sgd_canon<IN, AC>(2, i / H2P, i % H2P);
     W3[i] = c >= 0 ? a.params[c] : 0.f;
   }
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
   float mom[C::RT][16], vel[C::RT][16];
 #pragma unroll
   for (int k = 0; k < C::RT; ++k) {
-    const int q = t + kSgdThreads * k;
+    const int q = t + TH * k;
     int layer = 0, r0 = 0, c0 = 0;
     if (q < C::NT) sgd_tile<C>(q, layer, r0, c0);
 #pragma unroll
@@ -203,14 +204,14 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     // ---- this step's batch into LDS, the next step's loads in flight behind the compute
     stage();
     prefetch(st + 1);
-    for (int i = t; i < bsp * 4; i += kSgdThreads) {  // bias / padding columns of h1 (64..67), h2 (32..35)
+    for (int i = t; i < bsp * 4; i += TH) {  // bias / padding columns of h1 (64..67), h2 (32..35)
       const int b = i >> 2, j = i & 3;
       H1[b * H1P + 64 + j] = j == 0 ? 1.f : 0.f;
       H2[b * H2P + 32 + j] = j == 0 ? 1.f : 0.f;
     }
     __syncthreads();
     // ---- forward: h1 = tanh(fc1 x), h2 = tanh(fc2 h1) in 4 (samples) x 4 (units) tiles
-    for (int tt = t; tt < (bsp / 4) * 16; tt += kSgdThreads) {
+    for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
       const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
       float acc[4][4] = {};
       dot4x4(X + b0 * I1P, I1P, W1 + j0 * I1P, I1P, I1P / 4, acc);
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
             make_float4(tanhf(acc[i][0]), tanhf(acc[i][1]), tanhf(acc[i][2]), tanhf(acc[i][3]));
     }
     __syncthreads();
-    for (int tt = t; tt < (bsp / 4) * 8; tt += kSgdThreads) {
+    for (int tt = t; tt < (bsp / 4) * 8; tt += TH) {
       const int b0 = 4 * (tt >> 3), j0 = 4 * (tt & 7);
       float acc[4][4] = {};
       dot4x4(H1 + b0 * H1P, H1P, W2 + j0 * H1P, H1P, H1P / 4, acc);
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     __syncthreads();
     // ---- out = tanh(fc3 h2) * lim, MSE loss, dz3 = 2 (out - y) / n * lim * (1 - tanh^2)
     float lpart = 0.f;
-    for (int i = t; i < bsp * ACP; i += kSgdThreads) {
+    for (int i = t; i < bsp * ACP; i += TH) {
       const int b = i / ACP, c = i % ACP;
       float d = 0.f;
       if (b < bs && c < AC) {
@@ -254,9 +255,14 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     for (int o = 32; o > 0; o >>= 1) lpart += __shfl_xor(lpart, o, 64);
     if ((t & 63) == 0) lsum[t >> 6] = lpart;
     __syncthreads();
-    if (t == 0) loss_acc += (lsum[0] + lsum[1] + lsum[2] + lsum[3]) * inv_n;
+    if (t == 0) {
+      float ls = 0.f;
+#pragma unroll
+      for (int w = 0; w < TH / 64; ++w) ls += lsum[w];
+      loss_acc += ls * inv_n;
+    }
     // dz2 = (W3^T dz3) * (1 - h2^2), stored [b][32] and [32][b]
-    for (int i = t; i < bsp * 32; i += kSgdThreads) {
+    for (int i = t; i < bsp * 32; i += TH) {
       const int b = i >> 5, j = i & 31;
       float g = 0.f;
 #pragma unroll
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) g[k][i][j] = 0.f;
-      const int q = t + kSgdThreads * k;
+      const int q = t + TH * k;
       if (q >= C::T1 && q < C::NT) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     }
     __syncthreads();  // h1 is read above; it becomes dz1 below
     // dz1 = (W2^T dz2) * (1 - h1^2), in place of h1, 4 x 4 tiles over (samples, units)
-    for (int tt = t; tt < (bsp / 4) * 16; tt += kSgdThreads) {
+    for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
       const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
       float acc[4][4] = {};
       outer4x4(D2T + b0, MB, W2 + j0, H1P, 32, acc);
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     // part 2: layer 1 (dz1 x x)
 #pragma unroll
     for (int k = 0; k < C::RT; ++k) {
-      const int q = t + kSgdThreads * k;
+      const int q = t + TH * k;
       if (q < C::T1) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
@@ -316,7 +322,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
     __syncthreads();  // every thread has read the parameters it needs (dz1 used W2, dz2 used W3)
 #pragma unroll
     for (int k = 0; k < C::RT; ++k) {
-      const int q = t + kSgdThreads * k;
+      const int q = t + TH * k;
       if (q < C::NT) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(kSgdThreads, 1) void k_acm_sgd(AcmSgdArgs a) {
   // ---- write back parameters and moments (canonical layout)
 #pragma unroll
   for (int k = 0; k < C::RT; ++k) {
-    const int q = t + kSgdThreads * k;
+    const int q = t + TH * k;
     if (q < C::NT) {
       int layer, r0, c0;
       sgd_tile<C>(q, layer, r0, c0);

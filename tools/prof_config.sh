@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 C=${CONFIG:-sac_hopper}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$C -o run --output-format csv \
-  -- python3 $R/bench.py --config $C --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$C.log 2>&1
+  -- python3 $R/bench.py --config $C --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-pmc > $R/gpurun_out/prof_$C.log 2>&1
 python3 - $C <<'PY'
 import csv, os, sys
 R = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")

@@ -127,7 +127,8 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
         out = os.path.join(HERE, "spprl", "libspprl_prof.so")
         extra = (["-DSPP_ONLY_HOPPER"] if hopper_only else []) + (["-DSPP_PROF_NODENSE"] if nodense else []) + (
             ["-DSPP_ONLY_BF16"] if "--bf16-only" in sys.argv else []) + (
-            ["-DSPP_PROF_DRAIN"] if "--drain" in sys.argv else [])
+            ["-DSPP_PROF_DRAIN"] if "--drain" in sys.argv else []) + (
+            ["-DSPP_WITH_HCHEETAH"] if "--hcheetah" in sys.argv else [])
         cmd = [HIPCC] + FLAGS + ["-shared", "-DSPP_PROF", "-DSPP_SINGLE_TU"] + extra + [
             "-o", out, os.path.join(CSRC, "api.hip")]
         subprocess.check_call(cmd)

@@ -24,6 +24,9 @@
 #ifdef SPP_SINGLE_TU  // profiling / development builds: everything in one TU
 #include "ks_dw.hip"
 #include "ks_sac_hopper.hip"
+#if defined(SPP_WITH_HCHEETAH)  // region-profiling builds of the HalfCheetah AcM SGD: + the HalfCheetah set
+#include "ks_sac_hcheetah.hip"
+#endif
 #if defined(SPP_ONLY_BF16)  // region-profiling builds of the bf16 sets: Hopper fp32 + bf16 only
 #define SPP_ONLY_HOPPER
 #include "ks_sac_bf16.hip"
@@ -692,6 +695,9 @@ static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, 
   }
   if (algo == SPP_ALGO_SAC_ACM) {
     if (kset_sac_hopper(ob, aout, ac, acmc, ks)) return true;
+#if defined(SPP_ONLY_HOPPER) && defined(SPP_WITH_HCHEETAH)
+    if (kset_sac_hcheetah(ob, aout, ac, acmc, ks)) return true;
+#endif
 #ifndef SPP_ONLY_HOPPER  // kernel-development builds: one instantiation, fast compile
     if (kset_sac_hcheetah(ob, aout, ac, acmc, ks)) return true;
     if (kset_sac_ant(ob, aout, ac, acmc, ks)) return true;

@@ -32,8 +32,8 @@ __shared__ unsigned long long s_tlast[4];
 #define SPP_TP_INIT()                                                            \
   {                                                                              \
     const int w_ = threadIdx.x >> 6;                                             \
-    if ((threadIdx.x & 63) < 32) s_tprof[w_][threadIdx.x & 63] = 0;              \
-    if ((threadIdx.x & 63) == 0) s_tlast[w_] = clock64();                        \
+    if ((threadIdx.x & 63) < 32 && w_ < 4) s_tprof[w_][threadIdx.x & 63] = 0;    \
+    if ((threadIdx.x & 63) == 0 && w_ < 4) s_tlast[w_] = clock64();              \
   }
 #define SPP_TP(k)                                                                \
   {                                                                              \
@@ -50,7 +50,7 @@ __shared__ unsigned long long s_tlast[4];
 #define SPP_TP_FLUSH()                                                           \
   {                                                                              \
     const int w_ = threadIdx.x >> 6, l_ = threadIdx.x & 63;                      \
-    if (l_ < 32) atomicAdd(&g_tprof[l_], s_tprof[w_][l_]);                       \
+    if (l_ < 32 && w_ < 4) atomicAdd(&g_tprof[l_], s_tprof[w_][l_]);             \
   }
 #else
 #define SPP_TP_INIT()

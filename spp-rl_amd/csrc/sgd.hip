@@ -46,7 +46,13 @@ struct SgdCfg {
   // parameter tiles (4 rows x 4 columns): layer 1 | layer 2 | layer 3
   static constexpr int T1 = 16 * (I1P / 4), T2 = 8 * (H1P / 4), T3 = (ACP / 4) * (H2P / 4);
   static constexpr int NT = T1 + T2 + T3;
-  static constexpr int RT = (NT + TH - 1) / TH;  // tiles per thread
+  // PAIR (>= 8 waves): lane l < 32 of wave w owns gradient-phase-1 tile T1 + 32w + l (layers 2, 3) and
+  // lane l + 32 owns phase-2 tile 32w + l (layer 1); in each gradient phase the idle lane of the pair
+  // takes half of the samples of its partner's tile (one lane-swap add), and the second forward layer
+  // (half as many tiles as threads of 4 waves) is split over 4 lanes along K.  The phases that already
+  // keep every SIMD busy are not split: a split over more waves only adds work to the same SIMDs.
+  static constexpr bool PAIR = TH >= 512 && (TH / 64) * 32 >= T2 + T3 && (TH / 64) * 32 >= T1;
+  static constexpr int RT = PAIR ? 1 : (NT + TH - 1) / TH;  // tiles per thread
 };
 
 // canonical flat index of augmented (layer, row, col); -1 for padding
@@ -81,8 +87,50 @@ __device__ __forceinline__ void sgd_tile(int q, int& layer, int& r0, int& c0) {
   }
 }
 
+// the tile thread t owns (its k-th, k < RT), or -1
+template <class C, int TH>
+__device__ __forceinline__ int sgd_own(int t, int k) {
+  if constexpr (C::PAIR) {
+    const int w = t >> 6, l = t & 63;
+    if (l < 32) {
+      const int j = 32 * w + l;
+      return j < C::T2 + C::T3 ? C::T1 + j : -1;
+    }
+    const int j = 32 * w + l - 32;
+    return j < C::T1 ? j : -1;
+  } else {
+    const int q = t + TH * k;
+    return q < C::NT ? q : -1;
+  }
+}
+
+// v + (v of lane ^ M), M = 16 or 32, through gfx950's v_permlane16/32_swap (no LDS round trip): with
+// both operands = v the swap leaves the two halves of each lane pair in the two results, and every lane
+// adds them in the same order, so both lanes of a pair hold the same sum.
+template <int M>
+__device__ __forceinline__ float xor_sum(float v) {
+  const unsigned u = __float_as_uint(v);
+  if constexpr (M == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+}
+template <int M>
+__device__ __forceinline__ void add_xor(float (&acc)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = xor_sum<M>(acc[i][j]);
+}
+
 // acc[i][j] += sum_k A[i][k] B[j][k]  (rows i / j of A / B, K contiguous, K4 float4 steps)
+// (the k loops are unrolled so several steps' LDS reads are in flight: one step's reads alone would
+// expose the LDS latency to every 16 FMAs)
 __device__ __forceinline__ void dot4x4(const float* A, int lda, const float* B, int ldb, int K4, float (&acc)[4][4]) {
+#pragma unroll 3
   for (int k = 0; k < K4; ++k) {
     float4 a[4], b[4];
 #pragma unroll
@@ -103,6 +151,7 @@ __device__ __forceinline__ void dot4x4(const float* A, int lda, const float* B, 
 }
 // acc[i][j] += sum_k A[k][i] B[k][j]  (4 consecutive entries of row k of A / B)
 __device__ __forceinline__ void outer4x4(const float* A, int lda, const float* B, int ldb, int K, float (&acc)[4][4]) {
+#pragma unroll 4
   for (int k = 0; k < K; ++k) {
     const float4 a = *reinterpret_cast<const float4*>(A + k * lda);
     const float4 b = *reinterpret_cast<const float4*>(B + k * ldb);
@@ -130,6 +179,13 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
   __shared__ __attribute__((aligned(16))) float D3[MB * ACP];
   __shared__ float Y[MB * AC];
   __shared__ float lsum[TH / 64];
+  __shared__ float adam_s[2][2];  // per step parity: -lr / (1 - b1^t), sqrt(1 - b2^t)
+  // Adam's bias corrections of step st (torch.optim.Adam), computed once instead of by every thread
+  auto adam_scalars = [&](int st) {
+    const double tstep = (double)(a.step0 + st + 1);
+    adam_s[st & 1][0] = (float)(-((double)a.lr / (1.0 - pow(0.9, tstep))));
+    adam_s[st & 1][1] = (float)sqrt(1.0 - pow(0.999, tstep));
+  };
   const int t = threadIdx.x;
   const int bs = a.bs, bsp = (bs + 3) & ~3;
   // register prefetch of one step's batch: x elements t, t + 256, ... of [bs][IN]; y likewise
@@ -186,12 +242,12 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
   float mom[C::RT][16], vel[C::RT][16];
 #pragma unroll
   for (int k = 0; k < C::RT; ++k) {
-    const int q = t + TH * k;
+    const int q = sgd_own<C, TH>(t, k);
     int layer = 0, r0 = 0, c0 = 0;
-    if (q < C::NT) sgd_tile<C>(q, layer, r0, c0);
+    if (q >= 0) sgd_tile<C>(q, layer, r0, c0);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int c = q < C::NT ? sgd_canon<IN, AC>(layer, r0 + (e >> 2), c0 + (e & 3)) : -1;
+      const int c = q >= 0 ? sgd_canon<IN, AC>(layer, r0 + (e >> 2), c0 + (e & 3)) : -1;
       mom[k][e] = c >= 0 ? a.m[c] : 0.f;
       vel[k][e] = c >= 0 ? a.v[c] : 0.f;
     }
@@ -199,7 +255,9 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
   float loss_acc = 0.f;
   const float inv_n = 1.f / (float)(bs * AC);
   prefetch(0);
+  if (t == 0) adam_scalars(0);
   __syncthreads();
+  SPP_TP_INIT();
   for (int st = 0; st < a.nsteps; ++st) {
     // ---- this step's batch into LDS, the next step's loads in flight behind the compute
     stage();
@@ -210,27 +268,52 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
       H2[b * H2P + 32 + j] = j == 0 ? 1.f : 0.f;
     }
     __syncthreads();
+    SPP_TP(0);
     // ---- forward: h1 = tanh(fc1 x), h2 = tanh(fc2 h1) in 4 (samples) x 4 (units) tiles
-    for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
-      const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
-      float acc[4][4] = {};
-      dot4x4(X + b0 * I1P, I1P, W1 + j0 * I1P, I1P, I1P / 4, acc);
+    {  // layer 1: 4 waves' worth of tiles, one per thread (a K split over more waves only adds work
+       // to the same SIMDs)
+      for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
+        const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
+        float acc[4][4] = {};
+        dot4x4(X + b0 * I1P, I1P, W1 + j0 * I1P, I1P, I1P / 4, acc);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(H1 + (b0 + i) * H1P + j0) =
-            make_float4(tanhf(acc[i][0]), tanhf(acc[i][1]), tanhf(acc[i][2]), tanhf(acc[i][3]));
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float4*>(H1 + (b0 + i) * H1P + j0) =
+              make_float4(tanhf(acc[i][0]), tanhf(acc[i][1]), tanhf(acc[i][2]), tanhf(acc[i][3]));
+      }
     }
     __syncthreads();
-    for (int tt = t; tt < (bsp / 4) * 8; tt += TH) {
-      const int b0 = 4 * (tt >> 3), j0 = 4 * (tt & 7);
-      float acc[4][4] = {};
-      dot4x4(H1 + b0 * H1P, H1P, W2 + j0 * H1P, H1P, H1P / 4, acc);
+    SPP_TP(1);
+    if constexpr (C::PAIR) {  // layer 2: lanes l, l + 16, l + 32, l + 48 split K (H1P / 4 = 17 float4 steps)
+      const int w = t >> 6, l = t & 63, qd = l >> 4;
+      constexpr int KQ = H1P / 16;  // 4; the last quarter takes the remainder
+      for (int base = 16 * w; base < (bsp / 4) * 8; base += 16 * (TH / 64)) {
+        const int tt = base + (l & 15);
+        const bool ok = tt < (bsp / 4) * 8;
+        const int b0 = ok ? 4 * (tt >> 3) : 0, j0 = 4 * (tt & 7);
+        float acc[4][4] = {};
+        const int k0 = KQ * qd, nk = qd == 3 ? H1P / 4 - 3 * KQ : KQ;
+        dot4x4(H1 + b0 * H1P + 4 * k0, H1P, W2 + j0 * H1P + 4 * k0, H1P, nk, acc);
+        add_xor<16>(acc);
+        add_xor<32>(acc);
+        if (ok) {  // lane quarter qd stores row qd
+          *reinterpret_cast<float4*>(H2 + (b0 + qd) * H2P + j0) =
+              make_float4(tanhf(acc[qd][0]), tanhf(acc[qd][1]), tanhf(acc[qd][2]), tanhf(acc[qd][3]));
+        }
+      }
+    } else {
+      for (int tt = t; tt < (bsp / 4) * 8; tt += TH) {
+        const int b0 = 4 * (tt >> 3), j0 = 4 * (tt & 7);
+        float acc[4][4] = {};
+        dot4x4(H1 + b0 * H1P, H1P, W2 + j0 * H1P, H1P, H1P / 4, acc);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(H2 + (b0 + i) * H2P + j0) =
-            make_float4(tanhf(acc[i][0]), tanhf(acc[i][1]), tanhf(acc[i][2]), tanhf(acc[i][3]));
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float4*>(H2 + (b0 + i) * H2P + j0) =
+              make_float4(tanhf(acc[i][0]), tanhf(acc[i][1]), tanhf(acc[i][2]), tanhf(acc[i][3]));
+      }
     }
     __syncthreads();
+    SPP_TP(2);
     // ---- out = tanh(fc3 h2) * lim, MSE loss, dz3 = 2 (out - y) / n * lim * (1 - tanh^2)
     float lpart = 0.f;
     for (int i = t; i < bsp * ACP; i += TH) {
@@ -255,6 +338,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     for (int o = 32; o > 0; o >>= 1) lpart += __shfl_xor(lpart, o, 64);
     if ((t & 63) == 0) lsum[t >> 6] = lpart;
     __syncthreads();
+    SPP_TP(3);
     if (t == 0) {
       float ls = 0.f;
 #pragma unroll
@@ -273,57 +357,104 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
       D2T[j * MB + b] = dz;
     }
     __syncthreads();
+    SPP_TP(4);
     // ---- owned gradient tiles, part 1: layers 2 (dz2 x h1) and 3 (dz3 x h2)
     float g[C::RT][4][4];
 #pragma unroll
-    for (int k = 0; k < C::RT; ++k) {
+    for (int k = 0; k < C::RT; ++k)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) g[k][i][j] = 0.f;
-      const int q = t + TH * k;
-      if (q >= C::T1 && q < C::NT) {
+    const int hs = bsp / 2;  // PAIR: sample split of a gradient tile between its two lanes
+    if constexpr (C::PAIR) {
+      const int l = t & 63;
+      const int q = sgd_own<C, TH>(l < 32 ? t : t ^ 32, 0);  // lane l < 32's tile (a phase-1 tile)
+      const int s0 = l < 32 ? 0 : hs, ns = l < 32 ? hs : bsp - hs;
+      float gp[4][4] = {};
+      if (q >= 0) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
-        if (layer == 1) outer4x4(D2 + r0, 32, H1 + c0, H1P, bsp, g[k]);
-        else outer4x4(D3 + r0, ACP, H2 + c0, H2P, bsp, g[k]);
+        if (layer == 1) outer4x4(D2 + s0 * 32 + r0, 32, H1 + s0 * H1P + c0, H1P, ns, gp);
+        else outer4x4(D3 + s0 * ACP + r0, ACP, H2 + s0 * H2P + c0, H2P, ns, gp);
+      }
+      add_xor<32>(gp);
+      if (l < 32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[0][i][j] = gp[i][j];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < C::RT; ++k) {
+        const int q = t + TH * k;
+        if (q >= C::T1 && q < C::NT) {
+          int layer, r0, c0;
+          sgd_tile<C>(q, layer, r0, c0);
+          if (layer == 1) outer4x4(D2 + r0, 32, H1 + c0, H1P, bsp, g[k]);
+          else outer4x4(D3 + r0, ACP, H2 + c0, H2P, bsp, g[k]);
+        }
       }
     }
     __syncthreads();  // h1 is read above; it becomes dz1 below
+    SPP_TP(5);
     // dz1 = (W2^T dz2) * (1 - h1^2), in place of h1, 4 x 4 tiles over (samples, units)
-    for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
-      const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
-      float acc[4][4] = {};
-      outer4x4(D2T + b0, MB, W2 + j0, H1P, 32, acc);
+    {  // one tile per thread (all 4 SIMDs already busy)
+      for (int tt = t; tt < (bsp / 4) * 16; tt += TH) {
+        const int b0 = 4 * (tt >> 4), j0 = 4 * (tt & 15);
+        float acc[4][4] = {};
+        outer4x4(D2T + b0, MB, W2 + j0, H1P, 32, acc);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float4* hp = reinterpret_cast<float4*>(H1 + (b0 + i) * H1P + j0);
-        const float4 h = *hp;
-        *hp = make_float4(acc[i][0] * (1.f - h.x * h.x), acc[i][1] * (1.f - h.y * h.y),
-                          acc[i][2] * (1.f - h.z * h.z), acc[i][3] * (1.f - h.w * h.w));
+        for (int i = 0; i < 4; ++i) {
+          float4* hp = reinterpret_cast<float4*>(H1 + (b0 + i) * H1P + j0);
+          const float4 h = *hp;
+          *hp = make_float4(acc[i][0] * (1.f - h.x * h.x), acc[i][1] * (1.f - h.y * h.y),
+                            acc[i][2] * (1.f - h.z * h.z), acc[i][3] * (1.f - h.w * h.w));
+        }
       }
     }
     __syncthreads();
+    SPP_TP(6);
     // part 2: layer 1 (dz1 x x)
-#pragma unroll
-    for (int k = 0; k < C::RT; ++k) {
-      const int q = t + TH * k;
-      if (q < C::T1) {
+    if constexpr (C::PAIR) {
+      const int l = t & 63;
+      const int q = sgd_own<C, TH>(l >= 32 ? t : t ^ 32, 0);  // lane l >= 32's tile (a layer-1 tile)
+      const int s0 = l >= 32 ? 0 : hs, ns = l >= 32 ? hs : bsp - hs;
+      float gp[4][4] = {};
+      if (q >= 0) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
-        outer4x4(H1 + r0, H1P, X + c0, I1P, bsp, g[k]);
+        outer4x4(H1 + s0 * H1P + r0, H1P, X + s0 * I1P + c0, I1P, ns, gp);
+      }
+      add_xor<32>(gp);
+      if (l >= 32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[0][i][j] = gp[i][j];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < C::RT; ++k) {
+        const int q = t + TH * k;
+        if (q < C::T1) {
+          int layer, r0, c0;
+          sgd_tile<C>(q, layer, r0, c0);
+          outer4x4(H1 + r0, H1P, X + c0, I1P, bsp, g[k]);
+        }
       }
     }
     // ---- Adam (torch.optim.Adam, same operation order as k_adam) on the owned tiles
-    const double tstep = (double)(a.step0 + st + 1);
-    const float neg_step = (float)(-((double)a.lr / (1.0 - pow(0.9, tstep))));
-    const float bc2s = (float)sqrt(1.0 - pow(0.999, tstep));
     const float omb1 = 0.1f, b2 = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     __syncthreads();  // every thread has read the parameters it needs (dz1 used W2, dz2 used W3)
+    const float neg_step = adam_s[st & 1][0], bc2s = adam_s[st & 1][1];
+    if (t == TH - 64) adam_scalars(st + 1);  // the next step's, by a wave that owns no tile
+    SPP_TP(7);
 #pragma unroll
     for (int k = 0; k < C::RT; ++k) {
-      const int q = t + TH * k;
-      if (q < C::NT) {
+      const int q = sgd_own<C, TH>(t, k);
+      if (q >= 0) {
         int layer, r0, c0;
         sgd_tile<C>(q, layer, r0, c0);
 #pragma unroll
@@ -342,12 +473,14 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
       }
     }
     __syncthreads();
+    SPP_TP(8);
   }
+  SPP_TP_FLUSH();
   // ---- write back parameters and moments (canonical layout)
 #pragma unroll
   for (int k = 0; k < C::RT; ++k) {
-    const int q = t + TH * k;
-    if (q < C::NT) {
+    const int q = sgd_own<C, TH>(t, k);
+    if (q >= 0) {
       int layer, r0, c0;
       sgd_tile<C>(q, layer, r0, c0);
 #pragma unroll

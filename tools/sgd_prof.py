@@ -1,0 +1,56 @@
+"""Region timing of the persistent AcM SGD kernel (k_acm_sgd) at the PPO HalfCheetah shape (AcM in 34,
+out 6, 64-sample batches).  Profiling build: python spp-rl_amd/build.py --prof --hopper-only --hcheetah, then
+SPPRL_LIB=spp-rl_amd/spprl/libspprl_prof.so python tools/sgd_prof.py"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "spp-rl_amd"), REPO]
+import torch  # noqa: E402
+
+import spprl  # noqa: E402
+from spprl import _lib  # noqa: E402
+
+NAMES = {0: "stage batch", 1: "fwd L1", 2: "fwd L2", 3: "out / loss / dz3", 4: "dz2", 5: "grads L2+L3",
+         6: "dz1", 7: "grads L1", 8: "Adam"}
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    ob, ac, bs, K = 17, 6, 64, 400
+    ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", max_batch=4096, buffer_size=20_000, device=dev, seed=0)
+    rb = ag.replay_buffer
+    n = 10_000
+    slots = rb.add_obs_batch(torch.randn(n + 1, ob, device=dev))
+    rb.add_timestep_batch(slots[:n], slots[1:], torch.randn(n, ob, device=dev), torch.randn(n, device=dev),
+                          torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
+                          torch.rand(n, ac, device=dev) * 2 - 1)
+    idx = torch.randint(0, n, (K * bs,), device=dev)
+    x = torch.empty(K * bs, 2 * ob, device=dev)
+    y = torch.empty(K * bs, ac, device=dev)
+    loss = torch.zeros(1, device=dev)
+    st = _lib.stream_handle()
+    _lib.call("sppReplayGatherAcm", rb._h, _lib.ptr(idx), K * bs, _lib.ptr(x), _lib.ptr(y), st)
+    _lib.call("sppAcmSgd", ag._h, _lib.ptr(x), _lib.ptr(y), K, bs, _lib.ptr(loss), st)  # warm-up
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 64)()
+    _lib.call("sppDebugReadProf", buf, 1)
+    t0 = time.perf_counter()
+    _lib.call("sppAcmSgd", ag._h, _lib.ptr(x), _lib.ptr(y), K, bs, _lib.ptr(loss), st)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    _lib.call("sppDebugReadProf", buf, 1)
+    v = np.array(buf[:32], dtype=np.float64) / (4 * K)  # waves 0..3 recorded
+    tot = v.sum()
+    print("k_acm_sgd<34, 6>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
+          % (K, bs, el * 1e3, el * 1e6 / K, tot))
+    for k in range(9):
+        print("  %2d %-20s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
+
+
+if __name__ == "__main__":
+    main()

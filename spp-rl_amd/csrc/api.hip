@@ -1442,7 +1442,7 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
   tmark(a, 2, st);
   launch_dw(a, 0, 0, st);
   tmark(a, 2, st);
-  hipLaunchKernelGGL(k_finalize_critic, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
+  hipLaunchKernelGGL(k_finalize_critic, dim3(1), dim3(kFinThreads), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -1489,7 +1489,7 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   tmark(a, 2, st);
   launch_dw(a, 0, 1, st);
   tmark(a, 2, st);
-  hipLaunchKernelGGL(k_actor_partials, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, a->cfg.aout,
+  hipLaunchKernelGGL(k_actor_partials, dim3(1), dim3(kFinThreads), 0, st, (const float*)a->part, p.Bp / 32, B, a->cfg.aout,
                      a->cfg.custom_loss, (double)a->cfg.target_entropy, a->alpha_grad ? a->alpha_grad : a->aux,
                      losses);
   SPP_CHECK_HIP(hipGetLastError());
@@ -1608,7 +1608,7 @@ sppStatus sppDdpgAcmCriticGrads(sppAgentHandle a, const sppBatch* bt, float* los
   tmark(a, 2, st);
   launch_dw(a, 0, 0, st);
   tmark(a, 2, st);
-  hipLaunchKernelGGL(k_finalize_ddpg_critic, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
+  hipLaunchKernelGGL(k_finalize_ddpg_critic, dim3(1), dim3(kFinThreads), 0, st, (const float*)a->part, p.Bp / 32, B, losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -1636,7 +1636,7 @@ sppStatus sppDdpgAcmActorGrads(sppAgentHandle a, float* losses, void* stream) {
   tmark(a, 2, st);
   launch_dw(a, 0, 1, st);
   tmark(a, 2, st);
-  hipLaunchKernelGGL(k_finalize_ddpg_actor, dim3(1), dim3(256), 0, st, (const float*)a->part, p.Bp / 32, B,
+  hipLaunchKernelGGL(k_finalize_ddpg_actor, dim3(1), dim3(kFinThreads), 0, st, (const float*)a->part, p.Bp / 32, B,
                      a->cfg.aout, a->cfg.custom_loss, losses);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;

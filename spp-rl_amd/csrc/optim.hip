@@ -108,10 +108,40 @@ __device__ double block_sum(const float* part, int ntiles, int stride, int slot)
   return r;
 }
 
-// losses[0..1] = critic MSEs (sac_acm.py:117-123)
-__global__ void k_finalize_critic(const float* part, int ntiles, int B, float* losses) {
-  const double l0 = block_sum(part, ntiles, 8, 0);
-  const double l1 = block_sum(part, ntiles, 8, 1);
+// NS consecutive partial slots [slot0, slot0 + NS) of every tile summed in ONE pass by kFinThreads
+// threads (several tiles' loads in flight per thread), then one fixed-order LDS tree per slot:
+// deterministic, and one memory latency chain instead of one per slot.
+constexpr int kFinThreads = 1024;
+template <int NS>
+__device__ void block_sums(const float* part, int ntiles, int stride, int slot0, double (&out)[NS]) {
+  __shared__ double red[NS][kFinThreads];
+  double s[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) s[j] = 0.0;
+#pragma unroll 4
+  for (int t = threadIdx.x; t < ntiles; t += kFinThreads) {
+    const float* p = part + (int64_t)t * stride + slot0;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) s[j] += (double)p[j];
+  }
+#pragma unroll
+  for (int j = 0; j < NS; ++j) red[j][threadIdx.x] = s[j];
+  __syncthreads();
+  for (int o = kFinThreads / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + o];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < NS; ++j) out[j] = red[j][0];
+}
+
+// losses[0..1] = critic MSEs (sac_acm.py:117-123); launched with kFinThreads threads
+__global__ __launch_bounds__(kFinThreads) void k_finalize_critic(const float* part, int ntiles, int B, float* losses) {
+  double l[2];
+  block_sums<2>(part, ntiles, 8, 0, l);
+  const double l0 = l[0], l1 = l[1];
   if (threadIdx.x == 0 && losses) {
     losses[0] = (float)(l0 / B);
     losses[1] = (float)(l1 / B);
@@ -120,11 +150,12 @@ __global__ void k_finalize_critic(const float* part, int ntiles, int B, float* l
 
 // Actor losses (sac_acm.py:77-86) and the temperature-gradient operand
 // c = mean(-logpi - H) (sac.py:214-216), written for an optional all-reduce.
-__global__ void k_actor_partials(const float* part, int ntiles, int B, int aout, float custom_loss,
-                                 double target_entropy, float* alpha_grad, float* losses) {
-  const double ssac = block_sum(part, ntiles, 8, 2);
-  const double sdist = block_sum(part, ntiles, 8, 3);
-  const double slp = block_sum(part, ntiles, 8, 4);
+__global__ __launch_bounds__(kFinThreads) void k_actor_partials(const float* part, int ntiles, int B, int aout,
+                                                               float custom_loss, double target_entropy,
+                                                               float* alpha_grad, float* losses) {
+  double v[3];
+  block_sums<3>(part, ntiles, 8, 2, v);
+  const double ssac = v[0], sdist = v[1], slp = v[2];
   if (threadIdx.x != 0) return;
   const double sac = ssac / B;
   const double dist = sdist / ((double)B * aout);
@@ -167,14 +198,18 @@ __global__ void k_finalize_acm(const float* part, int ntiles, int B, int ac, flo
 }
 
 // DDPG_AcM losses {critic, actor, ddpg, dist} (ddpg_acm.py:133-143, :181)
-__global__ void k_finalize_ddpg_critic(const float* part, int ntiles, int B, float* losses) {
-  const double l0 = block_sum(part, ntiles, 8, 0);
+__global__ __launch_bounds__(kFinThreads) void k_finalize_ddpg_critic(const float* part, int ntiles, int B,
+                                                                     float* losses) {
+  double v[1];
+  block_sums<1>(part, ntiles, 8, 0, v);
+  const double l0 = v[0];
   if (threadIdx.x == 0 && losses) losses[0] = (float)(l0 / B);
 }
-__global__ void k_finalize_ddpg_actor(const float* part, int ntiles, int B, int aout, float custom_loss,
-                                      float* losses) {
-  const double sq = block_sum(part, ntiles, 8, 2);
-  const double sd = block_sum(part, ntiles, 8, 3);
+__global__ __launch_bounds__(kFinThreads) void k_finalize_ddpg_actor(const float* part, int ntiles, int B, int aout,
+                                                                    float custom_loss, float* losses) {
+  double v[2];
+  block_sums<2>(part, ntiles, 8, 2, v);
+  const double sq = v[0], sd = v[1];
   if (threadIdx.x != 0 || !losses) return;
   const double ddpg = sq / B, dist = sd / ((double)B * aout);
   losses[1] = (float)(custom_loss != 0.f ? ddpg + (double)custom_loss * dist : ddpg);

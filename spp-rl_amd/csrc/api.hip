@@ -1516,10 +1516,11 @@ sppStatus sppAgentBindAlphaGrad(sppAgentHandle a, float* g) {
 sppStatus sppSacAcmDrawEps(sppAgentHandle a, uint64_t seed, uint64_t counter, void* stream) {
   SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "no staged batch");
   const int B = a->cur_B, Bp = (int)round_up(B, 32);
-  const int64_t pairs = ((int64_t)a->cfg.aout * Bp + 1) / 2;
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, S(stream), a->EPS1, a->cfg.aout, B, Bp, seed,
+  SPP_REQUIRE((int64_t)a->cfg.aout * Bp < ((int64_t)1 << 31), SPP_E_SHAPE, "draw_eps: aout * Bp >= 2^31");
+  const int64_t quads = (int64_t)a->cfg.aout * Bp / 4;
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(quads, 256)), dim3(256), 0, S(stream), a->EPS1, a->cfg.aout, B, Bp, seed,
                      2 * counter);
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(pairs, 256)), dim3(256), 0, S(stream), a->EPS2, a->cfg.aout, B, Bp, seed,
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(quads, 256)), dim3(256), 0, S(stream), a->EPS2, a->cfg.aout, B, Bp, seed,
                      2 * counter + 1);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;

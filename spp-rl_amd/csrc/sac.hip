@@ -1227,17 +1227,29 @@ __global__ void k_eps_read_fm(const float* E, float* eps, int aout, int B, int B
 }
 
 // Device-side Gaussian eps straight into the feature-major layout (zero padded).
+// Box-Muller with the hardware transcendentals (v_log_f32, v_sqrt_f32, v_sin/cos_f32 of 2 pi v in
+// revolutions): the policy noise needs the N(0, 1) law, not libm-exact values.
+__device__ __forceinline__ void box_muller_hw(uint32_t a, uint32_t b, float& n0, float& n1) {
+  const float u = u01(a), v = u01(b);
+  const float r = __builtin_amdgcn_sqrtf(-2.f * 0.69314718055994531f * __builtin_amdgcn_logf(u));
+  n0 = r * __builtin_amdgcn_cosf(v);
+  n1 = r * __builtin_amdgcn_sinf(v);
+}
+// eps [aout][Bp] (padding columns b >= B zero): one philox block -> 4 normals -> one 16-B store
+// (Bp is a multiple of 32, so a quad never crosses a row).
 __global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint64_t ctr) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pair index
-  const int64_t n = (int64_t)aout * Bp;
-  if (2 * i >= n) return;
-  u32x4 r = philox(seed, ctr, (uint64_t)i);
-  float n0, n1;
-  box_muller(r.x, r.y, n0, n1);
-  for (int k = 0; k < 2; ++k) {
-    const int64_t idx = 2 * i + k;
-    if (idx < n) E[idx] = ((idx % Bp) < B) ? (k ? n1 : n0) : 0.f;
-  }
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // quad index; aout * Bp < 2^31 (host check)
+  if (4 * i >= aout * Bp) return;
+  const u32x4 r = philox(seed, ctr, (uint64_t)i);
+  float4 v;
+  box_muller_hw(r.x, r.y, v.x, v.y);
+  box_muller_hw(r.z, r.w, v.z, v.w);
+  const int col = (4 * i) % Bp;
+  v.x = col < B ? v.x : 0.f;
+  v.y = col + 1 < B ? v.y : 0.f;
+  v.z = col + 2 < B ? v.z : 0.f;
+  v.w = col + 3 < B ? v.w : 0.f;
+  *reinterpret_cast<float4*>(E + 4 * (int64_t)i) = v;
 }
 
 #endif  // SPP_KSET_TU

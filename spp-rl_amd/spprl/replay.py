@@ -115,6 +115,7 @@ class BufferAcMOffPolicy:
 
     def reset_idx(self):
         call("sppReplayReset", self._h)
+        self._gen = getattr(self, "_gen", 0) + 1
 
     def view(self):
         v = _lib.ReplayView()
@@ -151,6 +152,7 @@ class BufferAcMOffPolicy:
         e = self._dev(end, torch.uint8).reshape(E)
         call("sppReplayAddStep", self._h, prev.ctypes.data_as(ctypes.c_void_p), nxt.ctypes.data_as(ctypes.c_void_p),
              E, ptr(act), ptr(acm), ptr(r), ptr(d), ptr(e), stream_handle())
+        self._gen = getattr(self, "_gen", 0) + 1  # timestep writes so far (the DP stats' row-count cache key)
 
     def add_timestep(self, obs_idx, next_obs_idx, action, rew, done, end):
         """add_timestep (:65-75) + ReplayBuffer.addition (:133-137)"""
@@ -214,11 +216,17 @@ class BufferAcMOffPolicy:
         §8e): ``allreduce_sum(t)`` sums a device tensor in place across ranks (RCCL).  Exact
         global percentiles (radix select on all-reduced histograms); mean / std from fp64
         sums about the replicated current mean.  ``n_global`` (total live rows) may be given
-        when known on the host; otherwise it is all-reduced (one host sync)."""
+        when known on the host; otherwise it is all-reduced (one host sync) once per change of the
+        shards: the ranks write timesteps in lockstep, so the count of timestep writes is the same on
+        every rank and all of them reuse the cached total between writes (the bench's reference-rate
+        stats run several passes per vector step on unchanged shards)."""
         if n_global is None:
-            n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
-            allreduce_sum(n)
-            n_global = int(n.item())
+            gen = getattr(self, "_gen", 0)
+            if getattr(self, "_ng_gen", None) != gen:
+                n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
+                allreduce_sum(n)
+                self._ng, self._ng_gen = int(n.item()), gen
+            n_global = self._ng
         if n_global <= 10:  # replay_buffer.py:84, on the global buffer
             return
         if getattr(self, "_dp_hist", None) is None:

@@ -271,36 +271,6 @@ __device__ __forceinline__ void dense_impl(const float4* __restrict__ Wf, int NB
     });
     return acc;
   };
-#ifdef SPP_PREFETCH_ALL  // experiment (round-1 "all fragments up front"): every output block's chunks issued first
-  if constexpr (NQ <= 4) {
-    float4 all[8][NQ];
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob)
-      if (ob < NBO)
-        static_for<0, NQ>([&](auto Q) {
-          constexpr int q = Q;
-          all[ob][q] = wfrag(wr, l16, ob * OBSTRIDE + (q_ib(RV, NBI, q) * 4 + q_rq(RV, NBI, q)) * 1024);
-        });
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-      if (ob >= NBO) break;
-      f32x16 acc;
-      if constexpr (BIAS) acc = bias_tile(biasL, ob, h);
-      else acc = zero16();
-      static_for<0, NQ>([&](auto Q) {
-        constexpr int q = Q;
-        constexpr int ib = q_ib(RV, NBI, q);
-        constexpr int rq = q_rq(RV, NBI, q);
-        acc = mfma(all[ob][q].x, in[ib][4 * rq + 0], acc);
-        acc = mfma(all[ob][q].y, in[ib][4 * rq + 1], acc);
-        acc = mfma(all[ob][q].z, in[ib][4 * rq + 2], acc);
-        acc = mfma(all[ob][q].w, in[ib][4 * rq + 3], acc);
-      });
-      epi(ob, acc);
-    }
-    return;
-  }
-#endif
   SPP_TPD(23);
   f32x16 prev = chain(0);
 #pragma unroll 1

@@ -265,3 +265,40 @@ def test_rand_streams_do_not_alias():
     x, y = a.cpu().numpy(), b.cpu().numpy()
     assert abs(np.corrcoef(x, y)[0, 1]) < 6 / np.sqrt(n)
     assert not np.any(x == y)
+
+
+@pytest.mark.parametrize("B", [1000, 65536])
+def test_draw_eps_ragged_batch_law_and_determinism(B):
+    """sppSacAcmDrawEps (k_eps_fm: 4 normals per philox block, hardware Box-Muller) on a batch whose
+    padded width Bp is not B: standard normal law over the valid samples (moments, KS), the same
+    (seed, counter) reproduces the draws bit for bit, EPS1 / EPS2 and the next counter are unrelated."""
+    from scipy import stats
+
+    ob = 11
+    rng = np.random.RandomState(3)
+    ag = spprl.SAC_AcM(env_name="Hopper-v2", max_batch=B, buffer_size=5000, device=DEV, seed=0)
+    rb = _filled(ag, rng, 4000, ob, 3)
+    st = _lib.stream_handle()
+    idx = torch.randint(0, len(rb), (B,), device=DEV)
+    _lib.call("sppAgentStageFromReplay", ag._h, rb._h, _lib.ptr(idx), B, st)
+
+    def draw(counter):
+        _lib.call("sppSacAcmDrawEps", ag._h, 91, counter, st)
+        out = [torch.empty(B, ob, device=DEV) for _ in range(2)]
+        for w in (0, 1):
+            _lib.call("sppAgentReadEps", ag._h, w, _lib.ptr(out[w]), st)
+        torch.cuda.synchronize()
+        return [o.cpu().numpy().astype(np.float64) for o in out]
+
+    e1, e2 = draw(7)
+    r1, r2 = draw(7)
+    n1, _ = draw(8)
+    assert np.array_equal(e1, r1) and np.array_equal(e2, r2)
+    for e in (e1, e2):
+        x = e.ravel()
+        n = x.size
+        assert np.isfinite(x).all() and np.abs(x).max() < 7.0
+        assert abs(x.mean()) < 6 / np.sqrt(n) and abs(x.var() - 1) < 6 * np.sqrt(2.0 / n)
+        assert stats.kstest(x, "norm").pvalue > 1e-4
+    for a, b in ((e1, e2), (e1, n1)):
+        assert abs(np.corrcoef(a.ravel(), b.ravel())[0, 1]) < 6 / np.sqrt(a.size)

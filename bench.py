@@ -452,7 +452,9 @@ def main():
     backend = os.environ.get("SPP_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # SPP_DP_FORCE=1 (rehearsal): the process group and the exchange also run with one rank
+    distributed = world > 1 or os.environ.get("SPP_DP_FORCE", "0") == "1"
+    if distributed:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

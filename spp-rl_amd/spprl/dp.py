@@ -9,7 +9,16 @@ stay bit-identical.  With equal shard batches the average of per-rank mean-loss
 gradients equals the full-batch mean-loss gradient (all losses of the path are
 batch means: sac_acm.py:97-131, :60-87, sac.py:201-216, acm.py:356-372).
 """
+import os
+
 import torch.distributed as dist
+
+
+def _single_rank_exchange():
+    """SPP_DP_FORCE=1 keeps the exchange on with a one-rank group: the RCCL path (bucket
+    all-reduce, the stepwise global obs statistics) then runs on a single GPU, which is how it
+    is rehearsed on a one-GPU box (tests/test_gpu_dp_rccl.py).  Results equal the N = 1 path."""
+    return os.environ.get("SPP_DP_FORCE", "0") == "1"
 
 
 def make_allreduce(group=None):
@@ -18,7 +27,7 @@ def make_allreduce(group=None):
     if not dist.is_available() or not dist.is_initialized():
         return None
     world = dist.get_world_size(group)
-    if world == 1:
+    if world == 1 and not _single_rank_exchange():
         return None
     inv = 1.0 / world
 
@@ -32,7 +41,9 @@ def make_allreduce(group=None):
 def make_allreduce_sum(group=None):
     """Returns ``allreduce_sum(t)`` (in-place sum over the group; exact for integer
     histograms, fp64 for moment sums) or None with a single rank."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    if dist.get_world_size(group) == 1 and not _single_rank_exchange():
         return None
 
     def allreduce_sum(t):

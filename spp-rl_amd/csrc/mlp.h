@@ -559,20 +559,29 @@ __device__ __forceinline__ int soff(int row, int ld4) {
 __device__ __forceinline__ float fm_ld(rsrc_t r, int row, int ld4, uint32_t vo) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, soff(row, ld4), 0));
 }
+// Cache policy of the weight-gradient operand stores (activations / deltas that only k_dw reads
+// back, in a later launch): SPP_OPST_AUX is the buffer instruction's cache-policy operand.
+#ifndef SPP_OPST_AUX
+#define SPP_OPST_AUX 0
+#endif
 __device__ __forceinline__ void fm_st(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, soff(row, ld4), 0);
+}
+__device__ __forceinline__ void fm_st_op(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, soff(row, ld4), SPP_OPST_AUX);
 }
 // bf16 2-D array [rows][ld] addressed with the fp32 array's (row, ld4, vo): byte offsets halved.
 // RNE conversion, the same one the bf16 MFMA operand packs use.
 __device__ __forceinline__ void fm_st16(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
   const __bf16 b = (__bf16)v;
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, b), r, vo >> 1, soff(row, ld4 >> 1), 0);
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, b), r, vo >> 1, soff(row, ld4 >> 1),
+                                        SPP_OPST_AUX);
 }
 // weight-gradient operand store: bf16 kernel sets write the activations / deltas k_dw reads as bf16
 template <bool BF>
 __device__ __forceinline__ void op_st(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
   if constexpr (BF) fm_st16(r, row, ld4, vo, v);
-  else fm_st(r, row, ld4, vo, v);
+  else fm_st_op(r, row, ld4, vo, v);
 }
 __device__ __forceinline__ float fm_ldb(rsrc_t r, int row, int ld4, uint32_t vo) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + (uint32_t)soff(row, ld4), 0, 0));

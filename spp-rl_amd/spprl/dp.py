@@ -52,6 +52,36 @@ def make_allreduce_sum(group=None):
     return allreduce_sum
 
 
+_HOST_GROUP = None
+
+
+def make_host_allreduce_sum(group=None):
+    """Returns ``host_sum(x) -> int`` (sum of a host integer over the group) or None with a
+    single rank.  Host-known counts (the shards' live row counts) are exchanged as CPU tensors over
+    gloo: no device tensor, so no device synchronisation on the way.  With an RCCL default group
+    a gloo group over the same ranks is created once; every rank must call this in the same order
+    (the agents' constructors do)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    if dist.get_world_size(group) == 1 and not _single_rank_exchange():
+        return None
+    import torch
+
+    global _HOST_GROUP
+    g = group
+    if dist.get_backend(group) != "gloo":
+        if _HOST_GROUP is None:
+            _HOST_GROUP = dist.new_group(backend="gloo")
+        g = _HOST_GROUP
+
+    def host_sum(x):
+        t = torch.tensor([int(x)], dtype=torch.int64)
+        dist.all_reduce(t, group=g)
+        return int(t.item())
+
+    return host_sum
+
+
 def stream_key(seed, tag):
     """Philox key of one random-stream consumer (policy eps, replay indices, update eps, env
     resets, env actions): splitmix64 of (seed, tag), so consumers sharing a seed never share

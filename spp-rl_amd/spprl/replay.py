@@ -211,21 +211,28 @@ class BufferAcMOffPolicy:
              ptr(self.min_obs), 0 if self._have_minmax else 1, stream_handle())
         self._have_minmax = True
 
-    def update_obs_mean_std_dp(self, allreduce_sum, n_global=None):
+    def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None):
         """update_obs_mean_std over the union of the data-parallel ranks' shards (SURVEY.md
         §8e): ``allreduce_sum(t)`` sums a device tensor in place across ranks (RCCL).  Exact
         global percentiles (radix select on all-reduced histograms); mean / std from fp64
         sums about the replicated current mean.  ``n_global`` (total live rows) may be given
-        when known on the host; otherwise it is all-reduced (one host sync) once per change of the
-        shards: the ranks write timesteps in lockstep, so the count of timestep writes is the same on
-        every rank and all of them reuse the cached total between writes (the bench's reference-rate
-        stats run several passes per vector step on unchanged shards)."""
+        when known on the host; otherwise the shard lengths (host bookkeeping) are summed once per
+        change of the shards: through ``host_sum`` (a gloo exchange of host integers, no device
+        synchronisation, spprl.dp.make_host_allreduce_sum) when given, else as a device tensor
+        through ``allreduce_sum`` (one host sync).  The ranks write timesteps in lockstep, so the
+        count of timestep writes is the same on every rank and all of them reuse the cached total
+        between writes (the bench's reference-rate stats run several passes per vector step on
+        unchanged shards)."""
         if n_global is None:
             gen = getattr(self, "_gen", 0)
             if getattr(self, "_ng_gen", None) != gen:
-                n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
-                allreduce_sum(n)
-                self._ng, self._ng_gen = int(n.item()), gen
+                if host_sum is not None:
+                    ng = host_sum(len(self))
+                else:
+                    n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
+                    allreduce_sum(n)
+                    ng = int(n.item())
+                self._ng, self._ng_gen = ng, gen
             n_global = self._ng
         if n_global <= 10:  # replay_buffer.py:84, on the global buffer
             return

@@ -39,7 +39,7 @@ import torch
 
 from . import config
 from ._lib import call, ptr, stream_handle
-from .dp import make_allreduce, make_allreduce_sum, stream_key
+from .dp import make_allreduce, make_allreduce_sum, make_host_allreduce_sum, stream_key
 
 # ---------------------------------------------------------------- stats
 
@@ -342,6 +342,7 @@ class OffPolicyLoop:
             raise ValueError("schedule must be 'reference' or 'fused'")
         self.allreduce = allreduce if allreduce is not None else make_allreduce()
         self.allreduce_sum = make_allreduce_sum() if self.allreduce is not None else None
+        self.host_sum = make_host_allreduce_sum() if self.allreduce is not None else None
         self.loop_seed = int(loop_seed)
         # one Philox key per random-stream consumer (never a shared (key, counter) pair)
         self._key_policy, self._key_index = stream_key(loop_seed, "policy"), stream_key(loop_seed, "index")
@@ -430,7 +431,8 @@ class OffPolicyLoop:
         if self.allreduce_sum is not None:
             # shard lengths differ across ranks once resets (early terminations) advance the
             # obs rings unevenly: the global row count is all-reduced, never assumed
-            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum)
+            # (counted on the host and exchanged over gloo: no device synchronisation per step)
+            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, host_sum=self.host_sum)
         else:
             self.replay_buffer.update_obs_mean_std()
 

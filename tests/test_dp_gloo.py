@@ -243,3 +243,37 @@ def test_dp_ppo_actor_exchange_gloo():
         np.testing.assert_array_equal(res[r][1], res[0][1])  # replicas agree
         assert np.abs(res[r][1] - g).max() <= 1e-5 * np.abs(g).max()
         np.testing.assert_allclose(res[r][2], [out["actor"], out["kl"]], rtol=1e-5, atol=1e-6)
+
+
+def _host_sum_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from spprl.dp import make_host_allreduce_sum
+
+        hs = make_host_allreduce_sum()
+        # unequal shard lengths (resets advance the rings unevenly): the sum, on every rank
+        q.put((rank, hs(1000 + 37 * rank), hs(2 ** 33 + rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_row_count_exchange_gloo():
+    """The DP obs statistics' global row count: host integers summed over the ranks (int64,
+    no device tensor), identical on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_sum_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(60)
+    for r in range(2):
+        assert res[r] == (2037, 2 ** 34 + 1)
+
+
+def test_make_host_allreduce_sum_single_process_is_none():
+    from spprl.dp import make_host_allreduce_sum
+    assert make_host_allreduce_sum() is None

@@ -65,6 +65,16 @@ __device__ __forceinline__ float sum_bf8(const float4& a) {
 }
 
 // ABF / XBF: the A / X operand rows are bf16 (BF only); row pointers are then __bf16* cast to float*.
+// Operand loads: each operand byte is read once per launch; SPP_DW_LD_NT selects nt loads.
+__device__ __forceinline__ float4 dw_ld(const float* p) {
+#ifdef SPP_DW_LD_NT
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p)));
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+
 template <int NI, int NJ, bool DB, bool BF = false, bool ABF = false, bool XBF = false>
 __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
                                         f32x16 (&acc)[4][4], float (&bs)[4]) {
@@ -78,18 +88,18 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
     constexpr int sl = decltype(SL)::value;
     static_for<0, NI>([&](auto I) {
       if constexpr (ABF) {
-        ra[sl][I][0] = *reinterpret_cast<const float4*>(reinterpret_cast<const __bf16*>(a0[I]) + 16 * t);
+        ra[sl][I][0] = dw_ld(reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(a0[I]) + 16 * t));
       } else {
-        ra[sl][I][0] = *reinterpret_cast<const float4*>(a0[I] + 16 * t);
-        ra[sl][I][1] = *reinterpret_cast<const float4*>(a0[I] + 16 * t + 4);
+        ra[sl][I][0] = dw_ld(a0[I] + 16 * t);
+        ra[sl][I][1] = dw_ld(a0[I] + 16 * t + 4);
       }
     });
     static_for<0, NJ>([&](auto J) {
       if constexpr (XBF) {
-        rx[sl][J][0] = *reinterpret_cast<const float4*>(reinterpret_cast<const __bf16*>(x0[J]) + 16 * t);
+        rx[sl][J][0] = dw_ld(reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(x0[J]) + 16 * t));
       } else {
-        rx[sl][J][0] = *reinterpret_cast<const float4*>(x0[J] + 16 * t);
-        rx[sl][J][1] = *reinterpret_cast<const float4*>(x0[J] + 16 * t + 4);
+        rx[sl][J][0] = dw_ld(x0[J] + 16 * t);
+        rx[sl][J][1] = dw_ld(x0[J] + 16 * t + 4);
       }
     });
   };

@@ -529,6 +529,18 @@ __device__ __forceinline__ void dense_lds(const float4* __restrict__ Wf, const f
 
 // ---------------------------------------------------------------- loaders / stores
 
+// Cache policy of the weight-gradient operand stores (activations / deltas that only k_dw reads
+// back, in a later launch): SPP_OPST_AUX is the buffer instruction's cache-policy operand.
+// 2 = nt: measured (profiles/r02/ab_nt.txt) the default policy's lines of this write stream
+// evict weight fragments the other waves of the XCD re-read from L2 (critic phase 1.6-2.8 % faster).
+#ifndef SPP_OPST_AUX
+#define SPP_OPST_AUX 2
+#endif
+// cache policy of the feature-major streaming loads (staged minibatch, eps, scratch re-reads)
+#ifndef SPP_STREAM_LD_AUX
+#define SPP_STREAM_LD_AUX 0
+#endif
+
 // Feature-major arrays X[f][ld] are addressed as X[urow*ld + loff] with the
 // wave-uniform row urow = 32*ib + ru(r) and ONE 32-bit per-lane offset
 // loff = 4*h*ld + b (kept in a single VGPR; Bp*256 < 2^31 is asserted on the host).
@@ -557,13 +569,8 @@ __device__ __forceinline__ int soff(int row, int ld4) {
   return so;
 }
 __device__ __forceinline__ float fm_ld(rsrc_t r, int row, int ld4, uint32_t vo) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, soff(row, ld4), 0));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, soff(row, ld4), SPP_STREAM_LD_AUX));
 }
-// Cache policy of the weight-gradient operand stores (activations / deltas that only k_dw reads
-// back, in a later launch): SPP_OPST_AUX is the buffer instruction's cache-policy operand.
-#ifndef SPP_OPST_AUX
-#define SPP_OPST_AUX 0
-#endif
 __device__ __forceinline__ void fm_st(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, soff(row, ld4), 0);
 }
@@ -584,7 +591,8 @@ __device__ __forceinline__ void op_st(rsrc_t r, int row, int ld4, uint32_t vo, f
   else fm_st_op(r, row, ld4, vo, v);
 }
 __device__ __forceinline__ float fm_ldb(rsrc_t r, int row, int ld4, uint32_t vo) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + (uint32_t)soff(row, ld4), 0, 0));
+  return __builtin_bit_cast(float,
+                            __builtin_amdgcn_raw_buffer_load_b32(r, vo + (uint32_t)soff(row, ld4), 0, SPP_STREAM_LD_AUX));
 }
 __device__ __forceinline__ void fm_stb(rsrc_t r, int row, int ld4, uint32_t vo, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo + (uint32_t)soff(row, ld4), 0, 0);

@@ -404,21 +404,24 @@ static void stats_pass1(sppReplayHandle h, uint32_t* hist, const float* pivot, h
   hipLaunchKernelGGL(k_stats_p1, dim3(kStatsBlocks), dim3(256), lds1, st, h->d, h->len, hist, h->st_part, pivot);
 }
 
-// digit pass p (0-based) after the top byte: 6-bit digits at bits 18, 12, 6, 0, all columns
-constexpr int kStatsPasses = 24 / kStatsDigit;
-static int stats_shift(int p) { return 24 - kStatsDigit * (p + 1); }
+// digit pass p (0-based) after the top byte, all columns: 8-bit digits at bits 16, 8, 0 when the
+// [ob][4][256] LDS histogram fits 128 KiB (ob <= 32), else 6-bit digits at bits 18, 12, 6, 0
+static int stats_dbits(sppReplayHandle h) { return h->d.ob <= 32 ? 8 : 6; }
+static int stats_npass(sppReplayHandle h) { return 24 / stats_dbits(h); }
+static int stats_shift(sppReplayHandle h, int p) { return 24 - stats_dbits(h) * (p + 1); }
 
 static void stats_pk(sppReplayHandle h, int p, uint32_t* hist, hipStream_t st) {
-  const size_t ldsk = sizeof(uint32_t) * h->d.ob * 4 * kStatsBins;
+  const size_t ldsk = sizeof(uint32_t) * h->d.ob * 4 * (1u << stats_dbits(h));
   const int resident = std::max(1, std::min(2, (int)((160 * 1024) / ldsk)));  // 1024-thread blocks per CU
   hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(kStatsPkThreads), ldsk, st, h->d, h->len,
-                     stats_shift(p), (const uint32_t*)h->st_state, hist);
+                     stats_shift(h, p), stats_dbits(h), (const uint32_t*)h->st_state, hist);
 }
 
 static void stats_sel(sppReplayHandle h, int p, uint32_t* hist, int64_t n, float* max_obs, float* min_obs,
                       int first_update, hipStream_t st) {
   hipLaunchKernelGGL(k_stats_sel, dim3(h->d.ob), dim3(256), 0, st, hist, kStatsBlocks, h->d.ob, 0, h->d.ob,
-                     stats_shift(p), 0, (const double*)nullptr, n, h->st_state, h->st_mean, max_obs, min_obs,
+                     stats_shift(h, p), stats_dbits(h), 0, (const double*)nullptr, n, h->st_state, h->st_mean,
+                     max_obs, min_obs,
                      first_update);
 }
 
@@ -492,7 +495,7 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot, d
   sppStatus s = stats_alloc(h);
   if (s) return s;
   hipStream_t st = S(stream);
-  const int npass = kStatsPasses;
+  const int npass = stats_npass(h);
   SPP_REQUIRE(step <= npass + 1, SPP_E_INVALID_ARG, "obs_stats_dp: step %d > %d", step, npass + 1);
   *done = 0;
   if (step == 0) {  // local pass 1 -> sums [ob][2] about the shared pivot, top-byte histogram
@@ -506,7 +509,7 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot, d
     }
   } else {
     if (step == 1) {  // global top byte + moments
-      hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, hist, 1, ob, 0, ob, 24, 1, (const double*)sums,
+      hipLaunchKernelGGL(k_stats_sel, dim3(ob), dim3(256), 0, st, hist, 1, ob, 0, ob, 24, 8, 1, (const double*)sums,
                          n_global, h->st_state, h->st_mean, max_obs, min_obs, first_update);
       hipLaunchKernelGGL(k_stats_moments_out, dim3(1), dim3(128), 0, st, h->d, (const double*)h->st_mean, mean, std,
                          pivot);

@@ -273,19 +273,19 @@ __global__ __launch_bounds__(256) void k_stats_p1(ReplayDev r, int64_t len, uint
   }
 }
 
-// Passes 2-5 (k_stats_pk): per-rank histograms of the next 6-bit digit (bits
-// [shift, shift+6), shift = 18, 12, 6, 0) among the rows matching each rank's prefix,
-// all columns in one read of the data: LDS [ob][4][64] (<= 128 KiB for ob <= 128).
+// Passes 2.. (k_stats_pk): per-rank histograms of the next dbits-bit digit (bits
+// [shift, shift+dbits)) among the rows matching each rank's prefix, all columns in one read of
+// the data: LDS [ob][4][1 << dbits].  dbits = 8 (shifts 16, 8, 0: 3 passes) while that fits
+// 128 KiB (ob <= 32), else 6 (shifts 18, 12, 6, 0: 4 passes, <= 128 KiB for ob <= 128).
 // 1024 threads (64 row lanes x 16 column lanes) keep enough loads in flight per CU.
-constexpr int kStatsDigit = 6;
-constexpr int kStatsBins = 1 << kStatsDigit;
 constexpr int kStatsPkThreads = 1024;
-__global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64_t len, int shift,
+__global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64_t len, int shift, int dbits,
                                                               const uint32_t* __restrict__ state,
                                                               uint32_t* __restrict__ ghist) {
-  extern __shared__ uint32_t shk[];  // [ob][4][kStatsBins]
+  extern __shared__ uint32_t shk[];  // [ob][4][1 << dbits]
   const int ob = r.ob;
-  const int nb = ob * 4 * kStatsBins;
+  const int bins = 1 << dbits;
+  const int nb = ob * 4 * bins;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) shk[i] = 0;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4, nty = blockDim.x >> 4;
   uint32_t pre[kStatsColsPerThread][4], msk[kStatsColsPerThread][4];
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             if ((kk[k] & msk[j][q]) == pre[j][q])
-              atomicAdd(&shk[(c * 4 + q) * kStatsBins + ((kk[k] >> shift) & (kStatsBins - 1))], 1u);
+              atomicAdd(&shk[(c * 4 + q) * bins + ((kk[k] >> shift) & (bins - 1))], 1u);
     }
   }
   __syncthreads();
@@ -330,13 +330,14 @@ __global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64
 // re-zeroes) the global histogram.  first: one shared [ob][256] histogram
 // (pass 1) and the moment partials are reduced too.
 __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist, int nblk, int ob, int col0,
-                                                   int ncols, int shift, int first, const double* __restrict__ part,
+                                                   int ncols, int shift, int dbits, int first,
+                                                   const double* __restrict__ part,
                                                    int64_t len, uint32_t* __restrict__ state, double* __restrict__ mom,
                                                    float* max_out, float* min_out, int first_update) {
   __shared__ uint32_t cnt[4][256];
   __shared__ double rd[2][256];
   const int c = col0 + blockIdx.x, t = threadIdx.x;
-  const int nbins = first ? 256 : kStatsBins;  // pass 1: top byte; later passes: 6-bit digits
+  const int nbins = first ? 256 : 1 << dbits;  // pass 1: top byte; later passes: dbits-bit digits
   for (int q = 0; q < (first ? 1 : 4); ++q) {
     if (t >= nbins) break;
     const int64_t off = first ? (int64_t)c * 256 + t : ((int64_t)blockIdx.x * 4 + q) * nbins + t;

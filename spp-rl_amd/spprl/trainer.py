@@ -432,7 +432,7 @@ class OffPolicyLoop:
             # shard lengths differ across ranks once resets (early terminations) advance the
             # obs rings unevenly: the global row count is all-reduced, never assumed
             # (counted on the host and exchanged over gloo: no device synchronisation per step)
-            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, host_sum=self.host_sum)
+            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, host_sum=getattr(self, "host_sum", None))
         else:
             self.replay_buffer.update_obs_mean_std()
 

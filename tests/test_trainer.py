@@ -294,14 +294,18 @@ def test_dp_obs_stats_count_is_all_reduced_not_assumed():
     calls = []
 
     class RB(_FakeRB):
-        def update_obs_mean_std_dp(self, allreduce_sum, n_global=None):
-            calls.append(n_global)
+        def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None):
+            calls.append((n_global, host_sum))
+
+    def host_sum(x):  # the shard lengths are summed on the host (spprl.dp.make_host_allreduce_sum)
+        return x
 
     ag = _FakeAgent(n_envs=4)
     ag.replay_buffer = RB()
     ag.allreduce_sum = lambda t: t
+    ag.host_sum = host_sum
     ag.update_obs_stats()
-    assert calls == [None]
+    assert calls == [(None, host_sum)]
 
 
 def test_stream_keys_are_distinct_per_consumer():

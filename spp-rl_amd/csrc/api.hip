@@ -406,7 +406,13 @@ static void stats_pass1(sppReplayHandle h, uint32_t* hist, const float* pivot, h
 
 // digit pass p (0-based) after the top byte, all columns: 8-bit digits at bits 16, 8, 0 when the
 // [ob][4][256] LDS histogram fits 128 KiB (ob <= 32), else 6-bit digits at bits 18, 12, 6, 0
-static int stats_dbits(sppReplayHandle h) { return h->d.ob <= 32 ? 8 : 6; }
+static int stats_dbits(sppReplayHandle h) {
+#ifdef SPP_STATS_DBITS6  // A/B build: 6-bit digits for every ob
+  return 6;
+#else
+  return h->d.ob <= 32 ? 8 : 6;
+#endif
+}
 static int stats_npass(sppReplayHandle h) { return 24 / stats_dbits(h); }
 static int stats_shift(sppReplayHandle h, int p) { return 24 - stats_dbits(h) * (p + 1); }
 

@@ -418,7 +418,11 @@ static int stats_shift(sppReplayHandle h, int p) { return 24 - stats_dbits(h) * 
 
 static void stats_pk(sppReplayHandle h, int p, uint32_t* hist, hipStream_t st) {
   const size_t ldsk = sizeof(uint32_t) * h->d.ob * 4 * (1u << stats_dbits(h));
-  const int resident = std::max(1, std::min(2, (int)((160 * 1024) / ldsk)));  // 1024-thread blocks per CU
+#ifndef SPP_STATS_PK_PER_CU
+#define SPP_STATS_PK_PER_CU 1
+#endif
+  // 1024-thread blocks per CU (each flushes its LDS histogram with device atomics at the end)
+  const int resident = std::max(1, std::min(SPP_STATS_PK_PER_CU, (int)((160 * 1024) / ldsk)));
   hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(kStatsPkThreads), ldsk, st, h->d, h->len,
                      stats_shift(h, p), stats_dbits(h), (const uint32_t*)h->st_state, hist);
 }

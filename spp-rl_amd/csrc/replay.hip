@@ -364,6 +364,12 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
       __syncthreads();
     }
   }
+  // Each rank's digit: the bin d with (counts below d) <= rank < (counts through d), found by an
+  // inclusive block scan of the histogram (one per rank after pass 1) instead of a serial walk.
+  __shared__ uint32_t pfx[4][256];
+  __shared__ uint32_t srank[4], sacc[4];
+  __shared__ int sbin[4];
+  const int nh = first ? 1 : 4;
   if (t < 4) {
     const int q = t;
     uint32_t* st = state + (c * 4 + q) * 3;
@@ -377,19 +383,38 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
     } else {
       rank = st[2];
     }
-    const uint32_t* h = cnt[first ? 0 : q];
-    uint32_t acc = 0;
-    int bin = nbins - 1;
-    for (int d = 0; d < nbins; ++d) {
-      if (acc + h[d] > rank) {
-        bin = d;
-        break;
+    srank[q] = rank;
+    sbin[q] = nbins - 1;  // rank past the total: last bin, everything below it counted
+  }
+  for (int q = 0; q < nh; ++q)
+    if (t < nbins) pfx[q][t] = cnt[q][t];
+  __syncthreads();
+  for (int o = 1; o < nbins; o <<= 1) {
+    uint32_t v[4];
+    for (int q = 0; q < nh; ++q) v[q] = (t < nbins && t >= o) ? pfx[q][t - o] : 0u;
+    __syncthreads();
+    for (int q = 0; q < nh; ++q)
+      if (t < nbins) pfx[q][t] += v[q];
+    __syncthreads();
+  }
+  if (t < 4) sacc[t] = pfx[first ? 0 : t][nbins - 1];
+  __syncthreads();
+  if (t < nbins) {
+    for (int q = 0; q < 4; ++q) {
+      const int hq = first ? 0 : q;
+      const uint32_t inc = pfx[hq][t], exc = inc - cnt[hq][t];
+      if (exc <= srank[q] && srank[q] < inc) {  // at most one bin per rank
+        sbin[q] = t;
+        sacc[q] = exc;
       }
-      acc += h[d];
     }
-    st[0] |= (uint32_t)bin << shift;
+  }
+  __syncthreads();
+  if (t < 4) {
+    uint32_t* st = state + (c * 4 + t) * 3;
+    st[0] |= (uint32_t)sbin[t] << shift;
     st[1] |= (uint32_t)(nbins - 1) << shift;
-    st[2] = rank - acc;
+    st[2] = srank[t] - sacc[t];
   }
   if (first && t == 0) {
     const double n = (double)len;

@@ -241,10 +241,17 @@ class BufferAcMOffPolicy:
             self._dp_hist = torch.zeros(hs, dtype=torch.int32, device=self.device)
             self._dp_sums = torch.zeros(self.obs_shape, 2, dtype=torch.float64, device=self.device)
             self._dp_pivot = torch.zeros(self.obs_shape, device=self.device)
+        ob = self.obs_shape
+        top = ob * 256  # step 0's histogram: the top byte of every column ([ob][256]; the rest is zero)
         for step in self.obs_stats_dp_steps(n_global):
             if step == 0:
-                allreduce_sum(self._dp_sums)
-            allreduce_sum(self._dp_hist)
+                # one collective for the fp64 moment sums and the top-byte counts (exact in fp64)
+                buf = torch.cat([self._dp_sums.reshape(-1), self._dp_hist[:top].to(torch.float64)])
+                allreduce_sum(buf)
+                self._dp_sums.copy_(buf[:2 * ob].view(ob, 2))
+                self._dp_hist[:top].copy_(buf[2 * ob:].to(torch.int32))
+            else:
+                allreduce_sum(self._dp_hist)
 
     def obs_stats_dp_steps(self, n_global):
         """Generator over the stepwise protocol: yields after each step whose outputs

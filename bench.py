@@ -102,6 +102,8 @@ def parse():
                     help="concurrent 1-thread reference-loop processes (default: the host's CPU share, max 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic null)")
+    ap.add_argument("--no-rocprof", action="store_true",
+                    help="skip the rocprofv3 --kernel-trace child run (roofline.frac_rocprof null)")
     ap.add_argument("--host-env", action="store_true",
                     help="step the envs on the host CPU (HostSynthEnv: vectorised numpy SynthEnv behind pinned "
                          "staging + side-stream copies, the update overlapping the host step): the PCIe-inclusive "
@@ -261,7 +263,7 @@ def pmc_traffic(args, E, cap, kernels):
         d = tempfile.mkdtemp(prefix="spp_pmc_", dir="/tmp")
         cmd = ["timeout", "-s", "KILL", "240", rp, "--pmc", c, "-d", d, "-o", "run", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--config", args.config, "--envs", str(E), "--buffer",
-               str(cap), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+               str(cap), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             return None, "rocprofv3 --pmc %s exit %d: %s" % (c, r.returncode, r.stdout[-300:])
@@ -286,6 +288,39 @@ def pmc_traffic(args, E, cap, kernels):
     return out, "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py --config %s " \
                 "--envs %d --steps 2 --warmup 1, same library (sha1 %s); bytes = 2*FETCH + WRITE per launch" % (
                     args.config, E, lib_digest())
+
+
+def rocprof_kernel_ms(args, E, cap, kname, steps=40, warmup=5):
+    """Average duration (ms) of ``kname`` over the timed launches of a child run of this script under
+    ``rocprofv3 --kernel-trace`` (same config, E, buffer and library): the kernel-trace view of the
+    roofline's launch time, next to the HIP-event average measured in the main run."""
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    import csv
+    import glob
+
+    env = dict(os.environ, TMPDIR="/tmp")
+    d = tempfile.mkdtemp(prefix="spp_kt_", dir="/tmp")
+    cmd = ["timeout", "-s", "KILL", "300", rp, "--kernel-trace", "-d", d, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--config", args.config, "--envs", str(E), "--buffer", str(cap),
+           "--steps", str(steps), "--warmup", str(warmup), "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
+    r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        return None, "rocprofv3 --kernel-trace exit %d: %s" % (r.returncode, r.stdout[-300:])
+    files = glob.glob(os.path.join(d, "**", "run_kernel_trace.csv"), recursive=True)
+    if not files:
+        return None, "no kernel trace csv"
+    rows = [row for row in csv.DictReader(open(files[0])) if kname in row["Kernel_Name"]]
+    shutil.rmtree(d, ignore_errors=True)
+    rows.sort(key=lambda row: int(row["Start_Timestamp"]))
+    dur = [(int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6 for row in rows]
+    timed = dur[-steps:] if len(dur) >= steps else dur
+    if not timed:
+        return None, "kernel %s not in the trace" % kname
+    return sum(timed) / len(timed), ("rocprofv3 --kernel-trace over bench.py --config %s --envs %d --steps %d "
+                                     "--warmup %d (library sha1 %s): mean of the last %d of %d launches" % (
+                                         args.config, E, steps, warmup, lib_digest(), len(timed), len(dur)))
 
 
 # ------------------------------------------------------------------ HBM-bound kernels
@@ -345,22 +380,35 @@ def bench_ppo(args, world, rank, dev):
     """configs[3]: SPP-PPO HalfCheetah-v2, 16384 envs over 8 GPUs = 2048 per GPU (train/spp_ppo_hcheetah.py
     hyper-parameters).  One step = one PPO_AcM iteration: T = 16 vector steps of rollout (actor sample,
     AcM, env, ACM ring writes), 10 x 10 full-batch critic steps, GAE over [T][E], <= 10 clip-loss epochs of
-    512-sample minibatches with the KL stop, the ACM regression (5 epochs of 64-sample batches over the
-    1.1e5 ring every 3 iterations), ring obs statistics."""
+    512-sample minibatches with the KL stop, the ACM regression, ring obs statistics.
+
+    ACM cadence (acm/on_policy.py:78-82, acm/acm.py:126-141, 266-303): the reference runs update_acm(5 epochs)
+    every 3 iterations of batch_size = 2000 frames over a ring of 1.1 * acm_pre_train_samples = 1.1e5 rows in
+    batches of 64: sigma = 5 * 1.1e5 / (3 * 2000) = 91.67 ACM samples per env-step.  An iteration here is
+    N = T * E frames, so every sample count of that cadence is scaled by s = N / 2000 (as the critic's full
+    batch already is): ring 1.1e5 * s rows, ACM batch 64 * s, still 5 epochs every 3 iterations -- the same
+    sigma, the same number of sequential ACM steps per cycle as the reference (5 * 1719), one sppAcmSgd launch
+    per epoch spread over ~s workgroups."""
     import spprl
     from spprl import flops
     from spprl.dp import shard_seed
 
     E = args.envs or 2048
     T = 16
+    N = T * E
+    ref_batch, ref_pretrain, ref_acm_bs, acm_epochs, acm_freq = 2000, 100_000, 64, 5, 3
+    scale = N / ref_batch
+    acm_bs = int(round(ref_acm_bs * scale))
+    pretrain = int(round(ref_pretrain * scale))
     seed = shard_seed(1000, rank)
-    ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=T * E,
+    ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=N,
                        ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
                        custom_loss=0.1, norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True,
-                       acm_epochs=5, acm_batch_size=64, acm_update_freq=3, acm_lr=3e-4,
-                       acm_pre_train_samples=100_000, n_envs=E, device=dev, seed=0, loop_seed=seed)
+                       acm_epochs=acm_epochs, acm_batch_size=acm_bs, acm_update_freq=acm_freq, acm_lr=3e-4,
+                       acm_pre_train_samples=pretrain, n_envs=E, device=dev, seed=0, loop_seed=seed)
     rb = ag.replay_buffer
     ob, ac = ag.ob_dim, ag.ac_dim
+    sigma = acm_epochs * rb.size / (acm_freq * N)
     torch.manual_seed(seed)
     fill = rb.size - 2 * E  # the ACM ring after pre-training (random env actions)
     prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
@@ -371,9 +419,13 @@ def bench_ppo(args, world, rank, dev):
                           torch.rand(fill, ac, device=dev) * 2 - 1)
     ag.acm.update_obs_stats()
     ag.iteration = 1
+    epochs = {"ppo": 0, "acm_updates": 0}
 
     def iteration():
+        acm_now = ag.acm_update_freq and ag.iteration % ag.acm_update_freq == 0
         ag.perform_iteration(sync=False)
+        epochs["ppo"] += ag.nets.last_epochs
+        epochs["acm_updates"] += int(bool(acm_now))
         ag.iteration += 1  # ACM update every acm_update_freq iterations (on_policy.py:66-70)
 
     for _ in range(args.warmup):
@@ -381,6 +433,7 @@ def bench_ppo(args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    epochs["ppo"], epochs["acm_updates"] = 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         iteration()
@@ -392,11 +445,14 @@ def bench_ppo(args, world, rank, dev):
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
-    value = world * T * E * args.steps / elapsed
+    value = world * N * args.steps / elapsed
     mac = flops.onpolicy_macs(ob, ob, ac)
-    N = T * E
-    # algorithmic work of one iteration's 100 full-batch critic steps on N = T*E samples
-    critic_flop = 2.0 * mac["critic_step"] * N * 100
+    # algorithmic work of the timed iterations: 100 full-batch critic steps on N samples, the PPO
+    # epochs actually run (KL stop) over N samples, acm_epochs epochs over the ring per ACM update, the rollout
+    acm_samples = epochs["acm_updates"] * acm_epochs * rb.size
+    flop = 2.0 * (args.steps * (mac["critic_step"] * N * 100 + (mac["A"] + mac["M"]) * N)
+                  + mac["actor_step"] * N * epochs["ppo"] + mac["acm_step"] * acm_samples)
+    per_env_step = flop / (args.steps * N)
     res = {"metric": "env-steps/sec (rollout+update) SPP-PPO HalfCheetah-v2", "value": round(value, 1),
            "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -405,14 +461,21 @@ def bench_ppo(args, world, rank, dev):
                    "networks, ACM ring pre-filled with N(0,1) transitions",
            "config": {"workload": "SPP-PPO HalfCheetah-v2, %d vectorized envs per GPU x %d steps per iteration "
                                   "(BASELINE.json configs[3] per-GPU shape)" % (E, T), "envs_per_gpu": E,
-                      "steps_per_iteration": T, "acm_ring": rb.size, "parallelism": "dp%d" % world},
+                      "steps_per_iteration": T, "frames_per_iteration": N, "cadence_scale": round(scale, 4),
+                      "acm_ring": rb.size, "acm_batch": acm_bs, "acm_epochs_every_3_iterations": acm_epochs,
+                      "acm_sigma": round(sigma, 3), "acm_updates_timed": epochs["acm_updates"],
+                      "ppo_epochs_timed": epochs["ppo"], "ppo_minibatch": 512,
+                      "flop_per_env_step": round(per_env_step), "parallelism": "dp%d" % world,
+                      "cadence": "reference train/spp_ppo_hcheetah.py per iteration with every sample count x "
+                                 "N/2000 (critic full batch N, ACM ring 1.1e5*s, ACM batch 64*s); sigma = ACM "
+                                 "samples per env-step (reference 91.67)"},
            "roofline": {"bound": "mfma", "kernel": "whole iteration (64-wide MLPs, latency-bound chain of "
                                                     "dependent optimizer steps)",
-                        "achieved": round(critic_flop / (elapsed / args.steps) / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS,
+                        "achieved": round(flop / elapsed / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": None, "traffic": None,
-                        "note": "achieved = the 100 full-batch critic steps' algorithmic FLOPs per iteration / "
-                                "iteration time; 1719 sequential 64-sample ACM SGD steps and ~64 sequential "
-                                "512-sample actor steps bound the iteration by latency, not by a roofline"},
+                        "note": "achieved = the timed iterations' algorithmic FLOPs (critic, actor epochs run, ACM, "
+                                "rollout: SURVEY §8d) / elapsed; 3 x 1719 sequential ACM steps per iteration and "
+                                "~64 sequential 512-sample actor steps per epoch bound the iteration by latency"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -618,6 +681,15 @@ def main():
         result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
     if world == 1:
         result["hbm_kernels"] = hbm_kernels(ag, cfg, B, E)
+    if rank == 0 and world == 1 and not args.no_rocprof:
+        kt_ms, kt_src = rocprof_kernel_ms(args, E, cap, kname)
+        rl = result["roofline"]
+        rl["avg_launch_ms_rocprof"] = round(kt_ms, 4) if kt_ms else None
+        rl["frac_rocprof"] = round(rl["flop_per_launch"] / (kt_ms * 1e-3) / 1e12 / peak, 5) if kt_ms else None
+        rl["rocprof_source"] = kt_src
+        rl["frac_note"] = ("frac = algorithmic FLOP per launch / HIP-event mean launch time in this run's timed "
+                           "region; frac_rocprof = the same FLOP / the rocprofv3 kernel-trace mean of the same "
+                           "kernel over a child run's timed launches")
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, src = pmc_traffic(args, E, cap, [kname, "k_stats_", "k_replay_stage_fm"])
         if traffic:

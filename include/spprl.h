@@ -212,6 +212,13 @@ sppStatus sppSacAcmDrawEps(sppAgentHandle h, uint64_t seed, uint64_t counter, vo
  * caller-owned row-major [B][aout] device buffer, so parity tests can replay the exact
  * device draws through the oracle. */
 sppStatus sppAgentReadEps(sppAgentHandle h, int which, float* out_dev, void* stream);
+/* Test hooks on the packed weight images the phase kernels read (no reference counterpart: the
+ * reference reads nn.Linear weights directly).  ImageCount: how many images hold parameters of
+ * `net`; UnpackImage: write image i back into a caller-owned device buffer laid out like the
+ * net's flat parameters (every position the image covers; the rest untouched).  bf16 agents:
+ * the values are the bf16 image entries, which must equal RNE(fp32 parameter) after each step. */
+sppStatus sppAgentImageCount(sppAgentHandle h, int net, int* n_out);
+sppStatus sppAgentUnpackImage(sppAgentHandle h, int net, int i, float* out_dev, void* stream);
 /* Fused replay sample + gather into the agent's staging area (device indices). */
 sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int B,
                                   void* stream);
@@ -262,11 +269,16 @@ sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
  * acm_cat, acm.py:260-264): x = [obs | next_obs] [B][2ob], y = acm action [B][ac]. */
 /* nsteps sequential AcM regression steps (acm.py:246-258 each: MSE + Adam at acm_lr) in ONE
  * launch: step k's batch = rows [k*bs, k*bs + bs) of x [nsteps*bs][2ob] / y [nsteps*bs][ac]
- * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 128.  Parameters stay in
+ * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 16384.  Parameters stay in
  * LDS, moments in registers (update_acm epochs, update_acm_batches).  loss_sum += sum of the
- * steps' batch losses.  AcM agents (SAC_AcM) only. */
+ * steps' batch losses.  AcM agents (SAC_AcM) only.  bs <= 128: one workgroup; larger batches
+ * spread each step over ceil(bs / 64) workgroups that sum the step's gradient in a fixed order
+ * (deterministic) behind one arrival barrier per step. */
 sppStatus sppAcmSgd(sppAgentHandle h, const float* x_dev, const float* y_dev, int nsteps, int bs, float* loss_sum,
                     void* stream);
+/* Synchronous: 1 if a multi-workgroup sppAcmSgd launch timed out waiting for its workgroups (its
+ * results are then invalid), else 0. */
+sppStatus sppAcmSgdStatus(sppAgentHandle h, int* timed_out_host);
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
 
 /* Per-kernel device timing (HIP events on the launch stream), for measurement:

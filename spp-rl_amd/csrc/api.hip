@@ -775,6 +775,9 @@ struct sppAgent {
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
   float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
+  // multi-workgroup AcM SGD (sppAcmSgd with bs > kSgdMaxBatch): gradient slabs, {counter, timeout flag}
+  DevArray<float> sgd_slab;
+  DevArray<int> sgd_sync;
   // per-kernel timing (HIP events on the launch stream)
   bool timing = false;
   std::vector<hipEvent_t> tev[5];
@@ -1549,6 +1552,32 @@ sppStatus sppAgentReadEps(sppAgentHandle a, int which, float* out, void* stream)
   return SPP_OK;
 }
 
+// The packed weight images that hold parameters of `net` (test access, see sppAgentUnpackImage).
+static std::vector<PackJob> images_of(sppAgent* a, int net) {
+  std::vector<PackJob> out;
+  const NetBufs& nb = a->net[net];
+  if (!nb.p) return out;
+  for (auto* l : {&a->pj_actor, &a->pj_acm, &a->pj_targ, &a->pj_critic_fwd})
+    for (const PackJob& j : *l)
+      if (j.W >= nb.p && j.W < nb.p + nb.n) out.push_back(j);
+  return out;
+}
+
+sppStatus sppAgentImageCount(sppAgentHandle a, int net, int* n) {
+  SPP_REQUIRE(a && n && net >= 0 && net < SPP_NET_COUNT, SPP_E_INVALID_ARG, "image_count: bad args");
+  *n = (int)images_of(a, net).size();
+  return SPP_OK;
+}
+
+sppStatus sppAgentUnpackImage(sppAgentHandle a, int net, int i, float* out, void* stream) {
+  SPP_REQUIRE(a && out && net >= 0 && net < SPP_NET_COUNT, SPP_E_INVALID_ARG, "unpack_image: bad args");
+  const std::vector<PackJob> js = images_of(a, net);
+  SPP_REQUIRE(i >= 0 && i < (int)js.size(), SPP_E_INVALID_ARG, "unpack_image: image %d of %d", i, (int)js.size());
+  hipLaunchKernelGGL(k_unpack_matrix, dim3(64), dim3(256), 0, S(stream), js[i], (const float*)a->net[net].p, out);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
 sppStatus sppAgentSetTiming(sppAgentHandle a, int enable) {
   SPP_REQUIRE(a, SPP_E_INVALID_ARG, "null");
   a->timing = enable != 0;
@@ -1753,21 +1782,50 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
                     void* stream) {
   SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
-  SPP_REQUIRE(bs <= kSgdMaxBatch, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kSgdMaxBatch);
+  SPP_REQUIRE(bs <= kSgdMaxBatch * kSgdMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kSgdMaxBatch * kSgdMaxWG);
   sppStatus s = check_ready(a);
   if (s) return s;
   if (nsteps == 0) return SPP_OK;
   const NetBufs& n = a->net[SPP_NET_ACM];
   SPP_REQUIRE(n.p && n.m && n.v, SPP_E_STATE, "acm_sgd: ACM buffers not bound");
-  AcmSgdArgs g{x, y, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout, loss_sum};
+  AcmSgdArgs g{x, y, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout, loss_sum,
+               bs, nullptr, nullptr, nullptr};
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
-  if (ob == 11 && ac == 3) hipLaunchKernelGGL((k_acm_sgd<22, 3, 256>), dim3(1), dim3(256), 0, st, g);
-  else if (ob == 17 && ac == 6) hipLaunchKernelGGL((k_acm_sgd<34, 6, 512>), dim3(1), dim3(512), 0, st, g);
-  else if (ob == 3 && ac == 1) hipLaunchKernelGGL((k_acm_sgd<6, 1, 512>), dim3(1), dim3(512), 0, st, g);
+  // batches past one workgroup's rows: ~64 rows per workgroup, gradients summed over the workgroups
+  int nwg = 1;
+  if (bs > kSgdMaxBatch) {
+    nwg = cdiv(bs, kSgdBigRows);
+    g.bsl = (int)round_up(cdiv(bs, nwg), 4);
+    nwg = cdiv(bs, g.bsl);
+    if (!a->sgd_slab.ptr) {
+      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)2 * kSgdMaxWG * kSlabStride));
+      SPP_CHECK_HIP(a->sgd_sync.alloc(2));  // {arrival counter, timeout flag}
+      SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, 2 * sizeof(int), st));
+    }
+    g.slab = a->sgd_slab.ptr;
+    g.ctr = a->sgd_sync.ptr;
+    g.err = a->sgd_sync.ptr + 1;
+    SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, sizeof(int), st));
+  }
+  const bool mw = nwg > 1;
+#define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                          \
+  if (mw) hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_, true>), dim3(nwg), dim3(TH_), 0, st, g); \
+  else hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_>), dim3(1), dim3(TH_), 0, st, g)
+  if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3, 256);
+  else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6, 512);
+  else if (ob == 3 && ac == 1) SPP_SGD_LAUNCH(6, 1, 512);
   else SPP_REQUIRE(false, SPP_E_SHAPE, "acm_sgd: no instantiation for ob=%d ac=%d", ob, ac);
+#undef SPP_SGD_LAUNCH
   a->steps[3] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppAcmSgdStatus(sppAgentHandle a, int* timed_out) {
+  SPP_REQUIRE(a && timed_out, SPP_E_INVALID_ARG, "acm_sgd_status: null");
+  *timed_out = 0;
+  if (a->sgd_sync.ptr) SPP_CHECK_HIP(hipMemcpy(timed_out, a->sgd_sync.ptr + 1, sizeof(int), hipMemcpyDeviceToHost));
   return SPP_OK;
 }
 

@@ -70,6 +70,43 @@ __global__ void k_pack_matrix(const PackJob* __restrict__ jobs) {
   }
 }
 
+// Inverse of k_pack_matrix for tests: every image element that carries a weight is written back
+// (as fp32) to its position in the flat parameter buffer starting at `base` (out[(src - base)]),
+// so the caller can compare an image with the fp32 parameters (bf16 images: with their RNE values).
+__global__ void k_unpack_matrix(PackJob J, const float* base, float* out) {
+  const int per = J.bf16 ? 2 : 4;  // k-steps (bf16, 8 values) / register quads (fp32, 4) per block pair
+  const int64_t total = (int64_t)J.NBO * J.NBI * per * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    int64_t rest = i >> 6;
+    const int sq = (int)(rest % per);
+    rest /= per;
+    const int ib = J.ibmajor ? (int)(rest / J.NBO) : (int)(rest % J.NBI);
+    const int ob = J.ibmajor ? (int)(rest % J.NBO) : (int)(rest / J.NBI);
+    int q, hh;
+    row_to_pos(lane & 31, q, hh);
+    const int n = map_index(J.out, ob, q, hh);
+    if (n < 0) continue;
+    const float4 raw = J.dst[i];
+    const int nv = J.bf16 ? 8 : 4;
+    for (int j = 0; j < nv; ++j) {
+      const int k = map_index(J.in, ib, nv * sq + j, lane >> 5);
+      if (k < 0) continue;
+      float x;
+      if (J.bf16) {
+        typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+        x = (float)__builtin_bit_cast(bf16x8_t, raw)[j];
+      } else {
+        x = j == 0 ? raw.x : (j == 1 ? raw.y : (j == 2 ? raw.z : raw.w));
+      }
+      const int row = J.trans ? k : n;
+      const int col = J.coff + (J.trans ? n : k);
+      const float* src = row < J.split ? J.W + (int64_t)row * J.ld : J.W2 + (int64_t)(row - J.split) * J.ld;
+      out[(src + col) - base] = x;
+    }
+  }
+}
+
 // One Adam step per element (+ optional polyak of the matching target element).
 __global__ void k_adam(const AdamJob* __restrict__ jobs, float neg_step, float bc2s, float tau) {
   const AdamJob J = jobs[blockIdx.y];

@@ -23,7 +23,10 @@
 namespace spp {
 
 constexpr int kSgdThreads = 256;
-constexpr int kSgdMaxBatch = 128;
+constexpr int kSgdMaxBatch = 128;   // rows per workgroup and step
+constexpr int kSgdMaxWG = 128;      // workgroups of the multi-workgroup form (batches up to 16,384)
+constexpr int kSlabStride = 5120;   // floats per workgroup slab: >= 16 * NT + 1 for every instantiation
+constexpr int kSgdBigRows = 64;     // target rows per workgroup of the multi-workgroup form
 
 struct AcmSgdArgs {
   const float* x;      // [nsteps * bs][IN] acm_cat inputs, consumed in order (sppReplayGatherAcm)
@@ -36,6 +39,13 @@ struct AcmSgdArgs {
   int64_t step0;       // Adam steps already taken
   const float* lim;    // [ac]
   float* loss_sum;     // += sum of the steps' batch losses (fp32 scalar)
+  // several workgroups per step (k_acm_sgd<.., true>, bs > kSgdMaxBatch): workgroup g takes rows
+  // [g*bsl, min((g+1)*bsl, bs)) of every step's batch; per-step gradient hand-over through slab
+  // [2][gridDim.x][kSlabStride] (step parity) and the arrival counter ctr (zeroed per launch)
+  int bsl;
+  float* slab;
+  int* ctr;
+  int* err;            // set to 1 if a step's arrival wait timed out (results then invalid)
 };
 
 template <int IN, int AC, int TH>
@@ -163,10 +173,44 @@ __device__ __forceinline__ void outer4x4(const float* A, int lda, const float* B
   }
 }
 
+// Arrival barrier of the multi-workgroup SGD (MI355X_MICROARCH.md "Valid forms": plain slab stores, every
+// storing wave's vmcnt(0), workgroup barrier, one lane's agent release, a relaxed counter add; the same
+// lane polls with relaxed loads, then one agent acquire before the workgroup reads other workgroups'
+// slabs).  The counter address is kept in a VGPR so the add and the polls are vector-memory operations.
+// Bounded: a wait that times out sets *err and every later wait of the launch returns at once.
+__device__ __forceinline__ void sgd_arrive_wait(int* ctr, int target, int* err, int* s_dead) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && !*s_dead) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    int* c = ctr + off;
+    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 22)) {
+        *s_dead = 1;
+        err[off] = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 // TH threads (a multiple of 64): 512 (two waves per SIMD) where the per-thread registers fit in 256.
-template <int IN, int AC, int TH>
+// MW: one step's batch spread over gridDim.x workgroups (rows g*bsl ...), per-step gradients summed
+// over the workgroups in a fixed order (every workgroup the same sum, so every workgroup applies the
+// identical Adam step and the parameter copies in their LDS stay identical: no broadcast needed).
+template <int IN, int AC, int TH, bool MW = false>
 __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
   using C = SgdCfg<IN, AC, TH>;
+  static_assert(16 * C::NT + 1 <= kSlabStride, "gradient slab");
   constexpr int I1P = C::I1P, H1P = C::H1P, H2P = C::H2P, ACP = C::ACP, MB = kSgdMaxBatch;
   __shared__ __attribute__((aligned(16))) float W1[64 * I1P];
   __shared__ __attribute__((aligned(16))) float W2[32 * H1P];
@@ -180,6 +224,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
   __shared__ float Y[MB * AC];
   __shared__ float lsum[TH / 64];
   __shared__ float adam_s[2][2];  // per step parity: -lr / (1 - b1^t), sqrt(1 - b2^t)
+  __shared__ int s_dead;
   // Adam's bias corrections of step st (torch.optim.Adam), computed once instead of by every thread
   auto adam_scalars = [&](int st) {
     const double tstep = (double)(a.step0 + st + 1);
@@ -187,13 +232,16 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     adam_s[st & 1][1] = (float)sqrt(1.0 - pow(0.999, tstep));
   };
   const int t = threadIdx.x;
-  const int bs = a.bs, bsp = (bs + 3) & ~3;
+  const int bsg = a.bs;                                  // the step's batch (all workgroups)
+  const int r0 = MW ? (int)blockIdx.x * a.bsl : 0;       // this workgroup's first row of it
+  const int bs = MW ? min(a.bsl, bsg - r0) : bsg, bsp = (bs + 3) & ~3;
+  if (t == 0) s_dead = 0;
   // register prefetch of one step's batch: x elements t, t + 256, ... of [bs][IN]; y likewise
   constexpr int NXP = (MB * IN + TH - 1) / TH, NYP = (MB * AC + TH - 1) / TH;
   float xp[NXP], yp[NYP];
   auto prefetch = [&](int st) {
-    const float* xs = a.x + (int64_t)st * bs * IN;
-    const float* ys = a.y + (int64_t)st * bs * AC;
+    const float* xs = a.x + ((int64_t)st * bsg + r0) * IN;
+    const float* ys = a.y + ((int64_t)st * bsg + r0) * AC;
 #pragma unroll
     for (int k = 0; k < NXP; ++k) {
       const int i = t + TH * k;
@@ -253,7 +301,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     }
   }
   float loss_acc = 0.f;
-  const float inv_n = 1.f / (float)(bs * AC);
+  const float inv_n = 1.f / (float)(bsg * AC);
   prefetch(0);
   if (t == 0) adam_scalars(0);
   __syncthreads();
@@ -339,11 +387,13 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     if ((t & 63) == 0) lsum[t >> 6] = lpart;
     __syncthreads();
     SPP_TP(3);
+    float ls_part = 0.f;  // MW: this workgroup's share, handed over with the gradients
     if (t == 0) {
       float ls = 0.f;
 #pragma unroll
       for (int w = 0; w < TH / 64; ++w) ls += lsum[w];
-      loss_acc += ls * inv_n;
+      if constexpr (MW) ls_part = ls;
+      else loss_acc += ls * inv_n;
     }
     // dz2 = (W3^T dz3) * (1 - h2^2), stored [b][32] and [32][b]
     for (int i = t; i < bsp * 32; i += TH) {
@@ -445,6 +495,46 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
         }
       }
     }
+    if constexpr (MW) {
+      // ---- sum the step's gradient over the workgroups (fixed order g = 0 .. G-1)
+      const int G = gridDim.x;
+      float* mine = a.slab + ((int64_t)(st & 1) * G + blockIdx.x) * kSlabStride;
+#pragma unroll
+      for (int k = 0; k < C::RT; ++k) {
+        const int q = sgd_own<C, TH>(t, k);
+        if (q >= 0)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<float4*>(mine + 16 * q + 4 * i) = make_float4(g[k][i][0], g[k][i][1], g[k][i][2], g[k][i][3]);
+      }
+      if (t == 0) mine[16 * C::NT] = ls_part;
+      sgd_arrive_wait(a.ctr, G * (st + 1), a.err, &s_dead);
+      const float* all = a.slab + (int64_t)(st & 1) * G * kSlabStride;
+#pragma unroll
+      for (int k = 0; k < C::RT; ++k) {
+        const int q = sgd_own<C, TH>(t, k);
+        if (q >= 0) {
+          float4 acc[4] = {};
+          for (int gg = 0; gg < G; ++gg) {
+            const float4* src = reinterpret_cast<const float4*>(all + (int64_t)gg * kSlabStride + 16 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float4 v = src[i];
+              acc[i].x += v.x; acc[i].y += v.y; acc[i].z += v.z; acc[i].w += v.w;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            g[k][i][0] = acc[i].x; g[k][i][1] = acc[i].y; g[k][i][2] = acc[i].z; g[k][i][3] = acc[i].w;
+          }
+        }
+      }
+      if (blockIdx.x == 0 && t == 0) {
+        float ls = 0.f;
+        for (int gg = 0; gg < G; ++gg) ls += all[(int64_t)gg * kSlabStride + 16 * C::NT];
+        loss_acc += ls * inv_n;
+      }
+    }
     // ---- Adam (torch.optim.Adam, same operation order as k_adam) on the owned tiles
     const float omb1 = 0.1f, b2 = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     __syncthreads();  // every thread has read the parameters it needs (dz1 used W2, dz2 used W3)
@@ -476,6 +566,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     SPP_TP(8);
   }
   SPP_TP_FLUSH();
+  if (MW && blockIdx.x != 0) return;  // every workgroup holds the same parameters and moments
   // ---- write back parameters and moments (canonical layout)
 #pragma unroll
   for (int k = 0; k < C::RT; ++k) {

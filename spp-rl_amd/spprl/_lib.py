@@ -100,6 +100,8 @@ _SIGS = {
     "sppAgentBindAlphaGrad": (c_int, [c_void_p, c_void_p]),
     "sppSacAcmDrawEps": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
     "sppAgentReadEps": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    "sppAgentImageCount": (c_int, [c_void_p, c_int, c_void_p]),
+    "sppAgentUnpackImage": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sppAcmRegressGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "sppAcmRegressApply": (c_int, [c_void_p, c_void_p]),
     "sppReplayGatherAcm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
@@ -140,6 +142,7 @@ _SIGS = {
     "sppAdvSums": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAdvNormalizeGlobal": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, n, bs
+    "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -159,10 +159,15 @@ class OnPolicyNets:
         N = obs.shape[0]
         kl, i = 0.0, 0
         sums = torch.zeros(4, device=self.device)
+        self.last_epochs = 0
         for i in range(self.max_ppo_epochs):
             if kl >= self.kl_div_threshold:
                 break
-            perm = torch.randperm(N, generator=generator).to(self.device)
+            self.last_epochs += 1
+            # a CPU generator (tests) keeps its host permutation; by default the permutation is drawn on the
+            # device (a host randperm + pageable copy would stall the stream every epoch)
+            perm = (torch.randperm(N, generator=generator).to(self.device) if generator is not None
+                    else torch.randperm(N, device=self.device))
             mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
             # one permuted copy per epoch: every minibatch is then a contiguous slice
             o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]

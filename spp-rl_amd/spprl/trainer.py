@@ -576,7 +576,7 @@ class OffPolicyLoop:
 
     def _acm_sgd_ok(self, bs):
         """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank."""
-        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 128
+        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 16384
                 and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1)))
 
     def _acm_sgd(self, idx, nsteps, bs):
@@ -607,11 +607,13 @@ class OffPolicyLoop:
         n = len(self.replay_buffer)
         if n == 0:
             return
-        g = torch.Generator(device="cpu").manual_seed(self.loop_seed * 7919 + self._next())
+        # epoch permutations drawn on the device (DataLoader(shuffle=True), acm.py:275): a host randperm and
+        # its pageable copy would hold the stream for every epoch of a large ring
+        g = torch.Generator(device=self.device).manual_seed(self.loop_seed * 7919 + self._next())
         for _ in range(epochs):
             lr = self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step)
             self._set_acm_lr(lr)
-            perm = torch.randperm(n, generator=g).to(self.device)
+            perm = torch.randperm(n, generator=g, device=self.device)
             self._acm_loss_acc.zero_()
             bs = self.acm_batch_size
             nb = -(-n // bs)

@@ -123,7 +123,7 @@ def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
         check_sac(ag, o, ol, grad_tol=2e-4, loss_tol=1e-4)
 
 
-@pytest.mark.parametrize("B", [65536, 409600])
+@pytest.mark.parametrize("B", [65536, 409600, 819200])  # 819,200 = rho * E: the ddpg_hcheetah bench batch
 def test_ddpg_acm_update_large_batch_matches_oracle(B):
     ob, ac = 17, 6
     rng = np.random.RandomState(B % 977)

@@ -370,12 +370,15 @@ def test_obs_stats_data_parallel_protocol_matches_union(ob, ranks):
     np.testing.assert_array_equal(union.min_obs.cpu().numpy(), np.percentile(allx, 1, axis=0).astype(np.float32))
 
 
-@pytest.mark.parametrize("env_name,ob,ac,bs", [("Hopper-v2", 11, 3, 100), ("HalfCheetah-v2", 17, 6, 64)])
+@pytest.mark.parametrize("env_name,ob,ac,bs", [("Hopper-v2", 11, 3, 100), ("HalfCheetah-v2", 17, 6, 64),
+                                               ("Hopper-v2", 11, 3, 700), ("HalfCheetah-v2", 17, 6, 1049)])
 def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     """sppAcmSgd (K sequential AcM regression steps in one launch, parameters in LDS) against
     the oracle's AcMTrainer.batch_update sequence on the same replay batches (acm.py:246-264):
     losses rtol 1e-4; parameters after K Adam steps within 1e-5 * max(1, |p|) except for a
-    few lr-sized flips of near-zero-moment coordinates."""
+    few lr-sized flips of near-zero-moment coordinates.  bs 700 / 1049 (the PPO bench's scaled
+    ACM batch) run the multi-workgroup form: each step over ceil(bs/64) workgroups whose gradients
+    are summed behind one arrival barrier per step (its timeout flag must stay clear)."""
     ag = _filled_agent(env_name, ob, ac, 2000, seed=4)
     rb = ag.replay_buffer
     params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}
@@ -400,6 +403,30 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     steps = np.zeros(4, np.int64)
     _lib.call("sppAgentGetSteps", ag._h, steps.ctypes.data_as(__import__("ctypes").c_void_p))
     assert steps[3] == K
+    flag = np.ones(1, np.int32)
+    _lib.call("sppAcmSgdStatus", ag._h, flag.ctypes.data)
+    assert flag[0] == 0
+
+
+def test_acm_multi_workgroup_sgd_is_deterministic():
+    """The multi-workgroup sppAcmSgd sums the workgroups' gradients in a fixed order: two agents with
+    the same initial AcM and the same batches end bit-identical (what lets data-parallel ranks run
+    the ACM epochs replicated, with no per-batch collective)."""
+    bs, K = 1049, 20
+    out = []
+    for _ in range(2):
+        ag = _filled_agent("HalfCheetah-v2", 17, 6, 4000, seed=9)
+        rb = ag.replay_buffer
+        idx = torch.from_numpy(np.random.RandomState(5).randint(0, 4000, K * bs)).to(DEV)
+        xg = torch.empty(K * bs, 34, device=DEV)
+        yg = torch.empty(K * bs, 6, device=DEV)
+        loss = torch.zeros(1, device=DEV)
+        _lib.call("sppReplayGatherAcm", rb._h, _lib.ptr(idx), K * bs, _lib.ptr(xg), _lib.ptr(yg),
+                  _lib.stream_handle())
+        _lib.call("sppAcmSgd", ag._h, _lib.ptr(xg), _lib.ptr(yg), K, bs, _lib.ptr(loss), _lib.stream_handle())
+        torch.cuda.synchronize()
+        out.append((ag.params[_lib.SPP_NET_ACM].cpu().clone(), float(loss.item())))
+    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
 
 
 @pytest.mark.parametrize("bs", [100, 160])
@@ -408,8 +435,8 @@ def test_update_acm_epochs_with_step_lr_match_oracle(bs, monkeypatch):
     live row in batches of acm_batch_size with a ragged last batch, StepLR(step 1, gamma 0.5) stepped
     once per epoch, loss['acm'] = the last epoch's mean batch loss.  The oracle replays the same
     permutations (recorded from the loop's torch.randperm) through AcMTrainer.batch_update with
-    the scheduled lr.  bs = 100 runs the persistent sppAcmSgd launches, bs = 160 the per-batch
-    regress kernels.  Tolerance as for the persistent SGD test, over all 3 x 21 (13) Adam steps."""
+    the scheduled lr.  bs = 100 runs the one-workgroup sppAcmSgd launches, bs = 160 the
+    multi-workgroup form.  Tolerance as for the persistent SGD test, over all 3 x 21 (13) Adam steps."""
     import spprl.trainer as tr
 
     n = 2050
@@ -436,7 +463,7 @@ def test_update_acm_epochs_with_step_lr_match_oracle(bs, monkeypatch):
     steps = 0
     for e, p in enumerate(perms):
         o.opt.lr = ag.acm_lr * 0.5 ** e
-        p = p.numpy()
+        p = p.cpu().numpy()
         losses = [o.batch_update(x_all[p[s:s + bs]], acm[p[s:s + bs]]) for s in range(0, n, bs)]
         steps += len(losses)
     assert ag.acm_loss == pytest.approx(np.mean(losses), rel=1e-4)

@@ -385,10 +385,11 @@ def bench_ppo(args, world, rank, dev):
     ACM cadence (acm/on_policy.py:78-82, acm/acm.py:126-141, 266-303): the reference runs update_acm(5 epochs)
     every 3 iterations of batch_size = 2000 frames over a ring of 1.1 * acm_pre_train_samples = 1.1e5 rows in
     batches of 64: sigma = 5 * 1.1e5 / (3 * 2000) = 91.67 ACM samples per env-step.  An iteration here is
-    N = T * E frames, so every sample count of that cadence is scaled by s = N / 2000 (as the critic's full
-    batch already is): ring 1.1e5 * s rows, ACM batch 64 * s, still 5 epochs every 3 iterations -- the same
-    sigma, the same number of sequential ACM steps per cycle as the reference (5 * 1719), one sppAcmSgd launch
-    per epoch spread over ~s workgroups."""
+    N = T * E frames per rank, so every sample count of that cadence is scaled by s = world * N / 2000 (as the
+    critic's full batch already is): ring 1.1e5 * s rows, ACM batch 64 * s, still 5 epochs every 3 iterations --
+    the same sigma, the same number of sequential ACM steps per cycle as the reference (5 * 1719), one
+    sppAcmSgd launch per epoch spread over ~s workgroups.  N > 1: the ring is replicated (every rank writes
+    every rank's rows, spprl/ppo_acm.py) and the epochs run on every rank with no per-batch collective."""
     import spprl
     from spprl import flops
     from spprl.dp import shard_seed
@@ -396,20 +397,21 @@ def bench_ppo(args, world, rank, dev):
     E = args.envs or 2048
     T = 16
     N = T * E
-    ref_batch, ref_pretrain, ref_acm_bs, acm_epochs, acm_freq = 2000, 100_000, 64, 5, 3
-    scale = N / ref_batch
+    ref_batch, ref_ring, ref_acm_bs, acm_epochs, acm_freq = 2000, 110_000, 64, 5, 3
+    # N > 1: the ACM ring is replicated (every rank holds every rank's rows, spprl/ppo_acm.py), so the ACM
+    # cadence is scaled by the frames of all ranks
+    scale = world * N / ref_batch
     acm_bs = int(round(ref_acm_bs * scale))
-    pretrain = int(round(ref_pretrain * scale))
     seed = shard_seed(1000, rank)
     ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=N,
                        ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
                        custom_loss=0.1, norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True,
                        acm_epochs=acm_epochs, acm_batch_size=acm_bs, acm_update_freq=acm_freq, acm_lr=3e-4,
-                       acm_pre_train_samples=pretrain, n_envs=E, device=dev, seed=0, loop_seed=seed)
+                       acm_ring_size=int(round(ref_ring * scale)), n_envs=E, device=dev, seed=0, loop_seed=seed)
     rb = ag.replay_buffer
     ob, ac = ag.ob_dim, ag.ac_dim
-    sigma = acm_epochs * rb.size / (acm_freq * N)
-    torch.manual_seed(seed)
+    sigma = acm_epochs * rb.size / (acm_freq * N * world)
+    torch.manual_seed(1000)  # the same pre-filled ring on every rank (replicated)
     fill = rb.size - 2 * E  # the ACM ring after pre-training (random env actions)
     prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
     slots = rb.add_obs_batch(torch.randn(fill, ob, device=dev))
@@ -449,7 +451,8 @@ def bench_ppo(args, world, rank, dev):
     mac = flops.onpolicy_macs(ob, ob, ac)
     # algorithmic work of the timed iterations: 100 full-batch critic steps on N samples, the PPO
     # epochs actually run (KL stop) over N samples, acm_epochs epochs over the ring per ACM update, the rollout
-    acm_samples = epochs["acm_updates"] * acm_epochs * rb.size
+    # (the ACM epochs run replicated on every rank: their algorithmic share per rank is 1/world of them)
+    acm_samples = epochs["acm_updates"] * acm_epochs * rb.size / world
     flop = 2.0 * (args.steps * (mac["critic_step"] * N * 100 + (mac["A"] + mac["M"]) * N)
                   + mac["actor_step"] * N * epochs["ppo"] + mac["acm_step"] * acm_samples)
     per_env_step = flop / (args.steps * N)
@@ -474,7 +477,7 @@ def bench_ppo(args, world, rank, dev):
                         "achieved": round(flop / elapsed / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": None, "traffic": None,
                         "note": "achieved = the timed iterations' algorithmic FLOPs (critic, actor epochs run, ACM, "
-                                "rollout: SURVEY §8d) / elapsed; 3 x 1719 sequential ACM steps per iteration and "
+                                "rollout: SURVEY §8d) / elapsed; 5 x 1719 sequential ACM steps every 3 iterations and "
                                 "~64 sequential 512-sample actor steps per epoch bound the iteration by latency"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)

@@ -269,11 +269,12 @@ sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
  * acm_cat, acm.py:260-264): x = [obs | next_obs] [B][2ob], y = acm action [B][ac]. */
 /* nsteps sequential AcM regression steps (acm.py:246-258 each: MSE + Adam at acm_lr) in ONE
  * launch: step k's batch = rows [k*bs, k*bs + bs) of x [nsteps*bs][2ob] / y [nsteps*bs][ac]
- * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 16384.  Parameters stay in
+ * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 32768.  Parameters stay in
  * LDS, moments in registers (update_acm epochs, update_acm_batches).  loss_sum += sum of the
  * steps' batch losses.  AcM agents (SAC_AcM) only.  bs <= 128: one workgroup; larger batches
- * spread each step over ceil(bs / 64) workgroups that sum the step's gradient in a fixed order
- * (deterministic) behind one arrival barrier per step. */
+ * spread each step over min(ceil(bs / 64), 256) workgroups that sum the step's gradient in a fixed
+ * order (deterministic) behind one arrival barrier per step (two past 24 workgroups: a sliced
+ * reduction, then the reduced gradient). */
 sppStatus sppAcmSgd(sppAgentHandle h, const float* x_dev, const float* y_dev, int nsteps, int bs, float* loss_sum,
                     void* stream);
 /* Synchronous: 1 if a multi-workgroup sppAcmSgd launch timed out waiting for its workgroups (its

@@ -1795,11 +1795,11 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
   // batches past one workgroup's rows: ~64 rows per workgroup, gradients summed over the workgroups
   int nwg = 1;
   if (bs > kSgdMaxBatch) {
-    nwg = cdiv(bs, kSgdBigRows);
+    nwg = std::min(cdiv(bs, kSgdBigRows), kSgdMaxWG);
     g.bsl = (int)round_up(cdiv(bs, nwg), 4);
     nwg = cdiv(bs, g.bsl);
     if (!a->sgd_slab.ptr) {
-      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)2 * kSgdMaxWG * kSlabStride));
+      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)(2 * kSgdMaxWG + 2) * kSlabStride));  // + the reduced slabs
       SPP_CHECK_HIP(a->sgd_sync.alloc(2));  // {arrival counter, timeout flag}
       SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, 2 * sizeof(int), st));
     }

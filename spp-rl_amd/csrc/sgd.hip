@@ -24,9 +24,10 @@ namespace spp {
 
 constexpr int kSgdThreads = 256;
 constexpr int kSgdMaxBatch = 128;   // rows per workgroup and step
-constexpr int kSgdMaxWG = 128;      // workgroups of the multi-workgroup form (batches up to 16,384)
+constexpr int kSgdMaxWG = 256;      // workgroups of the multi-workgroup form (batches up to 32,768)
 constexpr int kSlabStride = 5120;   // floats per workgroup slab: >= 16 * NT + 1 for every instantiation
 constexpr int kSgdBigRows = 64;     // target rows per workgroup of the multi-workgroup form
+constexpr int kSgdTwoLevel = 24;    // more workgroups than this: two-level gradient reduction per step
 
 struct AcmSgdArgs {
   const float* x;      // [nsteps * bs][IN] acm_cat inputs, consumed in order (sppReplayGatherAcm)
@@ -508,8 +509,35 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
             *reinterpret_cast<float4*>(mine + 16 * q + 4 * i) = make_float4(g[k][i][0], g[k][i][1], g[k][i][2], g[k][i][3]);
       }
       if (t == 0) mine[16 * C::NT] = ls_part;
-      sgd_arrive_wait(a.ctr, G * (st + 1), a.err, &s_dead);
+      const int nsync = G > kSgdTwoLevel ? 2 : 1;  // arrival waits per step
+      sgd_arrive_wait(a.ctr, G * nsync * st + G, a.err, &s_dead);
       const float* all = a.slab + (int64_t)(st & 1) * G * kSlabStride;
+      if (G > kSgdTwoLevel) {
+        // many workgroups: workgroup g first sums slice g of the gradient over every slab (fixed order)
+        // into the step's reduced slab, then every workgroup reads the reduced gradient
+        float* red = a.slab + (int64_t)2 * G * kSlabStride + (int64_t)(st & 1) * kSlabStride;
+        constexpr int NTE = 16 * C::NT + 1;
+        const int chunk = (NTE + G - 1) / G;
+        const int e1 = min((int)(blockIdx.x + 1) * chunk, NTE);
+        for (int e = (int)blockIdx.x * chunk + t; e < e1; e += TH) {
+          float v = 0.f;
+          for (int gg = 0; gg < G; ++gg) v += all[(int64_t)gg * kSlabStride + e];
+          red[e] = v;
+        }
+        sgd_arrive_wait(a.ctr, G * nsync * st + 2 * G, a.err, &s_dead);
+#pragma unroll
+        for (int k = 0; k < C::RT; ++k) {
+          const int q = sgd_own<C, TH>(t, k);
+          if (q >= 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float4 v = reinterpret_cast<const float4*>(red + 16 * q)[i];
+              g[k][i][0] = v.x; g[k][i][1] = v.y; g[k][i][2] = v.z; g[k][i][3] = v.w;
+            }
+          }
+        }
+        if (blockIdx.x == 0 && t == 0) loss_acc += red[16 * C::NT] * inv_n;
+      } else {
 #pragma unroll
       for (int k = 0; k < C::RT; ++k) {
         const int q = sgd_own<C, TH>(t, k);
@@ -533,6 +561,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
         float ls = 0.f;
         for (int gg = 0; gg < G; ++gg) ls += all[(int64_t)gg * kSlabStride + 16 * C::NT];
         loss_acc += ls * inv_n;
+      }
       }
     }
     // ---- Adam (torch.optim.Adam, same operation order as k_adam) on the owned tiles

@@ -44,7 +44,8 @@ class PPO_AcM:
                  custom_loss=0.1, norm_closs=config.NORM_CLOSS, min_max_denormalize=True, denormalize_actor_out=True,
                  acm_epochs=5, acm_batch_size=64, acm_update_freq=3, acm_lr=3e-4, acm_update_batches=None,
                  acm_pre_train_samples=100_000, acm_pre_train_epochs=5, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
-                 acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, iterations=1001,
+                 acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, acm_ring_size=None,
+                 iterations=1001,
                  stats_freq=1, test_episodes=None, return_done=None, max_frames=None, n_envs=1, env=None,
                  env_spec=None, device="cuda", seed=None, loop_seed=0, **unused):
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
@@ -74,7 +75,7 @@ class PPO_AcM:
                                  kl_div_threshold=kl_div_threshold, normalize_adv=normalize_adv,
                                  max_batch=max(Nmax, ppo_batch_size), device=self.device, seed=seed)
         # the AcM and its replay ring (acm.py:127-141: size = pre-train samples * 1.1)
-        ring = int(acm_pre_train_samples * 1.1)
+        ring = int(acm_ring_size or acm_pre_train_samples * 1.1)
         self.acm = SAC_AcM(env_name=env_name, env_spec=(ob, ac, ac_high, max_ep), acm_lr=acm_lr, buffer_size=ring,
                            max_batch=max(acm_batch_size, 64), min_max_denormalize=min_max_denormalize,
                            denormalize_actor_out=denormalize_actor_out, device=self.device, seed=seed, env=env,
@@ -84,6 +85,19 @@ class PPO_AcM:
                            acm_scheduler_gamma=acm_scheduler_gamma, acm_keep_pretrain=acm_keep_pretrain,
                            loop_seed=loop_seed + 17)
         self.replay_buffer = self.acm.replay_buffer
+        # Data parallel: the ACM ring is REPLICATED (every rank writes every rank's transitions, in rank
+        # order, at the end of each iteration: ReplayBufferAcM.add_buffer, replay_buffer.py:284-297), so the
+        # ACM epochs (acm.py:266-303) run on identical rings with one permutation stream and need no
+        # per-batch collective, and the ring's obs statistics are global without a collective either.
+        import torch.distributed as dist
+
+        self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
+        self.rank = dist.get_rank() if self.world > 1 else 0
+        if self.nets.allreduce is not None:
+            self.acm.allreduce = self.acm.allreduce_sum = self.acm.host_sum = None
+        self.acm._perm_seed = int(seed or 0) * 7919 + 17  # rank-independent epoch permutations
+        self._ring_log = []  # this iteration's ring writes (applied by _flush_ring)
+        self._prev_all = None  # per rank: the ring slot of each env's last obs
         self.stats_logger = StatsLogger()
         self.iteration = 0
         self.loop_seed, self._ctr = int(loop_seed), 0
@@ -118,7 +132,33 @@ class PPO_AcM:
 
     # ---------------------------------------------------------------- RL.train / perform_iteration
     def pre_train(self):
-        self.acm.pre_train()
+        """acm.py:234-244.  Data parallel: the random-action samples of every rank go into every rank's
+        ring (replicated, as the iteration's writes), then the same epochs run on every rank."""
+        if self.world == 1:
+            self.acm.pre_train()
+            self._obs = None
+            return
+        acm, E = self.acm, self.n_envs
+        obs = self.env.reset()
+        self._ring_log.append(("start", obs.clone()))
+        act = torch.empty(E, self.ac_dim, device=self.device)
+        collected = 0
+        while collected < acm.acm_pre_train_samples:  # AcMOffPolicy.collect_samples (off_policy.py:56-87)
+            self.env.sample_actions(act)
+            nobs, rew, end, end_dev = self.env.step(act)
+            mask, robs = None, None
+            if end.any():
+                obs = self.env.reset(end)
+                mask, robs = end.copy(), obs.clone()
+            # the buffer's action slot holds the next obs; time-limit ends are kept as done
+            self._ring_log.append(("step", nobs.clone(), rew.clone(), end_dev.clone(), end_dev.clone(), act.clone(),
+                                   mask, robs))
+            collected += E
+        self._flush_ring()
+        acm.update_acm(epochs=acm.acm_pre_train_epochs, pretrain=True)
+        acm.update_obs_stats()
+        if not acm.acm_keep_pretrain:
+            self.replay_buffer.reset_idx()
         self._obs = None
 
     def train(self, iterations=None):
@@ -156,9 +196,76 @@ class PPO_AcM:
     # ---------------------------------------------------------------- A2C.collect_batch
     def _start(self):
         self._obs = self.env.reset()
-        self._prev_slots = self.replay_buffer.add_obs_batch(self._obs)
+        self._ring_log.append(("start", self._obs.clone()))
         self._ep_ret.zero_()
         self._ep_len = np.zeros(self.n_envs, np.int64)
+
+    # ---------------------------------------------------------------- the ACM ring (add_buffer)
+    def _flush_ring(self):
+        """Apply the iteration's ring writes (ReplayBufferAcM.add_buffer at the iteration's end,
+        replay_buffer.py:284-297): locally, or -- data parallel -- every rank's writes in rank order
+        after one all-gather of the iteration's records, so every rank holds the same ring."""
+        log, self._ring_log = self._ring_log, []
+        if not log:
+            return
+        E, ob, ac = self.n_envs, self.ob_dim, self.ac_dim
+        W = self.world
+        if self._prev_all is None:
+            self._prev_all = [None] * W
+        if W == 1:
+            blocks = [log]
+        else:
+            import torch.distributed as dist
+
+            F = 2 * ob + ac + 4  # obs | rew | done | end | env action | reset obs | reset mask
+            buf = torch.zeros(len(log), E, F, device=self.device)
+            for i, rec in enumerate(log):
+                if rec[0] == "start":
+                    buf[i, :, :ob] = rec[1]
+                else:
+                    _, nobs, rew, done, end, act, mask, robs = rec
+                    buf[i, :, :ob] = nobs
+                    buf[i, :, ob] = rew
+                    buf[i, :, ob + 1] = done.float()
+                    buf[i, :, ob + 2] = end.float()
+                    buf[i, :, ob + 3:ob + 3 + ac] = act
+                    if mask is not None:
+                        buf[i, :, ob + 3 + ac:2 * ob + 3 + ac] = robs
+                        buf[i, :, 2 * ob + 3 + ac] = torch.from_numpy(mask.astype(np.float32)).to(self.device)
+            allb = torch.empty(W * buf.shape[0], *buf.shape[1:], device=self.device)
+            dist.all_gather_into_tensor(allb, buf)  # rank-major along dim 0
+            allb = allb.view(W, *buf.shape)
+            masks = allb[:, :, :, 2 * ob + 3 + ac].cpu().numpy() > 0.5  # one host copy for every rank's masks
+            blocks = []
+            for r in range(W):
+                recs = []
+                for i, rec in enumerate(log):
+                    b = allb[r, i]
+                    if rec[0] == "start":
+                        recs.append(("start", b[:, :ob]))
+                    else:
+                        m = masks[r, i]
+                        recs.append(("step", b[:, :ob], b[:, ob], b[:, ob + 1].to(torch.uint8),
+                                     b[:, ob + 2].to(torch.uint8), b[:, ob + 3:ob + 3 + ac],
+                                     m if m.any() else None, b[:, ob + 3 + ac:2 * ob + 3 + ac]))
+                blocks.append(recs)
+        rb = self.replay_buffer
+        for r, recs in enumerate(blocks):
+            prev = self._prev_all[r]
+            for rec in recs:
+                if rec[0] == "start":
+                    prev = rb.add_obs_batch(rec[1])
+                    continue
+                _, nobs, rew, done, end, act, mask, robs = rec
+                slots = rb.add_obs_batch(nobs)
+                rb.add_timestep_batch(prev, slots, nobs, rew, done, end, act)  # ReplayBufferAcM ring
+                prev = slots
+                if mask is not None:
+                    idx = np.flatnonzero(mask)
+                    rs = rb.add_obs_batch(robs[torch.as_tensor(idx, device=self.device)])
+                    prev = prev.copy()
+                    prev[idx] = rs
+            self._prev_all[r] = prev
 
     def collect_batch(self):
         """Rollout memory, time-major [T][E]: normalised obs, actions, log-probs, rewards, done,
@@ -181,6 +288,7 @@ class PPO_AcM:
                 self._start()
                 self.stats_logger.rollouts += E
             flat = [self._step()[:-1] for _ in range(self.T)]
+        self._flush_ring()
         T = len(flat)
         cat = lambda k: torch.stack([f[k] for f in flat])  # noqa: E731
         mem = {"obs": cat(0), "act": cat(1), "lp": cat(2), "rew": cat(3), "done": cat(4), "end": cat(5),
@@ -207,17 +315,15 @@ class PPO_AcM:
         any_end = bool(end.any())
         call("sppEpisodeAccum", ptr(rew), ptr(end_dev) if any_end else None, E, ptr(self._ep_ret),
              ptr(self._ret_sums), stream_handle())
-        slots = rb.add_obs_batch(nobs)
-        rb.add_timestep_batch(self._prev_slots, slots, nobs, rew, done, end_dev, env_act)  # ReplayBufferAcM ring
-        self._prev_slots = slots
         out = (norm_obs, act, lp, rew.clone(), done, end_dev.clone(), nobs.clone(), end.any() if E == 1 else False)
         self._obs = nobs
+        mask, robs = None, None
         if any_end and E > 1:
             self.stats_logger.rollouts += int(end.sum())
             self._obs = self.env.reset(end)
-            rs = rb.add_obs_batch(self._obs[torch.as_tensor(np.flatnonzero(end), device=self.device)])
-            self._prev_slots = self._prev_slots.copy()
-            self._prev_slots[np.flatnonzero(end)] = rs
+            mask, robs = end.copy(), self._obs.clone()
+        # ring writes of this step (applied at the iteration's end, _flush_ring)
+        self._ring_log.append(("step", out[6], out[3], done, out[5], env_act.clone(), mask, robs))
         return out
 
     # ---------------------------------------------------------------- update (critic, GAE, actor)

@@ -576,7 +576,7 @@ class OffPolicyLoop:
 
     def _acm_sgd_ok(self, bs):
         """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank."""
-        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 16384
+        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 32768
                 and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1)))
 
     def _acm_sgd(self, idx, nsteps, bs):
@@ -609,7 +609,14 @@ class OffPolicyLoop:
             return
         # epoch permutations drawn on the device (DataLoader(shuffle=True), acm.py:275): a host randperm and
         # its pageable copy would hold the stream for every epoch of a large ring
-        g = torch.Generator(device=self.device).manual_seed(self.loop_seed * 7919 + self._next())
+        # (_perm_seed: a seed shared by data-parallel ranks that run the epochs replicated, spprl/ppo_acm.py)
+        ps = getattr(self, "_perm_seed", None)
+        if ps is None:
+            seed = self.loop_seed * 7919 + self._next()
+        else:
+            self._perm_ctr = getattr(self, "_perm_ctr", 0) + 1
+            seed = ps + 104729 * self._perm_ctr
+        g = torch.Generator(device=self.device).manual_seed(seed)
         for _ in range(epochs):
             lr = self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step)
             self._set_acm_lr(lr)

@@ -13,6 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from rank_results import collect
+
 
 def _free_port():
     with socket.socket() as s:
@@ -59,7 +61,7 @@ def test_dp_obs_stats_two_ranks_match_union(ob, use_host):
     procs = [ctx.Process(target=_worker, args=(r, port, ob, use_host, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r[0], r[1:]) for r in (q.get(timeout=180) for _ in procs))
+    res = collect(q, procs, timeout=180)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

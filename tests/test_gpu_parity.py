@@ -371,7 +371,8 @@ def test_obs_stats_data_parallel_protocol_matches_union(ob, ranks):
 
 
 @pytest.mark.parametrize("env_name,ob,ac,bs", [("Hopper-v2", 11, 3, 100), ("HalfCheetah-v2", 17, 6, 64),
-                                               ("Hopper-v2", 11, 3, 700), ("HalfCheetah-v2", 17, 6, 1049)])
+                                               ("Hopper-v2", 11, 3, 700), ("HalfCheetah-v2", 17, 6, 1049),
+                                               ("HalfCheetah-v2", 17, 6, 2500)])
 def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     """sppAcmSgd (K sequential AcM regression steps in one launch, parameters in LDS) against
     the oracle's AcMTrainer.batch_update sequence on the same replay batches (acm.py:246-264):

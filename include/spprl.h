@@ -94,7 +94,7 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
  *   step k   selection with the global counts (n_global = sum of the ranks' len),
  *            then the next local byte pass -> hist
  * and all-reduce (sum) `sums` after step 0 and `hist` after every step that did
- * not set *done.  hist: sppReplayObsStatsDPHistSize(h) uint32 counters. */
+ * not set *done.  hist: sppReplayObsStatsDPHistSize(h) uint32 counters.  n_global < 2^31. */
 int sppReplayObsStatsDPHistSize(sppReplayHandle h);
 sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot /*[ob], replicated*/,
                               double* sums /*[ob][2]*/, uint32_t* hist, int64_t n_global, float* mean, float* std,
@@ -256,6 +256,9 @@ sppStatus sppCommDestroy(void* comm);
  *   SPP_BUCKET_ALL     all of them. */
 enum { SPP_BUCKET_CRITIC = 0, SPP_BUCKET_ACTOR = 1, SPP_BUCKET_ACM = 2, SPP_BUCKET_ALL = 3 };
 sppStatus sppAllReduceGrads(sppAgentHandle h, int bucket, int world, void* rccl_comm, void* stream);
+/* In-place sum over the communicator of `count` elements (dtype 0 fp32, 1 fp64, 2 int32, 3 int64,
+ * 4 uint32): the obs-statistics sums / counts of sppReplayObsStatsDP and the global row count. */
+sppStatus sppCommAllReduceSum(void* rccl_comm, void* buf_dev, int64_t count, int dtype, void* stream);
 
 /* AcMTrainer.batch_update (rltoolkit/acm/acm.py:246-258): x [B][2ob], y [B][ac]
  * -> MSE loss (device float) and one Adam step on the bound ACM net. */

@@ -500,7 +500,8 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot, d
               SPP_E_INVALID_ARG, "obs_stats_dp: bad args");
   const int ob = h->d.ob;
   SPP_REQUIRE(ob <= 16 * kStatsColsPerThread, SPP_E_SHAPE, "obs_stats_dp: ob %d > %d", ob, 16 * kStatsColsPerThread);
-  SPP_REQUIRE(n_global > 10 && n_global < ((int64_t)1 << 32), SPP_E_INVALID_ARG, "obs_stats_dp: n_global %lld",
+  // counts travel as int32 (the host's fused first exchange converts fp64 sums back to int32)
+  SPP_REQUIRE(n_global > 10 && n_global < ((int64_t)1 << 31), SPP_E_INVALID_ARG, "obs_stats_dp: n_global %lld",
               (long long)n_global);
   sppStatus s = stats_alloc(h);
   if (s) return s;
@@ -2310,6 +2311,18 @@ sppStatus sppCommDestroy(void* comm) {
   SPP_REQUIRE(comm, SPP_E_INVALID_ARG, "comm destroy: null");
   SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
   SPP_CHECK_RCCL(rccl().destroy(comm));
+  return SPP_OK;
+}
+
+// In-place sum of a device buffer over the communicator (the obs-statistics exchange of C hosts).
+sppStatus sppCommAllReduceSum(void* comm, void* buf, int64_t count, int dtype, void* stream) {
+  SPP_REQUIRE(comm && buf && count >= 0 && dtype >= 0 && dtype <= 4, SPP_E_INVALID_ARG,
+              "comm allreduce sum: dtype %d count %lld", dtype, (long long)count);
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  // ncclFloat32 7, ncclFloat64 8, ncclInt32 2, ncclInt64 4, ncclUint32 3
+  static const int kType[5] = {7, 8, 2, 4, 3};
+  if (count == 0) return SPP_OK;
+  SPP_CHECK_RCCL(rccl().all_reduce(buf, buf, (size_t)count, kType[dtype], kNcclSum, comm, S(stream)));
   return SPP_OK;
 }
 

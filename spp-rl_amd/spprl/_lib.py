@@ -78,6 +78,7 @@ _SIGS = {
     "sppCommInitRank": (c_int, [P(c_void_p), c_int, c_void_p, c_int, c_int]),
     "sppCommDestroy": (c_int, [c_void_p]),
     "sppAllReduceGrads": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sppCommAllReduceSum": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "sppAgentCreate": (c_int, [P(c_void_p), P(AgentConfig), c_int]),
     "sppAgentDestroy": (c_int, [c_void_p]),
     "sppAgentNetSize": (c_int, [c_void_p, c_int, P(c_int64)]),

@@ -52,32 +52,35 @@ def make_allreduce_sum(group=None):
     return allreduce_sum
 
 
-_HOST_GROUP = None
+_HOST_GROUPS = {}
 
 
 def make_host_allreduce_sum(group=None):
-    """Returns ``host_sum(x) -> int`` (sum of a host integer over the group) or None with a
-    single rank.  Host-known counts (the shards' live row counts) are exchanged as CPU tensors over
-    gloo: no device tensor, so no device synchronisation on the way.  With an RCCL default group
-    a gloo group over the same ranks is created once; every rank must call this in the same order
-    (the agents' constructors do)."""
+    """Returns ``host_sum(x) -> int`` (sum of a host integer over the group; a list of integers gives the
+    list of sums) or None with a single rank.  Host-known counts (the shards' live row counts) are
+    exchanged as CPU tensors over gloo: no device tensor, so no device synchronisation on the way.  For a
+    group on another backend a gloo group over the SAME ranks is created once per distinct rank set (and
+    per default group: it is rebuilt after the default group is destroyed and re-initialised); every
+    rank must call this in the same order (the agents' constructors do)."""
     if not dist.is_available() or not dist.is_initialized():
         return None
     if dist.get_world_size(group) == 1 and not _single_rank_exchange():
         return None
     import torch
 
-    global _HOST_GROUP
     g = group
     if dist.get_backend(group) != "gloo":
-        if _HOST_GROUP is None:
-            _HOST_GROUP = dist.new_group(backend="gloo")
-        g = _HOST_GROUP
+        ranks = tuple(dist.get_process_group_ranks(group if group is not None else dist.group.WORLD))
+        key = (id(dist.group.WORLD), ranks)
+        if key not in _HOST_GROUPS:
+            _HOST_GROUPS[key] = dist.new_group(ranks=list(ranks), backend="gloo")
+        g = _HOST_GROUPS[key]
 
     def host_sum(x):
-        t = torch.tensor([int(x)], dtype=torch.int64)
+        many = isinstance(x, (list, tuple))
+        t = torch.tensor([int(v) for v in x] if many else [int(x)], dtype=torch.int64)
         dist.all_reduce(t, group=g)
-        return int(t.item())
+        return [int(v) for v in t.tolist()] if many else int(t.item())
 
     return host_sum
 
@@ -126,6 +129,34 @@ class NativeComm:
         uid = ctypes.create_string_buffer(bytes(raw), _lib.SPP_COMM_ID_BYTES)
         self.comm = ctypes.c_void_p()
         _lib.call("sppCommInitRank", ctypes.byref(self.comm), self.world, uid, self.rank, int(device))
+
+    def allreduce_sum(self, t):
+        """In-place sum of a device tensor over the communicator (fp32 / fp64 / int32 / int64 / uint32:
+        the obs-statistics exchange), on the current stream (sppCommAllReduceSum)."""
+        from . import _lib
+
+        import torch
+
+        code = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3}[t.dtype]
+        _lib.call("sppCommAllReduceSum", self.comm, _lib.ptr(t), t.numel(), code, _lib.stream_handle())
+
+    def host_sum(self, x):
+        """Sum of host integers over the communicator (one small device all-reduce + a host read)."""
+        import torch
+
+        many = isinstance(x, (list, tuple))
+        t = torch.tensor([int(v) for v in x] if many else [int(x)], dtype=torch.int64, device="cuda")
+        self.allreduce_sum(t)
+        return [int(v) for v in t.tolist()] if many else int(t.item())
+
+    def attach(self, agent):
+        """Run ``agent``'s data-parallel exchange over this communicator: gradient buckets, the
+        obs-statistics sums and the row counts (all three are needed: with the gradients averaged but the
+        statistics per rank, the replicas' normalisers would drift apart)."""
+        agent.allreduce = self.allreduce_for(agent)
+        agent.allreduce_sum = self.allreduce_sum
+        agent.host_sum = self.host_sum
+        return agent
 
     def allreduce_for(self, agent):
         """``allreduce(bucket)`` over the agent's exchange buckets (bucket_critic / _actor / _acm),

@@ -226,12 +226,18 @@ class BufferAcMOffPolicy:
         if n_global is None:
             gen = getattr(self, "_gen", 0)
             if getattr(self, "_ng_gen", None) != gen:
+                # (len, gen, 1) summed together: the ranks must be in lockstep (every rank writes timesteps
+                # the same number of times, so every rank reaches this exchange); a rank whose count of
+                # writes differs is caught here, not as a later hang
                 if host_sum is not None:
-                    ng = host_sum(len(self))
+                    ng, sgen, world = host_sum([len(self), gen, 1])
                 else:
-                    n = torch.tensor([len(self)], dtype=torch.int64, device=self.device)
+                    n = torch.tensor([len(self), gen, 1], dtype=torch.int64, device=self.device)
                     allreduce_sum(n)
-                    ng = int(n.item())
+                    ng, sgen, world = (int(v) for v in n.tolist())
+                if sgen != gen * world:
+                    raise RuntimeError("data-parallel replay shards out of lockstep: timestep-write counts "
+                                       "differ across ranks (this rank %d, sum %d over %d ranks)" % (gen, sgen, world))
                 self._ng, self._ng_gen = ng, gen
             n_global = self._ng
         if n_global <= 10:  # replay_buffer.py:84, on the global buffer

@@ -83,6 +83,8 @@ class ScalarWriter:
         self._write(_event(0, time.time(), file_version="brain.Event:2"))
 
     def _write(self, ev: bytes):
+        if self._f is None:  # closed at the end of train(): a later log call appends to the same file
+            self._f = open(self.path, "ab")
         hdr = struct.pack("<Q", len(ev))
         self._f.write(hdr + struct.pack("<I", _masked(crc32c(hdr))) + ev + struct.pack("<I", _masked(crc32c(ev))))
 
@@ -90,7 +92,8 @@ class ScalarWriter:
         self._write(_event(step, time.time(), summary=_scalar_summary(tag, float(value))))
 
     def flush(self):
-        self._f.flush()
+        if self._f is not None:
+            self._f.flush()
 
     def close(self):
         if self._f:

@@ -307,7 +307,8 @@ class OffPolicyLoop:
                    acm_update_batches=config.ACM_UPDATE_BATCHES, acm_pre_train_samples=config.ACM_PRE_TRAIN_SAMPLES,
                    acm_pre_train_epochs=config.ACM_PRE_TRAIN_N_EPOCHS, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
                    acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=config.ACM_KEEP_PRE_TRAIN,
-                   n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, tensorboard_dir=None,
+                   n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, allreduce_sum=None, host_sum=None,
+                   tensorboard_dir=None,
                    debug_mode=False, **unused):
         if max_frames is not None and max_frames > iterations * batch_size:
             raise AssertionError("max_frames should be smaller or equal than iterations * batch_size")  # rl.py:166
@@ -341,8 +342,15 @@ class OffPolicyLoop:
         if self.schedule not in ("reference", "fused"):
             raise ValueError("schedule must be 'reference' or 'fused'")
         self.allreduce = allreduce if allreduce is not None else make_allreduce()
-        self.allreduce_sum = make_allreduce_sum() if self.allreduce is not None else None
-        self.host_sum = make_host_allreduce_sum() if self.allreduce is not None else None
+        self.allreduce_sum = self.host_sum = None
+        if self.allreduce is not None:
+            # the obs statistics must be global whenever the gradients are (else the replicas' normalisers
+            # drift apart): an explicit gradient exchange needs its statistics exchange too
+            self.allreduce_sum = allreduce_sum if allreduce_sum is not None else make_allreduce_sum()
+            self.host_sum = host_sum if host_sum is not None else make_host_allreduce_sum()
+            if self.allreduce_sum is None:
+                raise ValueError("an explicit allreduce needs allreduce_sum (and host_sum) for the global obs "
+                                 "statistics, e.g. spprl.dp.NativeComm(...).attach(agent) or torch.distributed")
         self.loop_seed = int(loop_seed)
         # one Philox key per random-stream consumer (never a shared (key, counter) pair)
         self._key_policy, self._key_index = stream_key(loop_seed, "policy"), stream_key(loop_seed, "index")
@@ -428,6 +436,9 @@ class OffPolicyLoop:
 
     def update_obs_stats(self):
         """update_obs_mean_std (rl.py:93-112); global over the ranks' shards under DP."""
+        if self.allreduce is not None and self.allreduce_sum is None:
+            raise RuntimeError("data-parallel gradients without a statistics exchange (allreduce_sum): "
+                               "use NativeComm.attach(agent) or torch.distributed")
         if self.allreduce_sum is not None:
             # shard lengths differ across ranks once resets (early terminations) advance the
             # obs rings unevenly: the global row count is all-reduced, never assumed

@@ -183,6 +183,14 @@ def gen_replay():
         out[p + "done"] = np.array(done_log, np.bool_)
         out[p + "end"] = np.array(end_log, np.bool_)
         out[p + "states"] = np.array(states, np.int64)
+        # last_rollout (replay_buffer.py:335-383) on the built ring, before the stats below scale _obs
+        m = buf.last_rollout()
+        out[p + "lr_obs"] = m.obs.numpy()
+        out[p + "lr_next_obs"] = m.next_obs.numpy()
+        out[p + "lr_act"] = torch.cat([torch.as_tensor(a).reshape(1, -1) for a in m._actions]).numpy().astype(np.float32)
+        out[p + "lr_rew"] = np.array(m._rewards, np.float32)
+        out[p + "lr_end"] = np.array(m._end, np.bool_)
+        out[p + "lr_acm"] = np.stack([np.asarray(a, np.float32) for a in m.actions_acm])
         L = buf.current_len
         out[p + "obs_idx"] = buf._obs_idx[:L].astype(np.int64)
         out[p + "next_obs_idx"] = buf._next_obs_idx[:L].astype(np.int64)
@@ -538,7 +546,81 @@ def gen_onpolicy(seed=51):
     save("onpolicy_hcheetah.npz", **out)
 
 
-GROUPS = {"randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
+# ---------------------------------------------------------------- normalizer KATs + reference checkpoint
+def gen_interop(seed=61):
+    """(1) MemoryMeta.normalize / denormalize (memory.py:76-127) and utils.standardize_and_clip /
+    revert_standardization (utils.py:62-83) on the reference's own KAT inputs (buffer/test/test_memory.py:
+    84-96 test_normalize, test/test_utils.py:9-43) and on a random batch in both modes; (2) a checkpoint
+    written by the reference's own RL.save (rl.py:281-290; sac.py:287-296 + the ACM, ddpg_acm.py:87-90) from a
+    SAC_AcM Hopper with random weights and normaliser, and the reference's deterministic test action on a
+    batch of obs (ddpg.py:385-410: normalize -> noise_action(act_noise=0, deterministic=True) ->
+    process_action)."""
+    from rltoolkit import utils
+
+    out = {}
+    rng = np.random.RandomState(seed)
+    # (1a) test_memory.py::test_normalize (z-score, clip 10)
+    mem = Memory()
+    mem.obs_std = torch.tensor([2.0, 20.0])
+    mem.obs_mean = torch.tensor([2.5, 25.0])
+    ex = torch.tensor([[i, 10 * i] for i in range(6)]).float()
+    out["kat_mem_x"] = ex.numpy()
+    out["kat_mem_y"] = mem.normalize(ex).numpy()
+    ex2 = ex.clone()
+    ex2[0, 0] = 1000
+    out["kat_mem_x2"] = ex2.numpy()
+    out["kat_mem_y2"] = mem.normalize(ex2).numpy()
+    out["kat_mem_mean"], out["kat_mem_std"] = mem.obs_mean.numpy(), mem.obs_std.numpy()
+    # (1b) test_utils.py fixture: obs = arange(20).reshape(4, 5).T, torch mean / std(ddof=1)
+    obs = torch.tensor(np.arange(20).reshape(4, 5).T).float()
+    mean, std = obs.mean(axis=0), obs.std(axis=0)
+    st = utils.standardize_and_clip(obs, mean, std)
+    out.update(kat_utl_x=obs.numpy(), kat_utl_mean=mean.numpy(), kat_utl_std=std.numpy(), kat_utl_stand=st.numpy(),
+               kat_utl_revert=utils.revert_standardization(st, mean, std).numpy())
+    # (1c) random batch, both modes, normalize and denormalize
+    ob = 11
+    x = (rng.randn(257, ob) * 3).astype(np.float32)
+    x[0, :3] = [1e6, -1e6, 0.0]  # clipped in z-score mode
+    lo = -rng.uniform(0.5, 2, ob).astype(np.float32)
+    hi = rng.uniform(0.5, 2, ob).astype(np.float32)
+    mu = rng.randn(ob).astype(np.float32)
+    sd = rng.uniform(0.1, 3, ob).astype(np.float32)
+    for mm in (True, False):
+        m2 = Memory(min_max_denormalize=mm)
+        m2.min_obs, m2.max_obs = torch.from_numpy(lo), torch.from_numpy(hi)
+        m2.obs_mean, m2.obs_std = torch.from_numpy(mu), torch.from_numpy(sd)
+        tag = "mm" if mm else "z"
+        out["rnd_%s_norm" % tag] = m2.normalize(torch.from_numpy(x)).numpy()
+        out["rnd_%s_denorm" % tag] = m2.denormalize(torch.from_numpy(x)).numpy()
+    out.update(rnd_x=x, rnd_lo=lo, rnd_hi=hi, rnd_mean=mu, rnd_std=sd)
+    # (2) reference-written checkpoint + the reference's deterministic test action
+    torch.manual_seed(seed)
+    ag = SAC_AcM(env_name="Hopper-v2", acm_critic=True, custom_loss=0.2, min_max_denormalize=True,
+                 denormalize_actor_out=True, buffer_size=100)
+    for net in (ag.actor, ag.critic_1, ag.critic_2, ag.acm):
+        load(net, int(rng.randint(1 << 30)))
+    rb = ag.replay_buffer
+    rb.min_obs = torch.from_numpy(-rng.uniform(0.5, 2, ob).astype(np.float32))
+    rb.max_obs = torch.from_numpy(rng.uniform(0.5, 2, ob).astype(np.float32))
+    rb.obs_mean = torch.from_numpy(rng.randn(ob).astype(np.float32))
+    rb.obs_std = torch.from_numpy(rng.uniform(0.5, 2, ob).astype(np.float32))
+    path = os.path.join(HERE, "ref_sac_acm_hopper.pkl")
+    ag.save(path)
+    print("wrote", path)
+    obs_raw = (rng.randn(64, ob) * 1.5).astype(np.float32)
+    tgts, envs = [], []
+    with torch.no_grad():
+        for i in range(len(obs_raw)):
+            o = ag.replay_buffer.normalize(torch.from_numpy(obs_raw[i:i + 1]))
+            a = ag.noise_action(o, act_noise=0, deterministic=True)
+            tgts.append(a.numpy()[0])
+            envs.append(ag.process_action(a, o))
+    out.update(ckpt_obs=obs_raw, ckpt_target=np.array(tgts, np.float32), ckpt_env_action=np.array(envs, np.float32),
+               ckpt_obs_norm=np.array([int(rb.obs_norm)]))
+    save("ref_interop.npz", **out)
+
+
+GROUPS = {"interop": gen_interop, "randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
           "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy}
 
 if __name__ == "__main__":

@@ -140,6 +140,30 @@ def test_native_comm_wrapper_drives_the_dp_update():
         nc.close()
 
 
+def test_native_comm_attach_provides_the_statistics_exchange():
+    """NativeComm.attach sets all three exchanges a data-parallel agent needs (gradient buckets,
+    obs-statistics sums through sppCommAllReduceSum, host row counts); an explicit gradient exchange
+    without a statistics exchange is refused (the replicas' normalisers would drift apart)."""
+    from spprl.dp import NativeComm
+
+    nc = NativeComm(0, 1, 0, lambda b: b)
+    try:
+        ag = spprl.SAC_AcM(env_name="Hopper-v2", buffer_size=64, max_batch=64, device=DEV, seed=0)
+        nc.attach(ag)
+        assert ag.allreduce is not None and ag.allreduce_sum is not None and ag.host_sum is not None
+        for dt in (torch.float32, torch.float64, torch.int32, torch.int64):
+            t = torch.arange(7, device=DEV).to(dt)
+            nc.allreduce_sum(t)  # one rank: the sum is the identity
+            torch.cuda.synchronize()
+            assert torch.equal(t.cpu(), torch.arange(7).to(dt))
+        assert nc.host_sum([3, 4]) == [3, 4] and nc.host_sum(9) == 9
+        with pytest.raises(ValueError, match="allreduce_sum"):
+            spprl.SAC_AcM(env_name="Hopper-v2", buffer_size=64, max_batch=64, device=DEV, seed=0,
+                          allreduce=lambda b: None)
+    finally:
+        nc.close()
+
+
 def test_host_synth_env_matches_device_dynamics_and_runs_the_loop():
     from spprl import HostSynthEnv, SynthVecEnv
 

@@ -48,3 +48,15 @@ def test_corrupted_record_is_detected(tmp_path):
         f.write(data)
     with pytest.raises(ValueError):
         read_scalars(w.path)
+
+
+def test_logging_after_close_reopens_the_event_file(tmp_path):
+    """train() closes the writer on its last iteration (rl.py:229-235); a later train() or test log call
+    appends to the same event file instead of failing."""
+    w = TensorboardWriter(str(tmp_path))
+    w.add_scalar("x", 1.0, 1)
+    w.close()
+    w.add_scalar("x", 2.0, 2)
+    w.flush()
+    w.close()
+    assert read_scalars(w.path) == [(1, "x", 1.0), (2, "x", 2.0)]

@@ -148,6 +148,96 @@ __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float
   }
 }
 
+// 256 x 256 fp32 jobs (the hidden-layer weight gradients of the critics and the actor): the
+// workgroup's operand rows are staged through LDS so every A / X byte leaves HBM once per item.
+// (In dw_tile each A row is streamed by the two waves that share its row blocks and each X row by
+// the two that share its column blocks: twice the bytes, ~4.9 TB/s at the MFMA rate.)
+// Step = 32 samples = one 128-B line per row; the step's 512 rows ([A (256) | X (256)] x 128 B = 64 KiB)
+// arrive by LDS-DMA (global_load_lds_dwordx4: 8 rows per wave-instruction, 16 per wave, no VGPR
+// destination), one step ahead, into the other of two LDS buffers.  The LDS image is lane-linear
+// (row r at 128 r bytes); the 16-B slot q of row r holds piece q ^ ((r >> 1) & 7) of the row (the
+// swizzle is applied on the global SOURCE address and undone on the read), which makes the MFMA
+// operand reads (lane c reads row c of its block, ds_read_b128) bank-conflict free.
+typedef __attribute__((address_space(1))) void glob_void;
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void dw_big_lds(const DwJob& J, int b_begin, int nsteps, int nb0, int kb0, bool db,
+                                           f32x16 (&acc)[4][4], float (&bs)[4]) {
+  __shared__ __attribute__((aligned(16))) float lds[2][512 * 32];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int64_t ld = J.Bp;
+  // instruction k of wave w: rows 128 w + 8 k + (lane >> 3), slot lane & 7 <- piece (lane & 7) ^ ((row >> 1) & 7)
+  //   = (lane & 7) ^ ((lane >> 4) & 3) ^ (4 (k & 1))
+  const int pe = (lane & 7) ^ ((lane >> 4) & 3);
+  // wave-uniform row base (SGPRs) + one 32-bit per-lane offset per instruction parity
+  // wave-uniform values forced into SGPRs (the job fields may arrive in VGPRs)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const float* wsel = wu < 2 ? J.A : J.X0;
+  const uint64_t wbits = (uint64_t)(size_t)wsel;
+  const uint64_t wbu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wbits) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wbits >> 32)) << 32);
+  const int64_t ldu = (int64_t)__builtin_amdgcn_readfirstlane((int)ld);  // Bp < 2^31
+  const int bbu = __builtin_amdgcn_readfirstlane(b_begin);
+  const float* wb = opaque(reinterpret_cast<const float*>((size_t)wbu) + (int64_t)(128 * (wu & 1)) * ldu + bbu);
+  const uint32_t off0 = (uint32_t)((lane >> 3) * ld + 4 * pe), off1 = off0 ^ 16u;  // pe ^ 4: 16 floats
+  // The DMA is issued by inline asm: for the builtin the compiler cannot tell the LDS-DMA's
+  // destination from the buffer being read and waits vmcnt(0) before every ds_read, which serialises
+  // the next step's loads with this step's MFMAs.  Here the only wait is the explicit one before the
+  // step's closing barrier (the loop holds no other vector-memory loads whose counts it could skew).
+  auto issue = [&](int t, int buf) {
+    const uint32_t dst = (uint32_t)(size_t)(lds_void*)&lds[buf][(128 * wu) * 32];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float* src = opaque(wb + ((int64_t)(8 * k) * ldu + 32 * t)) + ((k & 1) ? off1 : off0);
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst + 1024u * k)
+                   : "memory");
+    }
+  };
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sw = (c >> 1) & 7;  // the read-side swizzle of rows 32 b + c
+#pragma unroll 1
+  for (int t = 0; t < nsteps; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nsteps) issue(t + 1, buf ^ 1);  // the other buffer: every wave finished reading it before the last barrier
+    const float* L = lds[buf];
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {  // one sub-step's operands live at a time (the 256 AGPRs hold the tiles)
+      const int q0 = (4 * s + 2 * h) ^ sw, q1 = (4 * s + 2 * h + 1) ^ sw;
+      float4 ra[4][2], rx[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float* pa = L + (32 * (nb0 + i) + c) * 32;
+        const float* px = L + (256 + 32 * (kb0 + i) + c) * 32;
+        ra[i][0] = *reinterpret_cast<const float4*>(pa + 4 * q0);
+        ra[i][1] = *reinterpret_cast<const float4*>(pa + 4 * q1);
+        rx[i][0] = *reinterpret_cast<const float4*>(px + 4 * q0);
+        rx[i][1] = *reinterpret_cast<const float4*>(px + 4 * q1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float4 av = ra[i][p];
+          if (db) bs[i] += (av.x + av.y) + (av.z + av.w);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 xv = rx[j][p];
+            acc[i][j] = mfma(av.x, xv.x, acc[i][j]);
+            acc[i][j] = mfma(av.y, xv.y, acc[i][j]);
+            acc[i][j] = mfma(av.z, xv.z, acc[i][j]);
+            acc[i][j] = mfma(av.w, xv.w, acc[i][j]);
+          }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for step t+1 landed
+    __syncthreads();  // every wave's DMA landed and every wave is done with buffer t & 1
+  }
+}
+
 // BFK: the bf16 job sets (every job of a launch has the agent's bf16 flag); one kernel per
 // precision so each gets its own register allocation.
 template <bool BFK>
@@ -230,6 +320,11 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
     }                                                                           \
     break;
   if constexpr (!BFK) {
+#ifndef SPP_DW_NO_LDS
+    if (N == 256 && K == 256 && J.K1 == 0 && !wsp) {  // uniform over the workgroup (every wave: 4 x 4 blocks)
+      dw_big_lds(J, b_begin, nsteps / 2, nb0, kb0, db, acc, bs);
+    } else
+#endif
     switch (ni * 8 + nj) {
       SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)
       SPP_DW_CASE(2, 1) SPP_DW_CASE(2, 2) SPP_DW_CASE(2, 3) SPP_DW_CASE(2, 4)

@@ -99,6 +99,18 @@ int sppReplayObsStatsDPHistSize(sppReplayHandle h);
 sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot /*[ob], replicated*/,
                               double* sums /*[ob][2]*/, uint32_t* hist, int64_t n_global, float* mean, float* std,
                               float* max_obs, float* min_obs, int first_update, int* done, void* stream);
+/* The same statistics with ONE read of the local rows per call (sample-bracketed, like
+ * sppReplayObsStats): call phase = 0 .. 6 in order and run, on the host, between them:
+ *   after phase 0   all-gather `samp` across ranks (rank-major [world][ob][Sl] u32, Sl =
+ *                   sppReplayObsStatsDP1SampleRows; this rank wrote slot `rank`; in place)
+ *   after phase 1   all-reduce (sum) `exch` (fp64, 2*ob + 10*ob: moments, per-target counts)
+ *   after 2,3,4,5   all-reduce (sum) `hist` (uint32, ob*2*2*256)
+ * Phase 6 writes mean / std / max_obs / min_obs (identical on every rank).  Exact: a sample miss or an
+ * overflowed candidate list selects over the raw columns in the same fixed phases.  n_global < 2^31. */
+int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_global);
+sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot /*[ob]*/,
+                               uint32_t* samp, double* exch, uint32_t* hist, int64_t n_global, float* mean,
+                               float* std, float* max_obs, float* min_obs, int first_update, void* stream);
 /* Raw device pointers of the ring (for the fused sample+update path). */
 typedef struct {
   float* obs;          /* [capacity][ob]    */
@@ -259,6 +271,8 @@ sppStatus sppAllReduceGrads(sppAgentHandle h, int bucket, int world, void* rccl_
 /* In-place sum over the communicator of `count` elements (dtype 0 fp32, 1 fp64, 2 int32, 3 int64,
  * 4 uint32): the obs-statistics sums / counts of sppReplayObsStatsDP and the global row count. */
 sppStatus sppCommAllReduceSum(void* rccl_comm, void* buf_dev, int64_t count, int dtype, void* stream);
+/* Rank-major all-gather of `bytes` bytes per rank into recv (in place when send = recv + rank*bytes). */
+sppStatus sppCommAllGather(void* rccl_comm, const void* send_dev, void* recv_dev, int64_t bytes, void* stream);
 
 /* AcMTrainer.batch_update (rltoolkit/acm/acm.py:246-258): x [B][2ob], y [B][ac]
  * -> MSE loss (device float) and one Adam step on the bound ACM net. */

@@ -113,6 +113,7 @@ struct sppReplay {
   uint32_t *sf_samp = nullptr, *sf_bounds = nullptr, *sf_cpart = nullptr, *sf_wgl = nullptr, *sf_wgn = nullptr, *sf_ovf = nullptr,
            *sf_ovf_n = nullptr;
   double* sf_part = nullptr;
+  void* dp_q = nullptr;  // one-pass data-parallel statistics: per (column, target, rank) query state
 };
 
 extern "C" {
@@ -216,7 +217,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
   }
   hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_state); hipFree(h->st_hist);
   hipFree(h->sf_samp); hipFree(h->sf_bounds); hipFree(h->sf_part); hipFree(h->sf_cpart); hipFree(h->sf_wgl); hipFree(h->sf_wgn);
-  hipFree(h->sf_ovf); hipFree(h->sf_ovf_n);
+  hipFree(h->sf_ovf); hipFree(h->sf_ovf_n); hipFree(h->dp_q);
   delete h;
   return SPP_OK;
 }
@@ -472,10 +473,11 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   const int ns = (int)std::min<int64_t>(len, big ? kStSampBig : kStSampSmall);
   hipLaunchKernelGGL(k_st_sample, dim3(cdiv(ns, 256)), dim3(256), 0, st, h->d, len, ns, h->sf_samp);
   if (big)
-    hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns, h->sf_bounds);
+    hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns, h->sf_bounds,
+                       ns, (int64_t)0, 4);
   else
     hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns,
-                       h->sf_bounds);
+                       h->sf_bounds, ns, (int64_t)0, 4);
   const int cap = st_list_cap(ob);
   StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                 h->sf_ovf_n, cap};
@@ -483,6 +485,62 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   StSelArgs sa{h->d, len, nblk, cap, h->sf_part, h->sf_cpart, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                h->sf_ovf_n, nullptr, mean, std, max_obs, min_obs, first_update};
   hipLaunchKernelGGL(k_st_select, dim3(ob, 2), dim3(kStSelThreads), 0, st, sa);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// ---- data-parallel statistics, one data pass per call (stats.hip "data-parallel: one data pass")
+int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_global) {
+  if (!h || world < 1) return -1;
+  const int S = n_global > kStBigLen ? kStSampBig : kStSampSmall;
+  return std::max(1, S / world);
+}
+
+sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot, uint32_t* samp,
+                               double* exch, uint32_t* hist, int64_t n_global, float* mean, float* std,
+                               float* max_obs, float* min_obs, int first_update, void* stream) {
+  SPP_REQUIRE(h && pivot && samp && exch && hist && mean && std && max_obs && min_obs && phase >= 0 && phase <= 6 &&
+                  world >= 1 && rank >= 0 && rank < world,
+              SPP_E_INVALID_ARG, "obs_stats_dp1: bad args (phase %d, rank %d of %d)", phase, rank, world);
+  SPP_REQUIRE(n_global > 10 && n_global < ((int64_t)1 << 31), SPP_E_INVALID_ARG, "obs_stats_dp1: n_global %lld",
+              (long long)n_global);
+  const int ob = h->d.ob;
+  SPP_REQUIRE(ob <= 128, SPP_E_SHAPE, "obs_stats_dp1: ob %d > 128", ob);
+  const int64_t len = h->len;
+  const int nblk = st_nblk(h);
+  SPP_REQUIRE(len / ((int64_t)nblk * (kStPassThreads / 64) * st_groups(ob)) < 60000, SPP_E_INVALID_ARG,
+              "obs_stats_dp1: len too large");
+  sppStatus s = stats_fast_alloc(h);
+  if (s) return s;
+  if (!h->dp_q) SPP_CHECK_HIP(hipMalloc(&h->dp_q, sizeof(DpQuery) * ob * 4));
+  hipStream_t st = S(stream);
+  const int Sl = sppReplayObsStatsDP1SampleRows(h, world, n_global);
+  uint32_t* mine = samp + (int64_t)rank * ob * Sl;
+  const int cap = st_list_cap(ob);
+  StDpArgs da{h->d, len, n_global, nblk, cap, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf, h->sf_ovf_n,
+              exch, hist, (DpQuery*)h->dp_q, pivot, mean, std, max_obs, min_obs, first_update};
+  if (phase == 0) {
+    if (len > 0) hipLaunchKernelGGL(k_st_sample, dim3(cdiv(Sl, 256)), dim3(256), 0, st, h->d, len, Sl, mine);
+    else SPP_CHECK_HIP(hipMemsetAsync(mine, 0, sizeof(uint32_t) * ob * Sl, st));  // (lockstep shards: not reached)
+  } else if (phase == 1) {
+    const int S = world * Sl;  // <= kStSampBig
+    // margin 5 sigma + 4 sample ranks: a miss costs the raw-column select of the rounds, not correctness
+    if (S > kStSampSmall)
+      hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
+                         h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
+    else
+      hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
+                         h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
+    StPassArgs pa{h->d, len, h->sf_bounds, pivot, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
+                  h->sf_ovf_n, cap};
+    st_launch_pass(pa, nblk, st);
+    hipLaunchKernelGGL(k_dp_reduce, dim3(ob, 2), dim3(256), 0, st, ob, nblk, (const double*)h->sf_part,
+                       (const uint32_t*)h->sf_cpart, (const uint32_t*)h->sf_wgn, (const uint32_t*)h->sf_ovf_n, exch);
+  } else if (phase <= 5) {
+    hipLaunchKernelGGL(k_dp_round, dim3(ob, 2), dim3(kStSelThreads), 0, st, da, phase - 2);
+  } else {
+    hipLaunchKernelGGL(k_dp_final, dim3(ob, 2), dim3(1), 0, st, da);
+  }
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -2244,6 +2302,7 @@ struct Rccl {
   int (*init_rank)(void**, int, RcclUid, int) = nullptr;
   int (*destroy)(void*) = nullptr;
   int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*all_gather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
   int (*group_start)() = nullptr;
   int (*group_end)() = nullptr;
   const char* (*err)(int) = nullptr;
@@ -2262,10 +2321,11 @@ Rccl& rccl() {
   r.init_rank = (int (*)(void**, int, RcclUid, int))dlsym(lib, "ncclCommInitRank");
   r.destroy = (int (*)(void*))dlsym(lib, "ncclCommDestroy");
   r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(lib, "ncclAllReduce");
+  r.all_gather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(lib, "ncclAllGather");
   r.group_start = (int (*)())dlsym(lib, "ncclGroupStart");
   r.group_end = (int (*)())dlsym(lib, "ncclGroupEnd");
   r.err = (const char* (*)(int))dlsym(lib, "ncclGetErrorString");
-  r.ok = r.get_uid && r.init_rank && r.destroy && r.all_reduce && r.group_start && r.group_end && r.err;
+  r.ok = r.get_uid && r.init_rank && r.destroy && r.all_reduce && r.all_gather && r.group_start && r.group_end && r.err;
   return r;
 }
 constexpr int kNcclFloat32 = 7, kNcclSum = 0;
@@ -2323,6 +2383,16 @@ sppStatus sppCommAllReduceSum(void* comm, void* buf, int64_t count, int dtype, v
   static const int kType[5] = {7, 8, 2, 4, 3};
   if (count == 0) return SPP_OK;
   SPP_CHECK_RCCL(rccl().all_reduce(buf, buf, (size_t)count, kType[dtype], kNcclSum, comm, S(stream)));
+  return SPP_OK;
+}
+
+// Rank-major all-gather of `bytes` per rank (the one-pass statistics' sample exchange); in place when
+// send == recv + rank * bytes.
+sppStatus sppCommAllGather(void* comm, const void* send, void* recv, int64_t bytes, void* stream) {
+  SPP_REQUIRE(comm && send && recv && bytes >= 0, SPP_E_INVALID_ARG, "comm allgather: bad args");
+  SPP_REQUIRE(rccl().ok, SPP_E_RCCL, "librccl.so.1 not loadable");
+  if (bytes == 0) return SPP_OK;
+  SPP_CHECK_RCCL(rccl().all_gather(send, recv, (size_t)bytes, 0 /* ncclInt8 */, comm, S(stream)));
   return SPP_OK;
 }
 

@@ -81,6 +81,22 @@ __device__ __forceinline__ float fsub_rn(float a, float b) {
 }
 __device__ __forceinline__ float fdiv_rn(float a, float b) { return __fdiv_rn(a, b); }
 
+// numpy's _lerp of np.percentile(..., 'linear') between the order statistics a <= b at fraction g, with
+// its two separate fp64 roundings (a contracted fma can land on the other side of an fp32 rounding
+// midpoint of the final cast)
+__device__ __forceinline__ double np_lerp(double a, double b, double g) {
+#pragma clang fp contract(off)
+  const double diff = b - a;
+  return g >= 0.5 ? b - diff * (1.0 - g) : a + diff * g;
+}
+// its interpolation fraction: virtual index (n - 1) q rounded BEFORE the floor is taken off (a contracted
+// fma(q, n - 1, -floor) keeps the product's low bits and moves g by ~1e-12)
+__device__ __forceinline__ double np_frac(int64_t n, double q) {
+#pragma clang fp contract(off)
+  const double vi = (double)(n - 1) * q;
+  return vi - floor(vi);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

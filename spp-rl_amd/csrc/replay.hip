@@ -432,13 +432,10 @@ __global__ __launch_bounds__(256) void k_stats_sel(uint32_t* __restrict__ ghist,
       double res[2];
       const double qs[2] = {0.99, 0.01};
       for (int k = 0; k < 2; ++k) {
-        const double vi = (double)(len - 1) * qs[k];
-        const double lo = floor(vi);
-        const double g = vi - lo;
+        const double g = np_frac(len, qs[k]);
         const double a = (double)funkey(state[(c * 4 + 2 * k) * 3 + 0]);
         const double b = (double)funkey(state[(c * 4 + 2 * k + 1) * 3 + 0]);
-        const double diff = b - a;
-        res[k] = g >= 0.5 ? b - diff * (1.0 - g) : a + diff * g;  // numpy _lerp
+        res[k] = np_lerp(a, b, g);  // numpy _lerp
       }
       const float cmax = (float)res[0], cmin = (float)res[1];
       max_out[c] = first_update ? cmax : fmaxf(cmax, max_out[c]);

@@ -148,9 +148,12 @@ __global__ __launch_bounds__(256) void k_st_sample(ReplayDev r, int64_t len, int
 
 // bounds[(c*2 + t)*2 + {0,1}] = {lo, hi} keys of target t (0: 99th, 1: 1st percentile) from the
 // column's S sample keys (KPT per thread, coalesced reads of samp[c][:]).
+// The S keys of column c may come in segments (the data-parallel union sample, [world][ob][Sl] rank-major):
+// key j at samp[(j / Sl) * seg + c * Sl + j % Sl]; one segment (Sl = S) is the local [ob][S] sample.
 template <int KPT>
 __global__ __launch_bounds__(1024) void k_st_bracket(const uint32_t* __restrict__ samp, int S,
-                                                      uint32_t* __restrict__ bounds) {
+                                                      uint32_t* __restrict__ bounds, int Sl, int64_t seg,
+                                                      int mstd) {
   __shared__ __attribute__((aligned(16))) uint32_t hist[4 * 256 * kStCopies];
   __shared__ uint32_t qpre[4], qmask[4], qrank[4];
   __shared__ int qn;
@@ -159,15 +162,16 @@ __global__ __launch_bounds__(1024) void k_st_bracket(const uint32_t* __restrict_
   uint32_t v[KPT];
 #pragma unroll
   for (int i = 0; i < KPT; ++i) {
-    const int j = i * 1024 + tid;
-    v[i] = samp[(int64_t)c * S + (j < S ? j : S - 1)];
+    int j = i * 1024 + tid;
+    j = j < S ? j : S - 1;
+    v[i] = samp[(int64_t)(j / Sl) * seg + (int64_t)c * Sl + j % Sl];
   }
   if (tid == 0) {
     int n = 0;
     for (int t = 0; t < 2; ++t) {
       const double p = t == 0 ? 0.99 : 0.01;
       const int64_t f = (int64_t)floor(p * (double)(S - 1));
-      const int m = (int)ceil(4.0 * sqrt((double)S * p * (1.0 - p))) + 4;
+      const int m = (int)ceil(mstd * sqrt((double)S * p * (1.0 - p))) + 4;
       const int64_t lo_i = f - m, hi_i = f + 1 + m;
       // a bracket touching the sample's end extends to the key range's end (nothing outside)
       if (lo_i <= 0) {
@@ -620,16 +624,229 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
   if (nq > 0 && tid < nq) vals[qslot[tid]] = qpre[tid];
   __syncthreads();
   if (tid == 0) {
-    const double vi = (double)(n - 1) * (t ? 0.01 : 0.99);
-    const double g = vi - floor(vi);
+    const double g = np_frac(n, t ? 0.01 : 0.99);
     const double x0 = (double)funkey(vals[0]);
     const double x1 = (double)funkey(vals[1]);
-    const double diff = x1 - x0;
-    const float res = (float)(g >= 0.5 ? x1 - diff * (1.0 - g) : x0 + diff * g);  // numpy _lerp
+    const float res = (float)np_lerp(x0, x1, g);  // numpy _lerp
     if (t == 0) a.max_out[c] = a.first_update ? res : fmaxf(res, a.max_out[c]);
     else a.min_out[c] = a.first_update ? res : fminf(res, a.min_out[c]);
     a.ovf_n[ct] = 0;  // every reader of this counter is past the barrier above
   }
+}
+
+// ================================================================ data-parallel: one data pass
+// update_obs_mean_std over the union of the ranks' shards (replay_buffer.py:83-96) with ONE
+// read of the local rows per call (the host runs the collectives between the phases):
+//   phase 0  k_st_sample of Sl local rows into this rank's slot of samp [world][ob][Sl]   -> all-gather samp
+//   phase 1  k_st_bracket over the union sample (identical bounds on every rank), k_st_pass over the local
+//            rows (moments about the replicated pivot, far-side / bound counts, candidate lists), k_dp_reduce
+//            -> exch [ob][2] moments | [ob][2][kDpCnt] counts (fp64, exact)                -> all-reduce exch
+//   phases 2..5  k_dp_round r = 0..3: radix-select the two 'linear' ranks of each (column, target) in the
+//            union of the ranks' candidate lists, 8 bits per round (a rank outside the bracket -- a sample
+//            miss -- or an overflowed list selects over the raw column instead; 32 bits = 4 rounds either
+//            way); each round's [ob][2][2][256] histogram                                    -> all-reduce hist
+//   phase 6  k_dp_final: percentiles (numpy 'linear'), running max / min, mean / std.
+// Every rank runs the same kernels on the same reduced data, so every rank holds the same statistics.
+constexpr int kDpCnt = 5;  // per (column, target): outside, == lo, == hi, candidates, overflowed lists (flag)
+
+__global__ __launch_bounds__(256) void k_dp_reduce(int ob, int nblk, const double* __restrict__ part,
+                                                   const uint32_t* __restrict__ cpart, const uint32_t* __restrict__ wgn,
+                                                   const uint32_t* __restrict__ ovf_n, double* __restrict__ exch) {
+  const int c = blockIdx.x, t = blockIdx.y, ct = c * 2 + t, tid = threadIdx.x;
+  double m1 = 0.0, m2 = 0.0, cc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = tid; b < nblk; b += 256) {
+    if (t == 0) {
+      m1 += part[((int64_t)b * ob + c) * 2 + 0];
+      m2 += part[((int64_t)b * ob + c) * 2 + 1];
+    }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) cc[f] += (double)cpart[((int64_t)b * ob + c) * 6 + 3 * t + f];
+    cc[3] += (double)wgn[(int64_t)b * ob * 2 + ct];
+  }
+  __shared__ double red[6][256];
+  red[0][tid] = m1;
+  red[1][tid] = m2;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) red[2 + f][tid] = cc[f];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o)
+#pragma unroll
+      for (int f = 0; f < 6; ++f) red[f][tid] += red[f][tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (t == 0) {
+      exch[c * 2 + 0] = red[0][0];
+      exch[c * 2 + 1] = red[1][0];
+    }
+    double* e = exch + 2 * ob + (int64_t)ct * kDpCnt;
+    const uint32_t no = ovf_n[ct];
+    e[0] = red[2][0];
+    e[1] = red[3][0];
+    e[2] = red[4][0];
+    e[3] = red[5][0] + (double)min(no, (uint32_t)kStOvfCap);
+    e[4] = no > (uint32_t)kStOvfCap ? 1.0 : 0.0;
+  }
+}
+
+struct DpQuery {
+  uint32_t pre, mask, rank;
+  int src;  // 0: resolved (pre is the key), 1: candidate lists, 2: raw column
+};
+
+struct StDpArgs {
+  ReplayDev r;
+  int64_t len;         // local live rows
+  int64_t n_global;
+  int nblk, cap;
+  const uint32_t* bounds;
+  const uint32_t* wgl;
+  const uint32_t* wgn;
+  const uint32_t* ovf;
+  uint32_t* ovf_n;
+  const double* exch;  // all-reduced
+  uint32_t* hist;      // [ob][2][2][256], all-reduced between rounds
+  DpQuery* q;          // [ob][2][2] device state (replicated: every rank derives the same)
+  const float* pivot;
+  float *mean, *std, *max_out, *min_out;
+  int first_update;
+};
+
+// digit geometry of a query whose mask holds kb known top bits
+__device__ __forceinline__ void dp_digit(uint32_t mask, int& shift, int& dbits) {
+  const int kb = __popc(mask);
+  shift = kb >= 24 ? 0 : 24 - kb;
+  dbits = 32 - kb - shift;
+}
+
+// Advance query u of (c, t) with its reduced histogram of the last round (thread 0 of the workgroup).
+__device__ void dp_consume(DpQuery& Q, const uint32_t* h) {
+  if (Q.src == 0) return;
+  int shift, dbits;
+  dp_digit(Q.mask, shift, dbits);
+  const int nb = 1 << dbits;
+  uint32_t acc = 0;
+  int d = -1, last = 0;
+  for (int b = 0; b < nb; ++b) {
+    if (h[b]) last = b;
+    if (d < 0 && acc + h[b] > Q.rank) d = b;
+    else if (d < 0) acc += h[b];
+  }
+  if (d < 0) {  // rank past the set (inconsistent counts): the last non-empty bin
+    d = last;
+    acc = 0;
+    for (int b = 0; b < d; ++b) acc += h[b];
+  }
+  const uint32_t dm = (uint32_t)(nb - 1) << shift;
+  Q.pre = (Q.pre & ~dm) | ((uint32_t)d << shift);
+  Q.mask |= dm;
+  Q.rank -= acc;
+  if (Q.mask == 0xffffffffu) Q.src = 0;
+}
+
+// One round (r = 0..3): derive (r = 0) or advance (r > 0) the queries, then this rank's histogram of their
+// next digit.  Grid (ob, 2), kStSelThreads threads.
+__global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
+  constexpr int T = kStSelThreads;
+  __shared__ uint32_t hl[2][256 * kStCopies];
+  __shared__ DpQuery qs[2];
+  const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, ob = a.r.ob, ct = c * 2 + t;
+  DpQuery* qg = a.q + ct * 2;
+  uint32_t* hg = a.hist + (int64_t)ct * 2 * 256;
+  if (tid == 0) {
+    if (r == 0) {
+      const double* e = a.exch + 2 * ob + (int64_t)ct * kDpCnt;
+      const int64_t n = a.n_global, out = (int64_t)e[0], eql = (int64_t)e[1], eqh = (int64_t)e[2],
+                    ncd = (int64_t)e[3];
+      const bool cand_ok = e[4] == 0.0;
+      const uint32_t lo = a.bounds[ct * 2], hi = a.bounds[ct * 2 + 1];
+      const int64_t k0 = (int64_t)floor((double)(n - 1) * (t ? 0.01 : 0.99));
+      const int64_t start = t ? out : n - out - eqh - ncd - eql;
+      const int cp = __clz(lo ^ hi);
+      const uint32_t mk = cp >= 32 ? 0xffffffffu : (cp == 0 ? 0u : ~(0xffffffffu >> cp));
+      for (int u = 0; u < 2; ++u) {
+        const int64_t rk = u ? (k0 + 1 < n ? k0 + 1 : n - 1) : k0;
+        const int64_t jj = rk - start;
+        DpQuery Q;
+        if (jj >= 0 && jj < eql) {
+          Q = {lo, 0xffffffffu, 0, 0};
+        } else if (jj >= eql && jj < eql + ncd && cand_ok) {
+          Q = {lo & mk, mk, (uint32_t)(jj - eql), 1};
+          if (mk == 0xffffffffu) Q.src = 0;
+        } else if (jj >= eql + ncd && jj < eql + ncd + eqh) {
+          Q = {hi, 0xffffffffu, 0, 0};
+        } else {  // outside the bracket (a sample miss) or an overflowed list: the raw column
+          Q = {0u, 0u, (uint32_t)rk, 2};
+        }
+        qs[u] = Q;
+      }
+    } else {
+      for (int u = 0; u < 2; ++u) {
+        DpQuery Q = qg[u];
+        dp_consume(Q, hg + u * 256);
+        qs[u] = Q;
+      }
+    }
+    qg[0] = qs[0];
+    qg[1] = qs[1];
+  }
+  for (int i = tid; i < 2 * 256 * kStCopies; i += T) (&hl[0][0])[i] = 0;
+  __syncthreads();
+  const DpQuery q0 = qs[0], q1 = qs[1];
+  int sh[2], db[2];
+  dp_digit(q0.mask, sh[0], db[0]);
+  dp_digit(q1.mask, sh[1], db[1]);
+  const int cp = tid & (kStCopies - 1);
+  auto hit = [&](uint32_t k, int src) {
+    if (q0.src == src && (k & q0.mask) == q0.pre)
+      atomicAdd(&hl[0][(((k >> sh[0]) & ((1u << db[0]) - 1)) * kStCopies) + cp], 1u);
+    if (q1.src == src && (k & q1.mask) == q1.pre)
+      atomicAdd(&hl[1][(((k >> sh[1]) & ((1u << db[1]) - 1)) * kStCopies) + cp], 1u);
+  };
+  if (q0.src == 1 || q1.src == 1) {  // this rank's candidate keys of (c, t): the pass's lists + overflow
+    if (tid < a.nblk) {
+      const uint32_t nb = a.wgn[(int64_t)tid * ob * 2 + ct];
+      const uint32_t* L = a.wgl + ((int64_t)tid * ob * 2 + ct) * a.cap;
+      for (uint32_t i = 0; i < nb; ++i) hit(L[i], 1);
+    }
+    const uint32_t no = min(a.ovf_n[ct], (uint32_t)kStOvfCap);
+    const uint32_t* O = a.ovf + (int64_t)ct * kStOvfCap;
+    for (uint32_t i = tid; i < no; i += T) hit(O[i], 1);
+  }
+  if (q0.src == 2 || q1.src == 2) {  // the raw local column
+    const ReplayDev rr = a.r;
+    for (int64_t i = tid; i < a.len; i += T) hit(fkey(rr.obs[rr.obs_idx[i] * ob + c]), 2);
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * 256; i += T) {
+    const uint32_t* p = &hl[i >> 8][(i & 255) * kStCopies];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kStCopies; ++k) sum += p[k];
+    hg[i] = sum;
+  }
+}
+
+// Phase 6: the last round's histograms resolve every query; numpy 'linear' percentile, running max / min;
+// target 0 also writes mean / std from the all-reduced moments.  Grid (ob, 2), one thread each.
+__global__ void k_dp_final(StDpArgs a) {
+  const int c = blockIdx.x, t = blockIdx.y, ob = a.r.ob, ct = c * 2 + t;
+  DpQuery Q[2] = {a.q[ct * 2], a.q[ct * 2 + 1]};
+  for (int u = 0; u < 2; ++u) dp_consume(Q[u], a.hist + ((int64_t)ct * 2 + u) * 256);
+  const int64_t n = a.n_global;
+  if (t == 0) {
+    const double mu = a.exch[c * 2 + 0] / (double)n;
+    const double var = fmax(a.exch[c * 2 + 1] / (double)n - mu * mu, 0.0);
+    a.mean[c] = (float)((double)a.pivot[c] + mu);
+    a.std[c] = (float)sqrt(var);
+  }
+  const double g = np_frac(n, t ? 0.01 : 0.99);
+  const double x0 = (double)funkey(Q[0].pre), x1 = (double)funkey(Q[1].pre);
+  const float res = (float)np_lerp(x0, x1, g);  // numpy _lerp
+  if (t == 0) a.max_out[c] = a.first_update ? res : fmaxf(res, a.max_out[c]);
+  else a.min_out[c] = a.first_update ? res : fminf(res, a.min_out[c]);
+  a.ovf_n[ct] = 0;  // the local overflow lists were last read by round 3
 }
 
 }  // namespace spp

@@ -79,6 +79,7 @@ _SIGS = {
     "sppCommDestroy": (c_int, [c_void_p]),
     "sppAllReduceGrads": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sppCommAllReduceSum": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "sppCommAllGather": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "sppAgentCreate": (c_int, [P(c_void_p), P(AgentConfig), c_int]),
     "sppAgentDestroy": (c_int, [c_void_p]),
     "sppAgentNetSize": (c_int, [c_void_p, c_int, P(c_int64)]),
@@ -138,6 +139,9 @@ _SIGS = {
     "sppReplayObsStatsDPHistSize": (c_int, [c_void_p]),
     "sppReplayObsStatsDP": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, P(c_int), c_void_p]),
+    "sppReplayObsStatsDP1SampleRows": (c_int, [c_void_p, c_int, c_int64]),
+    "sppReplayObsStatsDP1": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "sppObsNormalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                 c_void_p, c_void_p]),
     "sppAdvSums": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),

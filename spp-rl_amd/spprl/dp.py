@@ -52,6 +52,27 @@ def make_allreduce_sum(group=None):
     return allreduce_sum
 
 
+class _AllGather:
+    """Rank-major all-gather over a torch.distributed group: ``ag(out, inp)`` with out = world x inp
+    (inp may be this rank's slice of out); ``world`` / ``rank`` of the group."""
+
+    def __init__(self, group):
+        self.group, self.world, self.rank = group, dist.get_world_size(group), dist.get_rank(group)
+
+    def __call__(self, out, inp):
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+
+
+def make_allgather(group=None):
+    """The one-pass obs-statistics sample exchange (spprl.replay.update_obs_mean_std_dp) or None with a
+    single rank."""
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    if dist.get_world_size(group) == 1 and not _single_rank_exchange():
+        return None
+    return _AllGather(group)
+
+
 _HOST_GROUPS = {}
 
 
@@ -149,6 +170,13 @@ class NativeComm:
         self.allreduce_sum(t)
         return [int(v) for v in t.tolist()] if many else int(t.item())
 
+    def allgather(self, out, inp):
+        """Rank-major all-gather of device tensors over the communicator (sppCommAllGather)."""
+        from . import _lib
+
+        _lib.call("sppCommAllGather", self.comm, _lib.ptr(inp), _lib.ptr(out), inp.numel() * inp.element_size(),
+                  _lib.stream_handle())
+
     def attach(self, agent):
         """Run ``agent``'s data-parallel exchange over this communicator: gradient buckets, the
         obs-statistics sums and the row counts (all three are needed: with the gradients averaged but the
@@ -156,7 +184,11 @@ class NativeComm:
         agent.allreduce = self.allreduce_for(agent)
         agent.allreduce_sum = self.allreduce_sum
         agent.host_sum = self.host_sum
+        agent.allgather = self  # world / rank / __call__ (one-pass obs statistics)
         return agent
+
+    def __call__(self, out, inp):
+        self.allgather(out, inp)
 
     def allreduce_for(self, agent):
         """``allreduce(bucket)`` over the agent's exchange buckets (bucket_critic / _actor / _acm),

@@ -211,7 +211,7 @@ class BufferAcMOffPolicy:
              ptr(self.min_obs), 0 if self._have_minmax else 1, stream_handle())
         self._have_minmax = True
 
-    def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None):
+    def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None, allgather=None):
         """update_obs_mean_std over the union of the data-parallel ranks' shards (SURVEY.md
         §8e): ``allreduce_sum(t)`` sums a device tensor in place across ranks (RCCL).  Exact
         global percentiles (radix select on all-reduced histograms); mean / std from fp64
@@ -222,7 +222,12 @@ class BufferAcMOffPolicy:
         through ``allreduce_sum`` (one host sync).  The ranks write timesteps in lockstep, so the
         count of timestep writes is the same on every rank and all of them reuse the cached total
         between writes (the bench's reference-rate stats run several passes per vector step on
-        unchanged shards)."""
+        unchanged shards).
+
+        With ``allgather`` (spprl.dp.make_allgather / NativeComm.allgather: rank-major all-gather with
+        ``world`` / ``rank`` attributes) the call reads the local rows ONCE (sppReplayObsStatsDP1: union
+        sample all-gathered, one bracketed pass, one all-reduce of moments and counts, four all-reduces of
+        candidate histograms); without it, the stepwise radix protocol (4-5 passes over the rows)."""
         if n_global is None:
             gen = getattr(self, "_gen", 0)
             if getattr(self, "_ng_gen", None) != gen:
@@ -242,6 +247,8 @@ class BufferAcMOffPolicy:
             n_global = self._ng
         if n_global <= 10:  # replay_buffer.py:84, on the global buffer
             return
+        if allgather is not None:
+            return self._obs_stats_dp1(allreduce_sum, allgather, n_global)
         if getattr(self, "_dp_hist", None) is None:
             hs = _lib.load().sppReplayObsStatsDPHistSize(self._h)
             self._dp_hist = torch.zeros(hs, dtype=torch.int32, device=self.device)
@@ -258,6 +265,32 @@ class BufferAcMOffPolicy:
                 self._dp_hist[:top].copy_(buf[2 * ob:].to(torch.int32))
             else:
                 allreduce_sum(self._dp_hist)
+
+    def _obs_stats_dp1(self, allreduce_sum, allgather, n_global):
+        """The one-pass protocol (sppReplayObsStatsDP1 phases 0..6 with the collectives between)."""
+        W, R, ob = allgather.world, allgather.rank, self.obs_shape
+        Sl = _lib.load().sppReplayObsStatsDP1SampleRows(self._h, W, n_global)
+        key = (W, Sl)
+        if getattr(self, "_dp1_key", None) != key:
+            self._dp1_samp = torch.zeros(W * ob * Sl, dtype=torch.int32, device=self.device)
+            self._dp1_exch = torch.zeros(12 * ob, dtype=torch.float64, device=self.device)
+            self._dp1_hist = torch.zeros(ob * 1024, dtype=torch.int32, device=self.device)
+            self._dp1_pivot = torch.zeros(ob, device=self.device)
+            self._dp1_key = key
+        self._dp1_pivot.copy_(self.obs_mean)  # replicated across ranks
+        first = 0 if self._have_minmax else 1
+        mine = self._dp1_samp[R * ob * Sl:(R + 1) * ob * Sl]
+        for phase in range(7):
+            call("sppReplayObsStatsDP1", self._h, phase, W, R, ptr(self._dp1_pivot), ptr(self._dp1_samp),
+                 ptr(self._dp1_exch), ptr(self._dp1_hist), n_global, ptr(self.obs_mean), ptr(self.obs_std),
+                 ptr(self.max_obs), ptr(self.min_obs), first, stream_handle())
+            if phase == 0:
+                allgather(self._dp1_samp, mine)
+            elif phase == 1:
+                allreduce_sum(self._dp1_exch)
+            elif phase <= 5:
+                allreduce_sum(self._dp1_hist)
+        self._have_minmax = True
 
     def obs_stats_dp_steps(self, n_global):
         """Generator over the stepwise protocol: yields after each step whose outputs

@@ -39,7 +39,7 @@ import torch
 
 from . import config
 from ._lib import call, ptr, stream_handle
-from .dp import make_allreduce, make_allreduce_sum, make_host_allreduce_sum, stream_key
+from .dp import make_allgather, make_allreduce, make_allreduce_sum, make_host_allreduce_sum, stream_key
 
 # ---------------------------------------------------------------- stats
 
@@ -342,12 +342,13 @@ class OffPolicyLoop:
         if self.schedule not in ("reference", "fused"):
             raise ValueError("schedule must be 'reference' or 'fused'")
         self.allreduce = allreduce if allreduce is not None else make_allreduce()
-        self.allreduce_sum = self.host_sum = None
+        self.allreduce_sum = self.host_sum = self.allgather = None
         if self.allreduce is not None:
             # the obs statistics must be global whenever the gradients are (else the replicas' normalisers
             # drift apart): an explicit gradient exchange needs its statistics exchange too
             self.allreduce_sum = allreduce_sum if allreduce_sum is not None else make_allreduce_sum()
             self.host_sum = host_sum if host_sum is not None else make_host_allreduce_sum()
+            self.allgather = make_allgather()  # one-pass statistics (None: the stepwise protocol)
             if self.allreduce_sum is None:
                 raise ValueError("an explicit allreduce needs allreduce_sum (and host_sum) for the global obs "
                                  "statistics, e.g. spprl.dp.NativeComm(...).attach(agent) or torch.distributed")
@@ -443,7 +444,8 @@ class OffPolicyLoop:
             # shard lengths differ across ranks once resets (early terminations) advance the
             # obs rings unevenly: the global row count is all-reduced, never assumed
             # (counted on the host and exchanged over gloo: no device synchronisation per step)
-            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, host_sum=getattr(self, "host_sum", None))
+            self.replay_buffer.update_obs_mean_std_dp(self.allreduce_sum, host_sum=getattr(self, "host_sum", None),
+                                                      allgather=getattr(self, "allgather", None))
         else:
             self.replay_buffer.update_obs_mean_std()
 

@@ -516,3 +516,62 @@ def test_sac_acm_update_bf16_mlp_within_bf16_tolerance(env_name, ob, ac):
     gl = ag.loss
     for k in ("critic_1", "critic_2", "actor"):
         assert abs(gl[k] - ol[k]) <= 3e-2 * abs(ol[k]) + 1e-3, (k, gl[k], ol[k])
+
+
+@pytest.mark.parametrize("ob,ranks,kind", [(11, 2, "t3"), (17, 4, "t3"), (111, 3, "t3"), (11, 4, "skew"),
+                                           (17, 2, "ties"), (11, 8, "t3")])
+def test_obs_stats_one_pass_protocol_matches_union(ob, ranks, kind):
+    """sppReplayObsStatsDP1 (the one-pass protocol) over W shards, its all-gather / all-reduces emulated here
+    on one GPU between the phases, equals numpy on the union of the shards: percentiles and max/min
+    bit-exact, mean / std rtol 1e-6, the same statistics on every shard.  "skew": unequal shifted shards,
+    so the union sample (equal rows per shard) brackets the wrong place and the raw-column rounds must
+    carry the selection; "ties": discrete values (long runs at the bracket bounds)."""
+    rng = np.random.RandomState(ob + ranks)
+    if kind == "skew":
+        data = [(rng.randn(2000 * (1 + 5 * r), ob) * (0.5 + r) + 3.0 * r).astype(np.float32) for r in range(ranks)]
+    elif kind == "ties":
+        data = [np.round(rng.randn(7000 + 1000 * r, ob) * 2).astype(np.float32) for r in range(ranks)]
+    else:
+        data = [(rng.standard_t(3, size=(5000 + 997 * r, ob)) * rng.uniform(0.5, 3, ob) + rng.randn(ob))
+                .astype(np.float32) for r in range(ranks)]
+
+    def buf(rows):
+        rb = spprl.BufferAcMOffPolicy(len(rows) + 8, ob, ob, 2, device=DEV, min_max_denormalize=True)
+        sl = rb.add_obs_batch(torch.from_numpy(np.concatenate([rows, rows[:1]])))
+        n = len(rows)
+        z = np.zeros(n, bool)
+        rb.add_timestep_batch(sl[:n], sl[1:], torch.zeros(n, ob), np.zeros(n, np.float32), z, z,
+                              torch.zeros(n, 2))
+        return rb
+
+    shards = [buf(d) for d in data]
+    pivot = torch.from_numpy(rng.randn(ob).astype(np.float32)).to(DEV)
+    n_global = sum(len(d) for d in data)
+    W = ranks
+    Sl = _lib.load().sppReplayObsStatsDP1SampleRows(shards[0]._h, W, n_global)
+    st = _lib.stream_handle()
+    bufs = [dict(samp=torch.zeros(W * ob * Sl, dtype=torch.int32, device=DEV),
+                 exch=torch.zeros(12 * ob, dtype=torch.float64, device=DEV),
+                 hist=torch.zeros(ob * 1024, dtype=torch.int32, device=DEV)) for _ in shards]
+    for phase in range(7):
+        for r, rb in enumerate(shards):
+            b = bufs[r]
+            _lib.call("sppReplayObsStatsDP1", rb._h, phase, W, r, _lib.ptr(pivot), _lib.ptr(b["samp"]),
+                      _lib.ptr(b["exch"]), _lib.ptr(b["hist"]), n_global, _lib.ptr(rb.obs_mean), _lib.ptr(rb.obs_std),
+                      _lib.ptr(rb.max_obs), _lib.ptr(rb.min_obs), 1, st)
+        if phase == 0:  # all-gather: every rank's slot into every buffer
+            allg = torch.cat([bufs[r]["samp"][r * ob * Sl:(r + 1) * ob * Sl] for r in range(W)])
+            for b in bufs:
+                b["samp"].copy_(allg)
+        elif phase <= 5:  # all-reduce (sum)
+            k = "exch" if phase == 1 else "hist"
+            tot = sum(b[k] for b in bufs)
+            for b in bufs:
+                b[k].copy_(tot)
+    torch.cuda.synchronize()
+    allx = np.concatenate(data).astype(np.float64)
+    for rb in shards:
+        np.testing.assert_array_equal(rb.max_obs.cpu().numpy(), np.percentile(allx, 99, axis=0).astype(np.float32))
+        np.testing.assert_array_equal(rb.min_obs.cpu().numpy(), np.percentile(allx, 1, axis=0).astype(np.float32))
+        np.testing.assert_allclose(rb.obs_mean.cpu().numpy(), allx.mean(0).astype(np.float32), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(rb.obs_std.cpu().numpy(), allx.std(0).astype(np.float32), rtol=1e-6)

@@ -294,7 +294,7 @@ def test_dp_obs_stats_count_is_all_reduced_not_assumed():
     calls = []
 
     class RB(_FakeRB):
-        def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None):
+        def update_obs_mean_std_dp(self, allreduce_sum, n_global=None, host_sum=None, allgather=None):
             calls.append((n_global, host_sum))
 
     def host_sum(x):  # the shard lengths are summed on the host (spprl.dp.make_host_allreduce_sum)

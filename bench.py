@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic null)")
     ap.add_argument("--no-rocprof", action="store_true",
                     help="skip the rocprofv3 --kernel-trace child run (roofline.frac_rocprof null)")
+    ap.add_argument("--dp-comm", choices=["native", "torch"], default="native",
+                    help="N > 1 exchange: libspprl's own RCCL communicator on the compute stream (gradient buckets, "
+                         "obs-statistics collectives) or torch.distributed's (its own stream + event waits)")
     ap.add_argument("--host-env", action="store_true",
                     help="step the envs on the host CPU (HostSynthEnv: vectorised numpy SynthEnv behind pinned "
                          "staging + side-stream copies, the update overlapping the host step): the PCIe-inclusive "
@@ -509,6 +512,19 @@ def prefill(ag, rb, cap, E, ob, ac, aout, seed, dev, acm=True):
     return fill
 
 
+def native_comm(world, rank, local):
+    """libspprl's RCCL communicator (spprl.dp.NativeComm): its collectives run on the caller's stream,
+    so the exchange needs no cross-stream event waits; rank 0's id travels by a process-group broadcast."""
+    from spprl.dp import NativeComm
+
+    def share(uid):
+        box = [uid if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    return NativeComm(rank, world, local, share)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -565,6 +581,12 @@ def main():
     rb = ag.replay_buffer
     if sched == "fused":
         assert ag.fused_batch_sizes()[0] == B
+    comm = None
+    if distributed and backend == "nccl" and args.dp_comm == "native":
+        comm = native_comm(world, rank, local)
+        host_sum = ag.host_sum  # the live-row counts stay on gloo (host integers: no device read)
+        comm.attach(ag)
+        ag.host_sum = host_sum
 
     fill = prefill(ag, rb, cap, E, ob, ac, aout, seed, dev, acm=not vanilla)
     ag.update_obs_stats()
@@ -704,8 +726,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_report(args.config, args.cpu_seconds,
                                                      args.cpu_procs or default_cpu_procs())
+    if distributed:
+        result["config"]["dp_comm"] = "native RCCL (libspprl, compute stream)" if comm else "torch.distributed"
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -106,7 +106,8 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot /*
  *   after phase 1   all-reduce (sum) `exch` (fp64, 2*ob + 10*ob: moments, per-target counts)
  *   after 2,3,4,5   all-reduce (sum) `hist` (uint32, ob*2*2*256)
  * Phase 6 writes mean / std / max_obs / min_obs (identical on every rank).  Exact: a sample miss or an
- * overflowed candidate list selects over the raw columns in the same fixed phases.  n_global < 2^31. */
+ * overflowed candidate list selects over the raw columns in the same fixed phases.  n_global < 2^31.
+ * `pivot` (replicated) may alias `mean`: phase 6 reads pivot[c] before it writes mean[c]. */
 int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_global);
 sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot /*[ob]*/,
                                uint32_t* samp, double* exch, uint32_t* hist, int64_t n_global, float* mean,

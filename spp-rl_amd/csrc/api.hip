@@ -114,6 +114,7 @@ struct sppReplay {
            *sf_ovf_n = nullptr;
   double* sf_part = nullptr;
   void* dp_q = nullptr;  // one-pass data-parallel statistics: per (column, target, rank) query state
+  uint32_t* dp_cand = nullptr;  // and the compacted local candidates + counts
 };
 
 extern "C" {
@@ -217,7 +218,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
   }
   hipFree(h->st_part); hipFree(h->st_mean); hipFree(h->st_state); hipFree(h->st_hist);
   hipFree(h->sf_samp); hipFree(h->sf_bounds); hipFree(h->sf_part); hipFree(h->sf_cpart); hipFree(h->sf_wgl); hipFree(h->sf_wgn);
-  hipFree(h->sf_ovf); hipFree(h->sf_ovf_n); hipFree(h->dp_q);
+  hipFree(h->sf_ovf); hipFree(h->sf_ovf_n); hipFree(h->dp_q); hipFree(h->dp_cand);
   delete h;
   return SPP_OK;
 }
@@ -512,13 +513,17 @@ sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank
               "obs_stats_dp1: len too large");
   sppStatus s = stats_fast_alloc(h);
   if (s) return s;
-  if (!h->dp_q) SPP_CHECK_HIP(hipMalloc(&h->dp_q, sizeof(DpQuery) * ob * 4));
+  if (!h->dp_q) {
+    SPP_CHECK_HIP(hipMalloc(&h->dp_q, sizeof(DpQuery) * ob * 4));
+    SPP_CHECK_HIP(hipMalloc(&h->dp_cand, sizeof(uint32_t) * ((size_t)ob * 2 * kDpCandCap + ob * 2)));
+  }
+  uint32_t* dp_ncand = h->dp_cand + (size_t)ob * 2 * kDpCandCap;
   hipStream_t st = S(stream);
   const int Sl = sppReplayObsStatsDP1SampleRows(h, world, n_global);
   uint32_t* mine = samp + (int64_t)rank * ob * Sl;
   const int cap = st_list_cap(ob);
   StDpArgs da{h->d, len, n_global, nblk, cap, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf, h->sf_ovf_n,
-              exch, hist, (DpQuery*)h->dp_q, pivot, mean, std, max_obs, min_obs, first_update};
+              h->dp_cand, dp_ncand, exch, hist, (DpQuery*)h->dp_q, pivot, mean, std, max_obs, min_obs, first_update};
   if (phase == 0) {
     if (len > 0) hipLaunchKernelGGL(k_st_sample, dim3(cdiv(Sl, 256)), dim3(256), 0, st, h->d, len, Sl, mine);
     else SPP_CHECK_HIP(hipMemsetAsync(mine, 0, sizeof(uint32_t) * ob * Sl, st));  // (lockstep shards: not reached)
@@ -534,12 +539,13 @@ sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank
     StPassArgs pa{h->d, len, h->sf_bounds, pivot, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                   h->sf_ovf_n, cap};
     st_launch_pass(pa, nblk, st);
-    hipLaunchKernelGGL(k_dp_reduce, dim3(ob, 2), dim3(256), 0, st, ob, nblk, (const double*)h->sf_part,
-                       (const uint32_t*)h->sf_cpart, (const uint32_t*)h->sf_wgn, (const uint32_t*)h->sf_ovf_n, exch);
+    hipLaunchKernelGGL(k_dp_reduce, dim3(ob, 2), dim3(kStSelThreads), 0, st, ob, nblk, cap, (const double*)h->sf_part,
+                       (const uint32_t*)h->sf_cpart, (const uint32_t*)h->sf_wgl, (const uint32_t*)h->sf_wgn,
+                       (const uint32_t*)h->sf_ovf, (const uint32_t*)h->sf_ovf_n, exch, h->dp_cand, dp_ncand);
   } else if (phase <= 5) {
     hipLaunchKernelGGL(k_dp_round, dim3(ob, 2), dim3(kStSelThreads), 0, st, da, phase - 2);
   } else {
-    hipLaunchKernelGGL(k_dp_final, dim3(ob, 2), dim3(1), 0, st, da);
+    hipLaunchKernelGGL(k_dp_final, dim3(ob, 2), dim3(128), 0, st, da);
   }
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;

@@ -649,44 +649,110 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
 // Every rank runs the same kernels on the same reduced data, so every rank holds the same statistics.
 constexpr int kDpCnt = 5;  // per (column, target): outside, == lo, == hi, candidates, overflowed lists (flag)
 
-__global__ __launch_bounds__(256) void k_dp_reduce(int ob, int nblk, const double* __restrict__ part,
-                                                   const uint32_t* __restrict__ cpart, const uint32_t* __restrict__ wgn,
-                                                   const uint32_t* __restrict__ ovf_n, double* __restrict__ exch) {
-  const int c = blockIdx.x, t = blockIdx.y, ct = c * 2 + t, tid = threadIdx.x;
-  double m1 = 0.0, m2 = 0.0, cc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int b = tid; b < nblk; b += 256) {
+constexpr int kDpCandCap = 32768;  // compacted local candidates per (column, target); more: the rounds walk the lists
+
+// Grid (ob, 2), kStSelThreads threads: the pass's slabs -> exch (this rank's moments and counts), and this
+// rank's candidate keys of (column, target) compacted to cand[ct][0 .. ncand) (block prefix sum over the
+// workgroup lists, then the overflow list) so every round reads them with the whole workgroup.
+__global__ __launch_bounds__(kStSelThreads) void k_dp_reduce(int ob, int nblk, int cap, const double* __restrict__ part,
+                                                            const uint32_t* __restrict__ cpart,
+                                                            const uint32_t* __restrict__ wgl,
+                                                            const uint32_t* __restrict__ wgn,
+                                                            const uint32_t* __restrict__ ovf,
+                                                            const uint32_t* __restrict__ ovf_n, double* __restrict__ exch,
+                                                            uint32_t* __restrict__ cand, uint32_t* __restrict__ ncand) {
+  constexpr int T = kStSelThreads, NW = T / 64;
+  const int c = blockIdx.x, t = blockIdx.y, ct = c * 2 + t, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = tid;  // thread b owns pass workgroup b (nblk <= kStNblkMax = T)
+  double m1 = 0.0, m2 = 0.0;
+  uint32_t cc[3] = {0, 0, 0}, nb = 0;
+  if (b < nblk) {
     if (t == 0) {
-      m1 += part[((int64_t)b * ob + c) * 2 + 0];
-      m2 += part[((int64_t)b * ob + c) * 2 + 1];
+      m1 = part[((int64_t)b * ob + c) * 2 + 0];
+      m2 = part[((int64_t)b * ob + c) * 2 + 1];
     }
 #pragma unroll
-    for (int f = 0; f < 3; ++f) cc[f] += (double)cpart[((int64_t)b * ob + c) * 6 + 3 * t + f];
-    cc[3] += (double)wgn[(int64_t)b * ob * 2 + ct];
+    for (int f = 0; f < 3; ++f) cc[f] = cpart[((int64_t)b * ob + c) * 6 + 3 * t + f];
+    nb = wgn[(int64_t)b * ob * 2 + ct];
   }
-  __shared__ double red[6][256];
-  red[0][tid] = m1;
-  red[1][tid] = m2;
+  uint32_t incl = nb;  // inclusive wave scan of the list lengths
 #pragma unroll
-  for (int f = 0; f < 4; ++f) red[2 + f][tid] = cc[f];
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  m1 = wave_sum_d(m1);
+  m2 = wave_sum_d(m2);
+#pragma unroll
+  for (int f = 0; f < 3; ++f)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cc[f] += __shfl_xor(cc[f], o, 64);
+  __shared__ double rd[2][NW];
+  __shared__ uint32_t rc[4][NW];
+  if (lane == 63) rc[3][wv] = incl;
+  if (lane == 0) {
+    rd[0][wv] = m1;
+    rd[1][wv] = m2;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) rc[f][wv] = cc[f];
+  }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o)
+  uint32_t woff = 0, tot = 0;
+  for (int q = 0; q < NW; ++q) {
+    if (q < wv) woff += rc[3][q];
+    tot += rc[3][q];
+  }
+  const uint32_t no_raw = ovf_n[ct], no = min(no_raw, (uint32_t)kStOvfCap);
+  const uint32_t n_all = tot + no;
+  uint32_t* dst = cand + (int64_t)ct * kDpCandCap;
+  __shared__ uint32_t offs[T + 1];  // exclusive list offsets; offs[nblk] = tot
+  offs[b] = woff + incl - nb;
+  if (b == T - 1) offs[T] = tot;
+  __syncthreads();
+  if (n_all <= (uint32_t)kDpCandCap) {  // key i: binary search of its list in offs, then an independent load
+    constexpr int B = 8;  // keys in flight per thread: the loads of a batch are independent
+    for (uint32_t i0 = tid; i0 < tot; i0 += B * T) {
+      uint32_t v[B];
 #pragma unroll
-      for (int f = 0; f < 6; ++f) red[f][tid] += red[f][tid + o];
-    __syncthreads();
+      for (int k = 0; k < B; ++k) {
+        const uint32_t i = i0 + k * T;
+        if (i < tot) {
+          int lo = 0, hi = nblk - 1;  // the last list with offs <= i (empty lists share offsets: the last)
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (offs[mid] <= i) lo = mid;
+            else hi = mid - 1;
+          }
+          v[k] = wgl[((int64_t)lo * ob * 2 + ct) * cap + (i - offs[lo])];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k)
+        if (i0 + k * T < tot) dst[i0 + k * T] = v[k];
+    }
+    const uint32_t* O = ovf + (int64_t)ct * kStOvfCap;
+    for (uint32_t i = tid; i < no; i += T) dst[tot + i] = O[i];
   }
   if (tid == 0) {
+    double s1 = 0.0, s2 = 0.0, out = 0.0, eql = 0.0, eqh = 0.0;
+    for (int q = 0; q < NW; ++q) {
+      s1 += rd[0][q];
+      s2 += rd[1][q];
+      out += rc[0][q];
+      eql += rc[1][q];
+      eqh += rc[2][q];
+    }
     if (t == 0) {
-      exch[c * 2 + 0] = red[0][0];
-      exch[c * 2 + 1] = red[1][0];
+      exch[c * 2 + 0] = s1;
+      exch[c * 2 + 1] = s2;
     }
     double* e = exch + 2 * ob + (int64_t)ct * kDpCnt;
-    const uint32_t no = ovf_n[ct];
-    e[0] = red[2][0];
-    e[1] = red[3][0];
-    e[2] = red[4][0];
-    e[3] = red[5][0] + (double)min(no, (uint32_t)kStOvfCap);
-    e[4] = no > (uint32_t)kStOvfCap ? 1.0 : 0.0;
+    e[0] = out;
+    e[1] = eql;
+    e[2] = eqh;
+    e[3] = (double)n_all;
+    e[4] = no_raw > (uint32_t)kStOvfCap ? 1.0 : 0.0;
+    ncand[ct] = n_all <= (uint32_t)kDpCandCap ? n_all : 0xffffffffu;  // all-ones: walk the lists
   }
 }
 
@@ -705,6 +771,8 @@ struct StDpArgs {
   const uint32_t* wgn;
   const uint32_t* ovf;
   uint32_t* ovf_n;
+  const uint32_t* cand;   // [ob][2][kDpCandCap] compacted local candidates (k_dp_reduce)
+  const uint32_t* ncand;  // [ob][2] their count (all-ones: walk the pass's lists)
   const double* exch;  // all-reduced
   uint32_t* hist;      // [ob][2][2][256], all-reduced between rounds
   DpQuery* q;          // [ob][2][2] device state (replicated: every rank derives the same)
@@ -745,6 +813,69 @@ __device__ void dp_consume(DpQuery& Q, const uint32_t* h) {
   if (Q.mask == 0xffffffffu) Q.src = 0;
 }
 
+// dp_consume by one whole wave over an LDS copy of the histogram: lane l holds bins 4l..4l+3, a wave scan of
+// their sums finds the digit's lane (every lane returns the same query).
+__device__ DpQuery dp_consume_wave(DpQuery Q, const uint32_t* h, int lane) {
+  if (Q.src == 0) return Q;
+  int shift, dbits;
+  dp_digit(Q.mask, shift, dbits);
+  const int nb = 1 << dbits;
+  uint32_t v[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = 4 * lane + k < nb ? h[4 * lane + k] : 0u;
+    s += v[k];
+  }
+  uint32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += x;
+  }
+  const uint32_t excl = incl - s;
+  const uint64_t hitm = __ballot(excl <= Q.rank && Q.rank < incl);
+  int L, d = 0;
+  uint32_t acc = 0;
+  if (hitm) {
+    L = __ffsll((unsigned long long)hitm) - 1;
+    int dd = 4 * lane + 3;
+    uint32_t a = excl, run = excl;
+    bool f = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // first bin whose running sum passes the rank
+      if (!f && run + v[k] > Q.rank) {
+        dd = 4 * lane + k;
+        a = run;
+        f = true;
+      }
+      run += v[k];
+    }
+    d = __shfl(dd, L, 64);
+    acc = __shfl(a, L, 64);
+  } else {  // rank past the set (inconsistent counts): the last non-empty bin
+    const uint64_t nz = __ballot(s != 0);
+    L = nz ? 63 - __clzll((long long)nz) : 0;
+    int dd = 4 * lane;
+    uint32_t a = excl, run = excl;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (v[k]) {
+        dd = 4 * lane + k;
+        a = run;
+      }
+      run += v[k];
+    }
+    d = __shfl(dd, L, 64);
+    acc = __shfl(a, L, 64);
+  }
+  const uint32_t dm = (uint32_t)(nb - 1) << shift;
+  Q.pre = (Q.pre & ~dm) | ((uint32_t)d << shift);
+  Q.mask |= dm;
+  Q.rank -= acc;
+  if (Q.mask == 0xffffffffu) Q.src = 0;
+  return Q;
+}
+
 // One round (r = 0..3): derive (r = 0) or advance (r > 0) the queries, then this rank's histogram of their
 // next digit.  Grid (ob, 2), kStSelThreads threads.
 __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
@@ -754,8 +885,8 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
   const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x, ob = a.r.ob, ct = c * 2 + t;
   DpQuery* qg = a.q + ct * 2;
   uint32_t* hg = a.hist + (int64_t)ct * 2 * 256;
-  if (tid == 0) {
-    if (r == 0) {
+  if (r == 0) {
+    if (tid == 0) {
       const double* e = a.exch + 2 * ob + (int64_t)ct * kDpCnt;
       const int64_t n = a.n_global, out = (int64_t)e[0], eql = (int64_t)e[1], eqh = (int64_t)e[2],
                     ncd = (int64_t)e[3];
@@ -780,16 +911,22 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
           Q = {0u, 0u, (uint32_t)rk, 2};
         }
         qs[u] = Q;
-      }
-    } else {
-      for (int u = 0; u < 2; ++u) {
-        DpQuery Q = qg[u];
-        dp_consume(Q, hg + u * 256);
-        qs[u] = Q;
+        qg[u] = Q;
       }
     }
-    qg[0] = qs[0];
-    qg[1] = qs[1];
+  } else {
+    uint32_t* hs = &hl[0][0];  // the reduced histograms of the last round, staged before the zeroing below
+    if (tid < 512) hs[tid] = hg[tid];
+    __syncthreads();
+    const int wv = tid >> 6;
+    if (wv < 2) {
+      const DpQuery Q = dp_consume_wave(qg[wv], hs + wv * 256, tid & 63);
+      if ((tid & 63) == 0) {
+        qs[wv] = Q;
+        qg[wv] = Q;
+      }
+    }
+    __syncthreads();
   }
   for (int i = tid; i < 2 * 256 * kStCopies; i += T) (&hl[0][0])[i] = 0;
   __syncthreads();
@@ -804,7 +941,19 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
     if (q1.src == src && (k & q1.mask) == q1.pre)
       atomicAdd(&hl[1][(((k >> sh[1]) & ((1u << db[1]) - 1)) * kStCopies) + cp], 1u);
   };
-  if (q0.src == 1 || q1.src == 1) {  // this rank's candidate keys of (c, t): the pass's lists + overflow
+  const uint32_t ncl = a.ncand[ct];
+  if ((q0.src == 1 || q1.src == 1) && ncl != 0xffffffffu) {  // this rank's compacted candidate keys of (c, t)
+    const uint32_t* C = a.cand + (int64_t)ct * kDpCandCap;
+    constexpr int B = 8;
+    for (uint32_t i0 = tid; i0 < ncl; i0 += B * T) {
+      uint32_t v[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) v[k] = i0 + k * T < ncl ? C[i0 + k * T] : 0u;
+#pragma unroll
+      for (int k = 0; k < B; ++k)
+        if (i0 + k * T < ncl) hit(v[k], 1);
+    }
+  } else if (q0.src == 1 || q1.src == 1) {  // too many to compact: the pass's lists + overflow
     if (tid < a.nblk) {
       const uint32_t nb = a.wgn[(int64_t)tid * ob * 2 + ct];
       const uint32_t* L = a.wgl + ((int64_t)tid * ob * 2 + ct) * a.cap;
@@ -829,11 +978,18 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
 }
 
 // Phase 6: the last round's histograms resolve every query; numpy 'linear' percentile, running max / min;
-// target 0 also writes mean / std from the all-reduced moments.  Grid (ob, 2), one thread each.
-__global__ void k_dp_final(StDpArgs a) {
-  const int c = blockIdx.x, t = blockIdx.y, ob = a.r.ob, ct = c * 2 + t;
-  DpQuery Q[2] = {a.q[ct * 2], a.q[ct * 2 + 1]};
-  for (int u = 0; u < 2; ++u) dp_consume(Q[u], a.hist + ((int64_t)ct * 2 + u) * 256);
+// target 0 also writes mean / std from the all-reduced moments.  Grid (ob, 2), two waves (one per query).
+__global__ __launch_bounds__(128) void k_dp_final(StDpArgs a) {
+  const int c = blockIdx.x, t = blockIdx.y, ob = a.r.ob, ct = c * 2 + t, wv = threadIdx.x >> 6;
+  __shared__ uint32_t hs[2][256];
+  __shared__ DpQuery qs[2];
+  for (int i = threadIdx.x; i < 512; i += 128) (&hs[0][0])[i] = a.hist[(int64_t)ct * 512 + i];
+  __syncthreads();
+  const DpQuery Qw = dp_consume_wave(a.q[ct * 2 + wv], hs[wv], threadIdx.x & 63);
+  if ((threadIdx.x & 63) == 0) qs[wv] = Qw;
+  __syncthreads();
+  if (threadIdx.x) return;
+  const DpQuery Q[2] = {qs[0], qs[1]};
   const int64_t n = a.n_global;
   if (t == 0) {
     const double mu = a.exch[c * 2 + 0] / (double)n;

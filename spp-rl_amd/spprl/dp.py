@@ -70,6 +70,8 @@ def make_allgather(group=None):
         return None
     if dist.get_world_size(group) == 1 and not _single_rank_exchange():
         return None
+    if os.environ.get("SPP_DP_STATS", "onepass") == "stepwise":  # A/B: the stepwise radix protocol
+        return None
     return _AllGather(group)
 
 

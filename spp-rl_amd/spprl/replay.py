@@ -275,13 +275,13 @@ class BufferAcMOffPolicy:
             self._dp1_samp = torch.zeros(W * ob * Sl, dtype=torch.int32, device=self.device)
             self._dp1_exch = torch.zeros(12 * ob, dtype=torch.float64, device=self.device)
             self._dp1_hist = torch.zeros(ob * 1024, dtype=torch.int32, device=self.device)
-            self._dp1_pivot = torch.zeros(ob, device=self.device)
             self._dp1_key = key
-        self._dp1_pivot.copy_(self.obs_mean)  # replicated across ranks
         first = 0 if self._have_minmax else 1
         mine = self._dp1_samp[R * ob * Sl:(R + 1) * ob * Sl]
         for phase in range(7):
-            call("sppReplayObsStatsDP1", self._h, phase, W, R, ptr(self._dp1_pivot), ptr(self._dp1_samp),
+            # pivot = the running mean itself (replicated across ranks): phase 6 reads pivot[c] before it
+            # writes mean[c], in the same thread
+            call("sppReplayObsStatsDP1", self._h, phase, W, R, ptr(self.obs_mean), ptr(self._dp1_samp),
                  ptr(self._dp1_exch), ptr(self._dp1_hist), n_global, ptr(self.obs_mean), ptr(self.obs_std),
                  ptr(self.max_obs), ptr(self.min_obs), first, stream_handle())
             if phase == 0:

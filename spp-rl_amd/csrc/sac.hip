@@ -457,9 +457,6 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     // ---- target action: a' ~ pi(s'), a'_d, logpi'   (sac_acm.py:44-45)
     SPP_TP(0);
     actor_trunk<C, false>(p.actor, p.S2, C::OB * L.ld4, L, nullptr, nullptr, d0, d1, d2, d3);
-#ifdef SPP_CUT
-    if (SPP_CUT == 1) { p.part[tile] = L.bl[0]; continue; }
-#endif
     float lp2;
     {
       f32x16 hd[C::NB_PAIR];
@@ -477,18 +474,12 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     } else {
       load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, big, C::AOUT);
     }
-#ifdef SPP_CUT
-    if (SPP_CUT == 2) { p.part[tile] = L.bl[0] + tin[0][3] + lp2; continue; }
-#endif
     // ---- soft-min twin target (:50-56)
     SPP_TP(5);
     const float q1t = critic_forward<C, false, 6>(p.targ[0], tin, L, nullptr, nullptr, d0, d1, d2, d3);
     const float q2t = critic_forward<C, false, 8>(p.targ[1], tin, L, nullptr, nullptr, d0, d1, d2, d3);
     const float notdone = 1.f - p.DN[b];
     const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
-#ifdef SPP_CUT
-    if (SPP_CUT == 3) { p.part[tile] = y; continue; }
-#endif
     // ---- both critics: forward, MSE grad, backward to weight-gradient operands (:117-131)
     float lq0 = 0.f, lq1 = 0.f;
 #pragma unroll 1
@@ -504,9 +495,6 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
       if (i == 0) lq0 = lqi; else lq1 = lqi;
       if (L.h == 0) p.DQ[i][b] = dq;
-#ifdef SPP_CUT
-      if (SPP_CUT == 4) continue;
-#endif
       // delta2 = dq * w3 * relu'(h2): staged through the LDS image, stored feature-major
       const rsrc_t d2r = rsrc(p.D2[i]);
       const float* w3 = tbl + Q.tw3;

@@ -43,6 +43,7 @@
 #endif
 #include "onp.hip"
 #include "sgd.hip"
+#include "sgd_mf.hip"
 
 namespace spp {
 
@@ -1857,6 +1858,26 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
                bs, nullptr, nullptr, nullptr};
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
+#ifndef SPP_SGD_SCALAR
+  // the MFMA form (sgd_mf.hip): 64 rows per workgroup, gradients summed over the workgroups
+  const int nwg = cdiv(bs, kMfR);
+  if (nwg > 1) {
+    g.bsl = cdiv(bs, nwg);
+    if (!a->sgd_slab.ptr) {
+      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)(2 * kMfMaxWG + 2) * kMfSlab));  // + the reduced slabs
+      SPP_CHECK_HIP(a->sgd_sync.alloc(2));  // {arrival counter, timeout flag}
+      SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, 2 * sizeof(int), st));
+    }
+    g.slab = a->sgd_slab.ptr;
+    g.ctr = a->sgd_sync.ptr;
+    g.err = a->sgd_sync.ptr + 1;
+    SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, sizeof(int), st));
+  }
+  const bool mw = nwg > 1;
+#define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                              \
+  if (mw) hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, true>), dim3(nwg), dim3(kMfTH), 0, st, g);    \
+  else hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, false>), dim3(1), dim3(kMfTH), 0, st, g)
+#else
   // batches past one workgroup's rows: ~64 rows per workgroup, gradients summed over the workgroups
   int nwg = 1;
   if (bs > kSgdMaxBatch) {
@@ -1877,6 +1898,7 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
 #define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                          \
   if (mw) hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_, true>), dim3(nwg), dim3(TH_), 0, st, g); \
   else hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_>), dim3(1), dim3(TH_), 0, st, g)
+#endif
   if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3, 256);
   else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6, 512);
   else if (ob == 3 && ac == 1) SPP_SGD_LAUNCH(6, 1, 512);

@@ -26,8 +26,14 @@ constexpr int kSgdThreads = 256;
 constexpr int kSgdMaxBatch = 128;   // rows per workgroup and step
 constexpr int kSgdMaxWG = 256;      // workgroups of the multi-workgroup form (batches up to 32,768)
 constexpr int kSlabStride = 5120;   // floats per workgroup slab: >= 16 * NT + 1 for every instantiation
-constexpr int kSgdBigRows = 64;     // target rows per workgroup of the multi-workgroup form
-constexpr int kSgdTwoLevel = 24;    // more workgroups than this: two-level gradient reduction per step
+#ifndef SPP_SGD_ROWS
+#define SPP_SGD_ROWS 64
+#endif
+constexpr int kSgdBigRows = SPP_SGD_ROWS;  // target rows per workgroup of the multi-workgroup form
+#ifndef SPP_SGD_TWOLEVEL
+#define SPP_SGD_TWOLEVEL 4
+#endif
+constexpr int kSgdTwoLevel = SPP_SGD_TWOLEVEL;  // more workgroups than this: two-level gradient reduction per step
 
 struct AcmSgdArgs {
   const float* x;      // [nsteps * bs][IN] acm_cat inputs, consumed in order (sppReplayGatherAcm)
@@ -174,36 +180,52 @@ __device__ __forceinline__ void outer4x4(const float* A, int lda, const float* B
   }
 }
 
-// Arrival barrier of the multi-workgroup SGD (MI355X_MICROARCH.md "Valid forms": plain slab stores, every
-// storing wave's vmcnt(0), workgroup barrier, one lane's agent release, a relaxed counter add; the same
-// lane polls with relaxed loads, then one agent acquire before the workgroup reads other workgroups'
-// slabs).  The counter address is kept in a VGPR so the add and the polls are vector-memory operations.
-// Bounded: a wait that times out sets *err and every later wait of the launch returns at once.
-__device__ __forceinline__ void sgd_arrive_wait(int* ctr, int target, int* err, int* s_dead) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+// Arrival barrier of the multi-workgroup SGD.  The counter address is kept in a VGPR so the add and the
+// polls are vector-memory operations.  Bounded: a wait that times out sets *err and every later wait of
+// the launch returns at once.
+// The per-step gradient hand-over between the workgroups is write-through: every slab word is stored
+// sc1 (aux 16) and every load of slab words is an sc1 load, so the arrival needs no agent-scope release
+// (its L2 write-back cost ~6.5 us per step with a freshly written 18 KB slab) and no acquire
+// (cdna_hip_programming.md Guideline 16, R1 with sc1 loads; MI355X_MICROARCH.md visibility table row 1):
+// stores -> every wave's vmcnt(0) -> workgroup barrier -> lane 0 relaxed agent add -> relaxed poll -> barrier.
+constexpr int kSc1 = 16;  // buffer cache-policy operand: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sgd_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void slab_st4(__amdgpu_buffer_rsrc_t r, int idx, float4 v) {
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, 4u * (uint32_t)idx, 0, kSc1);
+}
+__device__ __forceinline__ void slab_st1(__amdgpu_buffer_rsrc_t r, int idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, 4u * (uint32_t)idx, 0, kSc1);
+}
+__device__ __forceinline__ float4 slab_ld4(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, 4u * (uint32_t)idx, 0, kSc1));
+}
+__device__ __forceinline__ float slab_ld1(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, 4u * (uint32_t)idx, 0, kSc1));
+}
+__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores are written through
+  __syncthreads();                                   // ... and every other wave's
   if (threadIdx.x == 0 && !*s_dead) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int off = 0;
     asm volatile("" : "+v"(off));
     int* c = ctr + off;
     __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int spins = 0;
     while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 22)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 23)) {
         *s_dead = 1;
         err[off] = 1;
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below the poll
   __syncthreads();
 }
-
 // TH threads (a multiple of 64): 512 (two waves per SIMD) where the per-thread registers fit in 256.
 // MW: one step's batch spread over gridDim.x workgroups (rows g*bsl ...), per-step gradients summed
 // over the workgroups in a fixed order (every workgroup the same sum, so every workgroup applies the
@@ -499,44 +521,44 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
     if constexpr (MW) {
       // ---- sum the step's gradient over the workgroups (fixed order g = 0 .. G-1)
       const int G = gridDim.x;
-      float* mine = a.slab + ((int64_t)(st & 1) * G + blockIdx.x) * kSlabStride;
+      const auto mine = sgd_rsrc(a.slab + ((int64_t)(st & 1) * G + blockIdx.x) * kSlabStride);
 #pragma unroll
       for (int k = 0; k < C::RT; ++k) {
         const int q = sgd_own<C, TH>(t, k);
         if (q >= 0)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<float4*>(mine + 16 * q + 4 * i) = make_float4(g[k][i][0], g[k][i][1], g[k][i][2], g[k][i][3]);
+            slab_st4(mine, 16 * q + 4 * i, make_float4(g[k][i][0], g[k][i][1], g[k][i][2], g[k][i][3]));
       }
-      if (t == 0) mine[16 * C::NT] = ls_part;
+      if (t == 0) slab_st1(mine, 16 * C::NT, ls_part);
       const int nsync = G > kSgdTwoLevel ? 2 : 1;  // arrival waits per step
-      sgd_arrive_wait(a.ctr, G * nsync * st + G, a.err, &s_dead);
-      const float* all = a.slab + (int64_t)(st & 1) * G * kSlabStride;
+      sgd_arrive_wait_wt(a.ctr, G * nsync * st + G, a.err, &s_dead);
+      const auto all = sgd_rsrc(a.slab + (int64_t)(st & 1) * G * kSlabStride);
       if (G > kSgdTwoLevel) {
         // many workgroups: workgroup g first sums slice g of the gradient over every slab (fixed order)
         // into the step's reduced slab, then every workgroup reads the reduced gradient
-        float* red = a.slab + (int64_t)2 * G * kSlabStride + (int64_t)(st & 1) * kSlabStride;
+        const auto red = sgd_rsrc(a.slab + (int64_t)2 * G * kSlabStride + (int64_t)(st & 1) * kSlabStride);
         constexpr int NTE = 16 * C::NT + 1;
         const int chunk = (NTE + G - 1) / G;
         const int e1 = min((int)(blockIdx.x + 1) * chunk, NTE);
         for (int e = (int)blockIdx.x * chunk + t; e < e1; e += TH) {
           float v = 0.f;
-          for (int gg = 0; gg < G; ++gg) v += all[(int64_t)gg * kSlabStride + e];
-          red[e] = v;
+          for (int gg = 0; gg < G; ++gg) v += slab_ld1(all, gg * kSlabStride + e);
+          slab_st1(red, e, v);
         }
-        sgd_arrive_wait(a.ctr, G * nsync * st + 2 * G, a.err, &s_dead);
+        sgd_arrive_wait_wt(a.ctr, G * nsync * st + 2 * G, a.err, &s_dead);
 #pragma unroll
         for (int k = 0; k < C::RT; ++k) {
           const int q = sgd_own<C, TH>(t, k);
           if (q >= 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float4 v = reinterpret_cast<const float4*>(red + 16 * q)[i];
+              const float4 v = slab_ld4(red, 16 * q + 4 * i);
               g[k][i][0] = v.x; g[k][i][1] = v.y; g[k][i][2] = v.z; g[k][i][3] = v.w;
             }
           }
         }
-        if (blockIdx.x == 0 && t == 0) loss_acc += red[16 * C::NT] * inv_n;
+        if (blockIdx.x == 0 && t == 0) loss_acc += slab_ld1(red, 16 * C::NT) * inv_n;
       } else {
 #pragma unroll
       for (int k = 0; k < C::RT; ++k) {
@@ -544,10 +566,9 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
         if (q >= 0) {
           float4 acc[4] = {};
           for (int gg = 0; gg < G; ++gg) {
-            const float4* src = reinterpret_cast<const float4*>(all + (int64_t)gg * kSlabStride + 16 * q);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float4 v = src[i];
+              const float4 v = slab_ld4(all, gg * kSlabStride + 16 * q + 4 * i);
               acc[i].x += v.x; acc[i].y += v.y; acc[i].z += v.z; acc[i].w += v.w;
             }
           }
@@ -559,7 +580,7 @@ __global__ __launch_bounds__(TH, 1) void k_acm_sgd(AcmSgdArgs a) {
       }
       if (blockIdx.x == 0 && t == 0) {
         float ls = 0.f;
-        for (int gg = 0; gg < G; ++gg) ls += all[(int64_t)gg * kSlabStride + 16 * C::NT];
+        for (int gg = 0; gg < G; ++gg) ls += slab_ld1(all, gg * kSlabStride + 16 * C::NT);
         loss_acc += ls * inv_n;
       }
       }

@@ -15,16 +15,17 @@ import torch  # noqa: E402
 import spprl  # noqa: E402
 from spprl import _lib  # noqa: E402
 
-NAMES = {0: "stage batch", 1: "fwd L1", 2: "fwd L2", 3: "out / loss / dz3", 4: "dz2", 5: "grads L2+L3",
-         6: "dz1", 7: "grads L1", 8: "Adam"}
+NAMES = {0: "stage batch", 1: "fc1", 2: "fc2, fc3, loss, dz3, dz2", 3: "dz1", 4: "gradient tiles",
+         5: "slab, barrier, reduce", 6: "Adam"}
 
 
 def main():
     dev = torch.device("cuda", 0)
-    ob, ac, bs, K = 17, 6, 64, 400
-    ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", max_batch=4096, buffer_size=20_000, device=dev, seed=0)
+    ob, ac, K = 17, 6, 400
+    bs = int(sys.argv[1]) if len(sys.argv) > 1 else 64  # > 128: the multi-workgroup form
+    ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", max_batch=max(4096, bs), buffer_size=40_000, device=dev, seed=0)
     rb = ag.replay_buffer
-    n = 10_000
+    n = 20_000
     slots = rb.add_obs_batch(torch.randn(n + 1, ob, device=dev))
     rb.add_timestep_batch(slots[:n], slots[1:], torch.randn(n, ob, device=dev), torch.randn(n, device=dev),
                           torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.uint8, device=dev),
@@ -46,9 +47,9 @@ def main():
     _lib.call("sppDebugReadProf", buf, 1)
     v = np.array(buf[:32], dtype=np.float64) / (4 * K)  # waves 0..3 recorded
     tot = v.sum()
-    print("k_acm_sgd<34, 6>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
+    print("k_acm_sgd_mf<34, 6>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
           % (K, bs, el * 1e3, el * 1e6 / K, tot))
-    for k in range(9):
+    for k in range(7):
         print("  %2d %-20s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
 
 

@@ -1064,7 +1064,11 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
       j.wsplit = thin_n && thin_k ? 4 : (thin_n != thin_k ? 2 : 1);
       // small jobs: >= 2048 samples per item, and at most ~256 slabs (the fixed-order reduce is
       // serial over slabs)
-      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big) : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
+#ifndef SPP_DW_RESERVE
+#define SPP_DW_RESERVE 0
+#endif
+      const int big_cu = std::max(num_cu / 2, num_cu - SPP_DW_RESERVE);
+      int ns = is_big(j) ? (int)std::lround(big_cu * pm / big) : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
       // small batches (PPO minibatches of 512): at least 4 items, so each wave of an item takes one
       // 32-sample unit instead of a serial chain over the whole batch
       if (!is_big(j)) ns = std::max(ns, std::min(cdiv(Bp, 32 * j.wsplit), 4));

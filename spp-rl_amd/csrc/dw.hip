@@ -253,6 +253,12 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   //   wsplit 2 (one side <= 128): 2 quadrants along the wide side, 2 sample halves each.
   const int N = J.N, K = J.K0 + J.K1;
   const bool wsp = J.wsplit > 1;
+#ifdef SPP_DW_EXP_SKIP_THIN  // timing experiment only (wrong results): the 256x256 items alone
+  if (!(N == 256 && K == 256 && J.K1 == 0 && !wsp)) return;
+#endif
+#ifdef SPP_DW_EXP_SKIP_BIG
+  if (N == 256 && K == 256 && J.K1 == 0 && !wsp) return;
+#endif
   int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1), part = 0;
   if (J.wsplit == 4) {
     nb0 = kb0 = 0;

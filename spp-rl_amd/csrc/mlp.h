@@ -16,6 +16,15 @@
 #include "common.h"
 
 namespace spp {
+// Cross-lane hand-over through the wave's LDS image.  Most layer boundaries are same-lane (a lane
+// reads back the units it wrote), but the heads' pairing layout (row j0 + 8h) and the natural
+// layout (row u + 4h) map a row to different lane halves.  Per-thread program order says nothing
+// about another lane's store, so without a fence the compiler may schedule such a read above the
+// writing lane's store whenever it can prove the two per-lane addresses distinct; this compiler
+// memory barrier pins every store before it ahead of every load after it (no instruction emitted;
+// LDS operations of one wave complete in order).
+#define SPP_XLANE_SYNC() asm volatile("" ::: "memory")
+
 
 // Region timing of the phase kernels (profiling builds only, -DSPP_PROF): each
 // wave accumulates s_memtime deltas per region in LDS, flushed to g_tprof.

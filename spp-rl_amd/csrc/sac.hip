@@ -165,6 +165,7 @@ __device__ __forceinline__ float t_softplus(float x) {
 // pairing layout: block ib, register r<8 (mu) / r+8 (logsig), half h -> j = 16*ib + 8*h + r
 template <class C>
 __device__ __forceinline__ void load_pair(f32x16 (&t)[C::NB_PAIR], const float* lds) {
+  SPP_XLANE_SYNC();
   const int lane = lane_id(), h8 = 8 * (lane >> 5);
   const float* pl = lds + h8 * 32 + (lane & 31);
 #pragma unroll
@@ -181,6 +182,7 @@ __device__ __forceinline__ void load_pair(f32x16 (&t)[C::NB_PAIR], const float* 
 template <int NB0, int NB1>
 __device__ __forceinline__ void load_cat_gl(f32x16 (&t)[NB0 + NB1], const float* X, int nbytes, int F0, int ld4,
                                             uint32_t vo, const float* lds, int F1) {
+  SPP_XLANE_SYNC();
   const int lane = lane_id(), h4 = 4 * (lane >> 5);
   const float* l = lds + h4 * 32 + (lane & 31);
   f32x16 g[NB0];
@@ -431,6 +433,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
         if (ok) L.pl[j0 * 32] = ad;
       }
     }
+  SPP_XLANE_SYNC();
   const float tot = lp + __shfl_xor(lp, 32, 64);
   const float tc = corr + __shfl_xor(corr, 32, 64);
   return fsub_rn(tot, tc);
@@ -759,6 +762,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
       const rsrc_t epsr = rsrc_n(p.EPS2, C::AOUT * L.ld4);
       const rsrc_t s2r = rsrc_n(p.S2, C::OB * L.ld4);
       const bool closs = p.custom_loss != 0.f;
+      SPP_XLANE_SYNC();  // d loss / d a_d was written in the natural layout (other lanes' rows)
   #pragma unroll
       for (int ib = 0; ib < C::NB_PAIR; ++ib)
   #pragma unroll

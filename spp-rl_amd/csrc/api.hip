@@ -114,6 +114,13 @@ struct sppReplay {
   uint32_t *sf_samp = nullptr, *sf_bounds = nullptr, *sf_cpart = nullptr, *sf_wgl = nullptr, *sf_wgn = nullptr, *sf_ovf = nullptr,
            *sf_ovf_n = nullptr;
   double* sf_part = nullptr;
+  // Ring generation: bumped by every entry point that can change the live rows (AddObs / AddStep /
+  // Reset / GetView, whose caller may write).  sf_bounds holds the bracket of generation sf_gen
+  // over sf_len rows: a later call on the same rows reuses it (the sample and its bracket would be
+  // recomputed bit for bit).  Any bounds give the exact result (a rank outside the bracket falls
+  // back to the raw column), so the generation only decides the cost, never the value.
+  uint64_t gen = 0, sf_gen = ~0ull;
+  int64_t sf_len = -1;
   void* dp_q = nullptr;  // one-pass data-parallel statistics: per (column, target, rank) query state
   uint32_t* dp_cand = nullptr;  // and the compacted local candidates + counts
 };
@@ -227,6 +234,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
 sppStatus sppReplayAddObs(sppReplayHandle h, const float* obs, int E, int64_t* slots, void* stream) {
   SPP_REQUIRE(h && obs && E > 0 && E <= h->d.cap, SPP_E_INVALID_ARG, "add_obs: bad args");
   const int64_t base = h->obs_idx;
+  ++h->gen;
   hipLaunchKernelGGL(k_replay_add_obs, dim3(cdiv((int64_t)E * h->d.ob, 256)), dim3(256), 0, S(stream), h->d.obs,
                      h->d.cap, h->d.ob, obs, E, base);
   SPP_CHECK_HIP(hipGetLastError());
@@ -260,6 +268,7 @@ sppStatus sppReplayAddStep(sppReplayHandle h, const int64_t* prev, const int64_t
   if (rs) return rs;
   const int slot = h->ring_pos;
   h->ring_pos = (h->ring_pos + 1) % sppReplay::kRing;
+  ++h->gen;
   SPP_CHECK_HIP(hipEventSynchronize(h->ev[slot]));  // the copy that last used this slot is done
   int64_t* m = h->pinned[slot];
   // add_timestep wrap rule (replay_buffer.py:65-75) applied sequentially in env order
@@ -298,6 +307,7 @@ sppStatus sppReplayState(sppReplayHandle h, int64_t* obs_idx, int64_t* ts_idx, i
 sppStatus sppReplayReset(sppReplayHandle h) {
   SPP_REQUIRE(h, SPP_E_INVALID_ARG, "null handle");
   h->obs_idx = h->ts_idx = h->len = 0;
+  ++h->gen;
   return SPP_OK;
 }
 
@@ -312,6 +322,7 @@ sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx, int B, float* o
 
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* v) {
   SPP_REQUIRE(h && v, SPP_E_INVALID_ARG, "null");
+  ++h->gen;  // the caller may write the ring through the view
   v->obs = h->d.obs;
   v->obs_idx = h->d.obs_idx;
   v->next_idx = h->d.next_idx;
@@ -473,13 +484,17 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
   hipStream_t st = S(stream);
   const bool big = len > kStBigLen;
   const int ns = (int)std::min<int64_t>(len, big ? kStSampBig : kStSampSmall);
-  hipLaunchKernelGGL(k_st_sample, dim3(cdiv(ns, 256)), dim3(256), 0, st, h->d, len, ns, h->sf_samp);
-  if (big)
-    hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns, h->sf_bounds,
-                       ns, (int64_t)0, 4);
-  else
-    hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns,
-                       h->sf_bounds, ns, (int64_t)0, 4);
+  if (h->sf_gen != h->gen || h->sf_len != len) {  // else: the same rows' bracket is in sf_bounds
+    hipLaunchKernelGGL(k_st_sample, dim3(cdiv(ns, 256)), dim3(256), 0, st, h->d, len, ns, h->sf_samp);
+    if (big)
+      hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns, h->sf_bounds,
+                         ns, (int64_t)0, 4);
+    else
+      hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, h->sf_samp, ns,
+                         h->sf_bounds, ns, (int64_t)0, 4);
+    h->sf_gen = h->gen;
+    h->sf_len = len;
+  }
   const int cap = st_list_cap(ob);
   StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                 h->sf_ovf_n, cap};

@@ -108,6 +108,105 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm(ReplayDev r, const int6
   stage_rows(r.acm, rt, r.ac, valid, stg, AENV, Bp, b0);
 }
 
+// Second form (the default): kStage2Tile = 32 samples per workgroup, the four row gathers (obs,
+// next obs, action, ACM action) issued together before one barrier, then the four transposed
+// stores.  Lane geometry per array of width w is fixed per thread (no per-element division):
+// narrow rows (w <= 64) put G = 64 / w rows side by side in a wave (lane -> row g = lane / w,
+// column lane % w), wide rows take one row per wave step with columns lane, lane + 64.  The
+// 4 waves deal the row steps round-robin and keep up to kStage2Ld loads per lane in flight.
+// The store side writes each feature row's 32 samples as one 128-B run; LDS rows have an odd
+// stride (w | 1) so the transposed reads are conflict-free.
+constexpr int kStage2Tile = 32;
+constexpr int kStage2Ld = 16;
+
+__host__ __device__ inline int stage2_stride(int w) { return w | 1; }
+__host__ __device__ inline size_t stage2_lds_bytes(int ob, int aout, int ac, bool act) {
+  return sizeof(float) * kStage2Tile * (2 * stage2_stride(ob) + (act ? stage2_stride(aout) : 0) + stage2_stride(ac));
+}
+
+struct Stage2Geo {
+  int w, G, g, f0, nsteps, nc;
+  bool on;
+  __device__ Stage2Geo(int w_, int lane) : w(w_) {
+    const bool narrow = w <= 64;
+    G = narrow ? 64 / w : 1;
+    g = narrow ? lane / w : 0;
+    f0 = narrow ? lane - g * w : lane;
+    on = narrow ? lane < G * w : true;
+    nsteps = (kStage2Tile + G - 1) / G;
+    nc = (w + 63) / 64;  // column chunks (1 or 2 for w <= 128)
+  }
+};
+
+// Items of this wave for one array: (step st = wv + 4 k, chunk j) flattened as i = k * nc + j.
+__device__ __forceinline__ int stage2_items(const Stage2Geo& G, int wv) {
+  const int ks = G.nsteps > wv ? (G.nsteps - wv + 3) / 4 : 0;
+  return ks * G.nc;
+}
+
+__device__ __forceinline__ void stage2_gather(const float* __restrict__ src, const int64_t* rows, int valid,
+                                              const Stage2Geo& G, int wv, float* l) {
+  const int n = stage2_items(G, wv), ls = stage2_stride(G.w);
+  for (int i0 = 0; i0 < n; i0 += kStage2Ld) {
+    float v[kStage2Ld];
+    int at[kStage2Ld];
+#pragma unroll
+    for (int u = 0; u < kStage2Ld; ++u) {
+      const int i = i0 + u;
+      const int k = i / G.nc, j = i - k * G.nc;  // nc is 1 or 2: a shift / compare, not a division loop
+      const int s = (wv + 4 * k) * G.G + G.g, f = G.f0 + 64 * j;
+      const bool ok = i < n && G.on && s < kStage2Tile && f < G.w;
+      at[u] = ok ? s * ls + f : -1;
+      v[u] = (ok && s < valid) ? src[rows[s] * G.w + f] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kStage2Ld; ++u)
+      if (at[u] >= 0) l[at[u]] = v[u];
+  }
+}
+
+__device__ __forceinline__ void stage2_store(const float* l, int w, float* dst, int64_t Bp, int64_t b0) {
+  const int s = threadIdx.x & (kStage2Tile - 1), ls = stage2_stride(w);
+  if (b0 + s >= Bp) return;
+  for (int f = threadIdx.x / kStage2Tile; f < w; f += 256 / kStage2Tile) dst[f * Bp + b0 + s] = l[s * ls + f];
+}
+
+__global__ __launch_bounds__(256) void k_replay_stage_fm2(ReplayDev r, const int64_t* __restrict__ idx, int B, int Bp,
+                                                          float* S, float* S2, float* ACT, float* AENV, float* R,
+                                                          float* DN) {
+  extern __shared__ float stg[];
+  __shared__ int64_t rt[kStage2Tile], ro[kStage2Tile], rn[kStage2Tile];
+  const int64_t b0 = (int64_t)blockIdx.x * kStage2Tile;
+  const int valid = (int)min((int64_t)kStage2Tile, (int64_t)B - b0 > 0 ? (int64_t)B - b0 : 0);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < kStage2Tile) {
+    const int s = tid;
+    const int64_t t = s < valid ? idx[b0 + s] : 0;
+    rt[s] = t;
+    ro[s] = s < valid ? r.obs_idx[t] : 0;
+    rn[s] = s < valid ? r.next_idx[t] : 0;
+    if (b0 + s < Bp) {
+      R[b0 + s] = s < valid ? r.rew[t] : 0.f;
+      DN[b0 + s] = s < valid ? (float)r.done[t] : 0.f;
+    }
+  }
+  __syncthreads();
+  float* lo = stg;
+  float* ln = lo + kStage2Tile * stage2_stride(r.ob);
+  float* la = ln + kStage2Tile * stage2_stride(r.ob);
+  float* lm = la + (ACT ? kStage2Tile * stage2_stride(r.aout) : 0);
+  const Stage2Geo go(r.ob, lane), gm(r.ac, lane);
+  stage2_gather(r.obs, ro, valid, go, wv, lo);
+  stage2_gather(r.obs, rn, valid, go, wv, ln);
+  if (ACT) stage2_gather(r.act, rt, valid, Stage2Geo(r.aout, lane), wv, la);
+  stage2_gather(r.acm, rt, valid, gm, wv, lm);
+  __syncthreads();
+  stage2_store(lo, r.ob, S, Bp, b0);
+  stage2_store(ln, r.ob, S2, Bp, b0);
+  if (ACT) stage2_store(la, r.aout, ACT, Bp, b0);
+  stage2_store(lm, r.ac, AENV, Bp, b0);
+}
+
 // last_end (replay_buffer.py:170-177) and the walk of last_rollout (:335-383): out[0] = the first
 // index at distance 0, 1, ... back from p (cyclic over [0, len)) with end set; out[1] = the first
 // one at distance 1 .. len back from out[0] (itself when it is the only end).  -1: none.

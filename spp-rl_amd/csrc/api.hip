@@ -765,6 +765,7 @@ struct DwSet {
   DevArray<int> items;
   int B = -1;
   int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
+  int nlds[2] = {0, 0};  // leading items of a phase that run as k_dw_big (256 x 256 fp32 jobs)
   int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
   bool bf16 = false;              // bf16 MFMA job set (k_dw<true>)
   void release() { slab.release(); jobs.release(); items.release(); }
@@ -1067,23 +1068,23 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
   auto is_big = [](const DwJob& j) {
     return (int64_t)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32) >= 128 * 128;
   };
+  // 256 x 256 fp32 jobs run as their own launch (k_dw_big); the other large jobs share k_dw's launch
+  auto lds_big = [](const DwJob& j) { return !j.bf16 && j.N == 256 && j.K0 == 256 && j.K1 == 0; };
   auto assign_splits = [&](int first, int count) {
-    double big = 0.0;
+    double big[2] = {0.0, 0.0};  // MACs of the large jobs per launch
     for (int i = first; i < first + count; ++i)
-      if (is_big(jobs[i])) big += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
+      if (is_big(jobs[i]))
+        big[lds_big(jobs[i]) ? 0 : 1] += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
     for (int i = first; i < first + count; ++i) {
       DwJob& j = jobs[i];
       const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
       // outputs that fit one 128x128 wave quadrant: the 4 waves split each item's samples
       const bool thin_n = j.N <= 128, thin_k = j.K0 + j.K1 <= 128;
       j.wsplit = thin_n && thin_k ? 4 : (thin_n != thin_k ? 2 : 1);
-      // small jobs: >= 2048 samples per item, and at most ~256 slabs (the fixed-order reduce is
-      // serial over slabs)
-#ifndef SPP_DW_RESERVE
-#define SPP_DW_RESERVE 0
-#endif
-      const int big_cu = std::max(num_cu / 2, num_cu - SPP_DW_RESERVE);
-      int ns = is_big(j) ? (int)std::lround(big_cu * pm / big) : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
+      // large jobs: ~one workgroup per CU over their launch, in proportion to their MACs; small jobs:
+      // >= 2048 samples per item, and at most ~256 slabs (the fixed-order reduce is serial over slabs)
+      int ns = is_big(j) ? (int)std::lround(num_cu * pm / big[lds_big(j) ? 0 : 1])
+                         : std::min(cdiv(Bp, 2048), std::max(1, 256 / j.wsplit));
       // small batches (PPO minibatches of 512): at least 4 items, so each wave of an item takes one
       // 32-sample unit instead of a serial chain over the whole batch
       if (!is_big(j)) ns = std::max(ns, std::min(cdiv(Bp, 32 * j.wsplit), 4));
@@ -1119,13 +1120,17 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
         off += (size_t)jobs[j].nsplit * jobs[j].wsplit * jobs[j].slab_stride;
       }
     }
-    // large-GEMM items first (they set the launch's critical path)
-    for (int pass = 0; pass < 2; ++pass)
+    // large-GEMM items first (they set the phase's critical path): the 256 x 256 fp32 jobs (k_dw_big,
+    // LDS-DMA operands), then the other large ones, then the thin ones (k_dw)
+    D.nlds[ph] = 0;
+    for (int pass = 0; pass < 3; ++pass)
       for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
-        if (is_big(jobs[j]) != (pass == 0)) continue;
+        const int cls = lds_big(jobs[j]) ? 0 : (is_big(jobs[j]) ? 1 : 2);
+        if (cls != pass) continue;
         for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
           jj.push_back(j - D.j0[ph]);
           ss.push_back(sp);
+          if (pass == 0) ++D.nlds[ph];
         }
       }
     D.max_elems[ph] = 1;
@@ -1251,7 +1256,7 @@ static void launch_dw_set(DwSet& D, int ph, hipStream_t st) {
   const int* ij = D.items.ptr + D.ioff[ph];
   const int* is = ij + D.nitems[ph];
   const DwJob* jobs = D.jobs.ptr + D.j0[ph];
-  launch_dw_kernels(jobs, ij, is, D.nitems[ph], D.nj[ph], D.max_elems[ph], D.bf16, st);
+  launch_dw_kernels(jobs, ij, is, D.nitems[ph], D.nlds[ph], D.nj[ph], D.max_elems[ph], D.bf16, st);
 }
 static void launch_dw(sppAgent* a, int set, int ph, hipStream_t st) { launch_dw_set(a->dws[set], ph, st); }
 

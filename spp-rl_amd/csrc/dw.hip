@@ -195,46 +195,96 @@ __device__ __forceinline__ void dw_big_lds(const DwJob& J, int b_begin, int nste
                    : "memory");
     }
   };
+  // Operand registers are double-buffered across the step's two sub-steps (16 samples each): the
+  // reads of the next sub-step are in flight while the current one's 128 MFMAs issue, so no LDS
+  // latency is exposed.  A step's sub-step 1 reads are complete (lgkmcnt) before the step's closing
+  // barrier, after which buffer t & 1 may be refilled by DMA for step t + 2.
+  const int sw = (c >> 1) & 7;  // the read-side swizzle of rows 32 b + c
+  auto rd = [&](const float* L, int s, float4 (&ra)[4][2], float4 (&rx)[4][2]) {
+    const int q0 = (4 * s + 2 * h) ^ sw, q1 = (4 * s + 2 * h + 1) ^ sw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* pa = L + (32 * (nb0 + i) + c) * 32;
+      const float* px = L + (256 + 32 * (kb0 + i) + c) * 32;
+      ra[i][0] = *reinterpret_cast<const float4*>(pa + 4 * q0);
+      ra[i][1] = *reinterpret_cast<const float4*>(pa + 4 * q1);
+      rx[i][0] = *reinterpret_cast<const float4*>(px + 4 * q0);
+      rx[i][1] = *reinterpret_cast<const float4*>(px + 4 * q1);
+    }
+  };
+  auto mm = [&](const float4 (&ra)[4][2], const float4 (&rx)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float4 av = ra[i][p];
+        if (db) bs[i] += (av.x + av.y) + (av.z + av.w);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 xv = rx[j][p];
+          acc[i][j] = mfma(av.x, xv.x, acc[i][j]);
+          acc[i][j] = mfma(av.y, xv.y, acc[i][j]);
+          acc[i][j] = mfma(av.z, xv.z, acc[i][j]);
+          acc[i][j] = mfma(av.w, xv.w, acc[i][j]);
+        }
+      }
+  };
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int sw = (c >> 1) & 7;  // the read-side swizzle of rows 32 b + c
+  if (nsteps > 1) issue(1, 1);
+  float4 ra0[4][2], rx0[4][2], ra1[4][2], rx1[4][2];
+  rd(lds[0], 0, ra0, rx0);
 #pragma unroll 1
   for (int t = 0; t < nsteps; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nsteps) issue(t + 1, buf ^ 1);  // the other buffer: every wave finished reading it before the last barrier
-    const float* L = lds[buf];
-#pragma unroll 1
-    for (int s = 0; s < 2; ++s) {  // one sub-step's operands live at a time (the 256 AGPRs hold the tiles)
-      const int q0 = (4 * s + 2 * h) ^ sw, q1 = (4 * s + 2 * h + 1) ^ sw;
-      float4 ra[4][2], rx[4][2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float* pa = L + (32 * (nb0 + i) + c) * 32;
-        const float* px = L + (256 + 32 * (kb0 + i) + c) * 32;
-        ra[i][0] = *reinterpret_cast<const float4*>(pa + 4 * q0);
-        ra[i][1] = *reinterpret_cast<const float4*>(pa + 4 * q1);
-        rx[i][0] = *reinterpret_cast<const float4*>(px + 4 * q0);
-        rx[i][1] = *reinterpret_cast<const float4*>(px + 4 * q1);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const float4 av = ra[i][p];
-          if (db) bs[i] += (av.x + av.y) + (av.z + av.w);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 xv = rx[j][p];
-            acc[i][j] = mfma(av.x, xv.x, acc[i][j]);
-            acc[i][j] = mfma(av.y, xv.y, acc[i][j]);
-            acc[i][j] = mfma(av.z, xv.z, acc[i][j]);
-            acc[i][j] = mfma(av.w, xv.w, acc[i][j]);
-          }
-        }
+    rd(lds[t & 1], 1, ra1, rx1);
+    mm(ra0, rx0);
+    if (t + 1 < nsteps) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // my DMA for t + 1 landed, my reads of t done
+      __syncthreads();  // every wave's DMA landed and every wave is done reading buffer t & 1
+      if (t + 2 < nsteps) issue(t + 2, t & 1);
+      rd(lds[(t + 1) & 1], 0, ra0, rx0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for step t+1 landed
-    __syncthreads();  // every wave's DMA landed and every wave is done with buffer t & 1
+    mm(ra1, rx1);
+  }
+}
+
+// Partial (or final) result of an item's (nb0, kb0) quadrant; rows >= nrow2 go to the second output
+// (dW2 / db2).
+__device__ __forceinline__ void dw_store(const DwJob& J, int split, int part, int nb0, int kb0, int ni, int nj,
+                                         bool db, const f32x16 (&acc)[4][4], const float (&bs)[4]) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const int N = J.N, K = J.K0 + J.K1;
+  const bool direct = J.nsplit * J.wsplit == 1;
+  float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + part) * J.slab_stride;
+  auto out_w = [&](int n, int k, float v) {
+    if (!direct) slab[(int64_t)n * K + k] = v;
+    else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;
+    else J.dW2[(int64_t)(n - J.nrow2) * K + k] = v;
+  };
+  auto out_b = [&](int n, float v) {
+    if (!direct) slab[(int64_t)N * K + n] = v;
+    else if (n < J.nrow2) J.db[n] = v;
+    else J.db2[n - J.nrow2] = v;
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= ni) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= nj) break;
+      const int k = 32 * (kb0 + j) + c;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int n = 32 * (nb0 + i) + unit_of(q, h);
+        if (n < N && k < K) out_w(n, k, acc[i][j][q]);
+      }
+    }
+    if (db) {
+      const float tot = bs[i] + __shfl_xor(bs[i], 32, 64);
+      const int n = 32 * (nb0 + i) + c;
+      if (h == 0 && n < N) out_b(n, tot);
+    }
   }
 }
 
@@ -253,12 +303,6 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
   //   wsplit 2 (one side <= 128): 2 quadrants along the wide side, 2 sample halves each.
   const int N = J.N, K = J.K0 + J.K1;
   const bool wsp = J.wsplit > 1;
-#ifdef SPP_DW_EXP_SKIP_THIN  // timing experiment only (wrong results): the 256x256 items alone
-  if (!(N == 256 && K == 256 && J.K1 == 0 && !wsp)) return;
-#endif
-#ifdef SPP_DW_EXP_SKIP_BIG
-  if (N == 256 && K == 256 && J.K1 == 0 && !wsp) return;
-#endif
   int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1), part = 0;
   if (J.wsplit == 4) {
     nb0 = kb0 = 0;
@@ -326,11 +370,6 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
     }                                                                           \
     break;
   if constexpr (!BFK) {
-#ifndef SPP_DW_NO_LDS
-    if (N == 256 && K == 256 && J.K1 == 0 && !wsp) {  // uniform over the workgroup (every wave: 4 x 4 blocks)
-      dw_big_lds(J, b_begin, nsteps / 2, nb0, kb0, db, acc, bs);
-    } else
-#endif
     switch (ni * 8 + nj) {
       SPP_DW_CASE(1, 1) SPP_DW_CASE(1, 2) SPP_DW_CASE(1, 3) SPP_DW_CASE(1, 4)
       SPP_DW_CASE(2, 1) SPP_DW_CASE(2, 2) SPP_DW_CASE(2, 3) SPP_DW_CASE(2, 4)
@@ -348,38 +387,32 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw(const DwJob* __restrict__ 
 #undef SPP_DW_CASE
 #undef SPP_DW_CASE16
 #undef SPP_DW_T
-  // partial (or final) result; rows >= nrow2 go to the second output (dW2/db2)
-  const bool direct = J.nsplit * J.wsplit == 1;
-  float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + part) * J.slab_stride;
-  auto out_w = [&](int n, int k, float v) {
-    if (!direct) slab[(int64_t)n * K + k] = v;
-    else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;
-    else J.dW2[(int64_t)(n - J.nrow2) * K + k] = v;
-  };
-  auto out_b = [&](int n, float v) {
-    if (!direct) slab[(int64_t)N * K + n] = v;
-    else if (n < J.nrow2) J.db[n] = v;
-    else J.db2[n - J.nrow2] = v;
-  };
+  dw_store(J, split, part, nb0, kb0, ni, nj, db, acc, bs);
+}
+
+// 256 x 256 fp32 items (host: DwJob N = K0 = 256, K1 = 0, wsplit = 1, not bf16), listed first in a
+// phase's item table: their own kernel, so the LDS-DMA path gets the kernel's whole register budget
+// (double-buffered operands) and k_dw's thin / mid items carry no 128 KiB static LDS.
+__global__ __launch_bounds__(kDwThreads, 1) void k_dw_big(const DwJob* __restrict__ jobs,
+                                                          const int* __restrict__ item_job,
+                                                          const int* __restrict__ item_split) {
+  const int item = blockIdx.x;
+  const DwJob J = jobs[item_job[item]];
+  const int split = item_split[item];
+  const int w = threadIdx.x >> 6;
+  const int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1);
+  const int b_begin = split * J.split_len;
+  const int b_end = min(b_begin + J.split_len, J.Bp);
+  const int nsteps = (b_end - b_begin) / 32;  // ranges are multiples of 32 samples
+  const bool db = J.db != nullptr && kb0 == 0;
+  f32x16 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i >= ni) break;
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j >= nj) break;
-      const int k = 32 * (kb0 + j) + c;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int n = 32 * (nb0 + i) + unit_of(q, h);
-        if (n < N && k < K) out_w(n, k, acc[i][j][q]);
-      }
-    }
-    if (db) {
-      const float tot = bs[i] + __shfl_xor(bs[i], 32, 64);
-      const int n = 32 * (nb0 + i) + c;
-      if (h == 0 && n < N) out_b(n, tot);
-    }
-  }
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (nsteps > 0) dw_big_lds(J, b_begin, nsteps, nb0, kb0, db, acc, bs);
+  dw_store(J, split, 0, nb0, kb0, 4, 4, db, acc, bs);
 }
 
 // Fixed-order reduction of the split slabs: one thread per element of a job's [N*K | N] image,

@@ -24,10 +24,11 @@ struct DwJob {
 };
 
 // dw.hip (own translation unit, ks_dw.hip): the split-K weight-gradient launch + fixed-order reduce
-// over nitems work items of jobs[0, njobs); item_job / item_split index the job table; bf16: the
-// set's jobs are bf16 MFMA jobs (DwJob::bf16).
-void launch_dw_kernels(const DwJob* jobs, const int* item_job, const int* item_split, int nitems, int njobs,
-                       int64_t max_elems, bool bf16, hipStream_t st);
+// over nitems work items of jobs[0, njobs); item_job / item_split index the job table; the first
+// nlds items are 256 x 256 fp32 jobs (k_dw_big), the rest run in k_dw; bf16: the set's jobs are
+// bf16 MFMA jobs (DwJob::bf16).
+void launch_dw_kernels(const DwJob* jobs, const int* item_job, const int* item_split, int nitems, int nlds,
+                       int njobs, int64_t max_elems, bool bf16, hipStream_t st);
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)
 //   L[n][k] = trans ? S[k][coff + n] : S[n][coff + k]; source rows >= split come from W2

@@ -1069,7 +1069,8 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
     return (int64_t)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32) >= 128 * 128;
   };
   // 256 x 256 fp32 jobs run as their own launch (k_dw_big); the other large jobs share k_dw's launch
-  auto lds_big = [](const DwJob& j) { return !j.bf16 && j.N == 256 && j.K0 == 256 && j.K1 == 0; };
+  // (small batches -- vanilla SAC's B = 100, PPO minibatches -- keep one launch: k_dw's register tiles)
+  auto lds_big = [Bp](const DwJob& j) { return Bp >= 8192 && !j.bf16 && j.N == 256 && j.K0 == 256 && j.K1 == 0; };
   auto assign_splits = [&](int first, int count) {
     double big[2] = {0.0, 0.0};  // MACs of the large jobs per launch
     for (int i = first; i < first + count; ++i)

@@ -262,7 +262,9 @@ class BufferAcMOffPolicy:
                 buf = torch.cat([self._dp_sums.reshape(-1), self._dp_hist[:top].to(torch.float64)])
                 allreduce_sum(buf)
                 self._dp_sums.copy_(buf[:2 * ob].view(ob, 2))
-                self._dp_hist[:top].copy_(buf[2 * ob:].to(torch.int32))
+                # counts reach 2^32 - 1 (n_global < 2^32): through int64 and the low 32 bits, the uint32
+                # pattern k_stats_sel reads (a direct fp64 -> int32 cast is undefined past 2^31)
+                self._dp_hist[:top].copy_((buf[2 * ob:].to(torch.int64) & 0xFFFFFFFF).to(torch.int32))
             else:
                 allreduce_sum(self._dp_hist)
 

@@ -83,7 +83,9 @@ sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx_dev, int B, floa
 /* update_obs_mean_std (:83-96): fp64 mean / std(ddof=0) over the live obs,
  * exact np.percentile(.., 99 / 1, linear) by radix select, running max/min.
  * Skipped (returns *updated = 0) when len <= 10.  max/min are read-modify-
- * written (first_update != 0 overwrites them). */
+ * written (first_update != 0 overwrites them).  A call on rows unchanged since
+ * the last call (no AddObs / AddStep / Reset / GetView in between) reuses the
+ * stored sample bracket; the result is exact either way. */
 sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
                             int first_update, void* stream);
 /* Data-parallel update_obs_mean_std over the union of the ranks' replay shards
@@ -123,6 +125,7 @@ typedef struct {
   uint8_t* done;       /* [capacity]        */
   uint8_t* end;        /* [capacity]        */
 } sppReplayView;
+/* Raw device arrays of the ring; counts as a possible write (the next ObsStats re-brackets). */
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);
 /* The SURVEY §8b constructor: n_envs sizes the per-step metadata ring up front; compat_mode must
  * be 1 (the reference obs-index ring with the Q6 wrap -- the only ring rltoolkit has);

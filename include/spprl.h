@@ -109,7 +109,13 @@ sppStatus sppReplayObsStatsDP(sppReplayHandle h, int step, const float* pivot /*
  *   after 2,3,4,5   all-reduce (sum) `hist` (uint32, ob*2*2*256)
  * Phase 6 writes mean / std / max_obs / min_obs (identical on every rank).  Exact: a sample miss or an
  * overflowed candidate list selects over the raw columns in the same fixed phases.  n_global < 2^31.
- * `pivot` (replicated) may alias `mean`: phase 6 reads pivot[c] before it writes mean[c]. */
+ * `pivot` (replicated) may alias `mean`: phase 6 reads pivot[c] before it writes mean[c].
+ * Bracket reuse: every rank may skip phase 0 and its all-gather and pass phase 1 as
+ * (1 | SPP_DP1_REUSE_BRACKET) when the shards are unchanged since the previous call (the decision
+ * must be the same on every rank: the host's lockstep-checked write count).  Phase 1 then keeps the
+ * union bracket of that call (or recomputes it from `samp`, which holds the same union sample on every
+ * rank, if this handle's bounds were overwritten since).  Any bracket gives the exact result. */
+#define SPP_DP1_REUSE_BRACKET 0x100
 int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_global);
 sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot /*[ob]*/,
                                uint32_t* samp, double* exch, uint32_t* hist, int64_t n_global, float* mean,

@@ -121,6 +121,7 @@ struct sppReplay {
   // back to the raw column), so the generation only decides the cost, never the value.
   uint64_t gen = 0, sf_gen = ~0ull;
   int64_t sf_len = -1;
+  bool bounds_dp1 = false;  // sf_bounds holds the union bracket of the last sppReplayObsStatsDP1 phase 1
   void* dp_q = nullptr;  // one-pass data-parallel statistics: per (column, target, rank) query state
   uint32_t* dp_cand = nullptr;  // and the compacted local candidates + counts
 };
@@ -494,6 +495,7 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
                          h->sf_bounds, ns, (int64_t)0, 4);
     h->sf_gen = h->gen;
     h->sf_len = len;
+    h->bounds_dp1 = false;
   }
   const int cap = st_list_cap(ob);
   StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
@@ -516,6 +518,8 @@ int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_globa
 sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot, uint32_t* samp,
                                double* exch, uint32_t* hist, int64_t n_global, float* mean, float* std,
                                float* max_obs, float* min_obs, int first_update, void* stream) {
+  const bool reuse = phase == (1 | SPP_DP1_REUSE_BRACKET);
+  if (reuse) phase = 1;
   SPP_REQUIRE(h && pivot && samp && exch && hist && mean && std && max_obs && min_obs && phase >= 0 && phase <= 6 &&
                   world >= 1 && rank >= 0 && rank < world,
               SPP_E_INVALID_ARG, "obs_stats_dp1: bad args (phase %d, rank %d of %d)", phase, rank, world);
@@ -545,13 +549,19 @@ sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank
     else SPP_CHECK_HIP(hipMemsetAsync(mine, 0, sizeof(uint32_t) * ob * Sl, st));  // (lockstep shards: not reached)
   } else if (phase == 1) {
     const int S = world * Sl;  // <= kStSampBig
-    // margin 5 sigma + 4 sample ranks: a miss costs the raw-column select of the rounds, not correctness
-    if (S > kStSampSmall)
-      hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
-                         h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
-    else
-      hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
-                         h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
+    // margin 5 sigma + 4 sample ranks: a miss costs the raw-column select of the rounds, not correctness.
+    // reuse (decided alike on every rank): keep the last union bracket; if the N = 1 path overwrote the
+    // bounds since, recompute them from samp (the same union sample on every rank)
+    if (!(reuse && h->bounds_dp1)) {
+      if (S > kStSampSmall)
+        hipLaunchKernelGGL(k_st_bracket<kStSampBig / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
+                           h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
+      else
+        hipLaunchKernelGGL(k_st_bracket<kStSampSmall / 1024>, dim3(ob), dim3(1024), 0, st, (const uint32_t*)samp, S,
+                           h->sf_bounds, Sl, (int64_t)ob * Sl, 5);
+      h->bounds_dp1 = true;
+      h->sf_gen = ~0ull;  // the N = 1 path must not take these (union) bounds for its own
+    }
     StPassArgs pa{h->d, len, h->sf_bounds, pivot, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
                   h->sf_ovf_n, cap};
     st_launch_pass(pa, nblk, st);

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("SPPRL_LIB") or os.path.join(HERE, "libspprl.so")
 SPP_ALGO_SAC_ACM, SPP_ALGO_DDPG_ACM, SPP_ALGO_SAC = 1, 2, 3
 SPP_BUCKET_CRITIC, SPP_BUCKET_ACTOR, SPP_BUCKET_ACM, SPP_BUCKET_ALL = range(4)
 SPP_COMM_ID_BYTES = 128
+SPP_DP1_REUSE_BRACKET = 0x100  # sppReplayObsStatsDP1 phase flag (spprl.h)
 NUM_LOSSES = 8
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,

@@ -280,10 +280,23 @@ class BufferAcMOffPolicy:
             self._dp1_key = key
         first = 0 if self._have_minmax else 1
         mine = self._dp1_samp[R * ob * Sl:(R + 1) * ob * Sl]
+        # Shards unchanged since the last call (timestep-write count, checked in lockstep across ranks, and
+        # the same global row count): every rank skips the sample and its all-gather and keeps the union
+        # bracket.  Rows changed by add_obs alone keep a stale bracket, which is still exact.
+        gen = getattr(self, "_gen", 0)
+        bkey = (gen, n_global, key)
+        # only on a write count the lockstep exchange verified (else a rank out of step would skip the
+        # all-gather the others run)
+        verified = getattr(self, "_ng_gen", None) == gen and getattr(self, "_ng", None) == n_global
+        reuse = verified and getattr(self, "_dp1_bkey", None) == bkey
+        self._dp1_bkey = bkey
         for phase in range(7):
+            if reuse and phase == 0:
+                continue
+            ph = (1 | _lib.SPP_DP1_REUSE_BRACKET) if (reuse and phase == 1) else phase
             # pivot = the running mean itself (replicated across ranks): phase 6 reads pivot[c] before it
             # writes mean[c], in the same thread
-            call("sppReplayObsStatsDP1", self._h, phase, W, R, ptr(self.obs_mean), ptr(self._dp1_samp),
+            call("sppReplayObsStatsDP1", self._h, ph, W, R, ptr(self.obs_mean), ptr(self._dp1_samp),
                  ptr(self._dp1_exch), ptr(self._dp1_hist), n_global, ptr(self.obs_mean), ptr(self.obs_std),
                  ptr(self.max_obs), ptr(self.min_obs), first, stream_handle())
             if phase == 0:

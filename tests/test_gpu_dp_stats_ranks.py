@@ -33,7 +33,7 @@ def _shards(ob, kind="t3"):
             for n in (6000, 7321)]
 
 
-def _worker(rank, port, ob, use_host, q, proto="stepwise", kind="t3"):
+def _worker(rank, port, ob, use_host, q, proto="stepwise", kind="t3", repeat=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
@@ -49,8 +49,23 @@ def _worker(rank, port, ob, use_host, q, proto="stepwise", kind="t3"):
         z = np.zeros(n, bool)
         rb.add_timestep_batch(sl[:n], sl[1:], torch.zeros(n, ob), np.zeros(n, np.float32), z, z, torch.zeros(n, 2))
         rb.obs_mean.zero_()  # replicated pivot
+        ag, gathers = (make_allgather() if proto == "onepass" else None), [0]
+
+        class CountingGather:  # the sample all-gather, counted
+            def __init__(self, inner):
+                self.world, self.rank = inner.world, inner.rank
+
+            def __call__(self, *a):
+                gathers[0] += 1
+                return ag(*a)
+
+        cg = CountingGather(ag) if ag is not None else None
         rb.update_obs_mean_std_dp(make_allreduce_sum(), host_sum=make_host_allreduce_sum() if use_host else None,
-                                  allgather=make_allgather() if proto == "onepass" else None)
+                                  allgather=cg)
+        if repeat:  # a second call on the same shards (one-pass: reuses the union bracket, no all-gather)
+            rb.update_obs_mean_std_dp(make_allreduce_sum(), host_sum=make_host_allreduce_sum() if use_host else None,
+                                      allgather=cg)
+            assert cg is None or gathers[0] == 1, gathers
         torch.cuda.synchronize()
         q.put((rank, rb.obs_mean.cpu().numpy(), rb.obs_std.cpu().numpy(), rb.max_obs.cpu().numpy(),
                rb.min_obs.cpu().numpy()))
@@ -59,15 +74,21 @@ def _worker(rank, port, ob, use_host, q, proto="stepwise", kind="t3"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ob,use_host,proto,kind", [(11, True, "stepwise", "t3"), (111, False, "stepwise", "t3"),
-                                                    (11, True, "onepass", "t3"), (111, True, "onepass", "t3"),
-                                                    (17, True, "onepass", "skew"), (11, True, "onepass", "ties")])
-def test_dp_obs_stats_two_ranks_match_union(ob, use_host, proto, kind):
-    """proto: the stepwise radix protocol or the one-pass sample-bracketed one (sppReplayObsStatsDP1)."""
+@pytest.mark.parametrize("ob,use_host,proto,kind,repeat", [(11, True, "stepwise", "t3", False),
+                                                           (111, False, "stepwise", "t3", False),
+                                                           (11, True, "onepass", "t3", False),
+                                                           (111, True, "onepass", "t3", False),
+                                                           (17, True, "onepass", "skew", False),
+                                                           (11, True, "onepass", "ties", False),
+                                                           (17, True, "onepass", "skew", True),
+                                                           (111, False, "onepass", "t3", True)])
+def test_dp_obs_stats_two_ranks_match_union(ob, use_host, proto, kind, repeat):
+    """proto: the stepwise radix protocol or the one-pass sample-bracketed one (sppReplayObsStatsDP1);
+    repeat: a second call on unchanged shards (bracket reuse) must give the same exact statistics."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, ob, use_host, q, proto, kind)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, ob, use_host, q, proto, kind, repeat)) for r in range(2)]
     for p in procs:
         p.start()
     res = collect(q, procs, timeout=180)

@@ -20,7 +20,8 @@ FLOPs per env-step equal the reference cadence (one grad step of 100 samples per
          ppo_hcheetah (configs[3] per-GPU shape: 16384 envs / 8 GPUs = 2048, one PPO_AcM iteration per step)
          vanilla_sac_hcheetah (configs[0]: vanilla SAC, 1 env, the reference cadence frame by frame;
                                one step = one frame)
-N > 1: one process per GPU (torchrun), each with E envs and a local replay shard; gradient
+N > 1: one process per GPU (torchrun; `bench.py --gpus N` started without one launches it as a child
+process and relays rank 0's JSON line), each with E envs and a local replay shard; gradient
 buckets are averaged with RCCL all-reduce at the update's exchange points (critic grads,
 actor grads, ACM grads); value = all ranks' env-steps / max-over-ranks time.
 
@@ -525,8 +526,43 @@ def native_comm(world, rank, local):
     return NativeComm(rank, world, local, share)
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``bench.py --gpus N`` (N > 1) started without a launcher: run it as one process per GPU under
+    ``torch.distributed.run`` (a CHILD process; this parent never touches the GPU, so no exec after GPU
+    init), forward every output line to stderr except the JSON result line(s), which rank 0 prints and
+    this process relays on stdout, and exit with the child's code."""
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC (the only mode the host supports)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in p.stdout:
+        t = line.strip()
+        if t.startswith("{") and '"metric"' in t:
+            print(t, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return p.wait()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: WORLD_SIZE=%s but --gpus %d: launch one rank per GPU with --gpus equal to the "
+                         "rank count\n" % (env_world, args.gpus))
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -88,6 +88,10 @@ sppStatus sppReplayGather(sppReplayHandle h, const int64_t* idx_dev, int B, floa
  * stored sample bracket; the result is exact either way. */
 sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* max_obs, float* min_obs,
                             int first_update, void* stream);
+/* Test hook of the sample-bracketed statistics (sppReplayObsStats, sppReplayObsStatsDP1): lower the per-pass-
+ * workgroup candidate-list capacity to list_cap and the per-(column, target) overflow list to ovf_cap keys (0:
+ * the full capacities), so the overflow fallbacks run at small sizes.  Results stay exact at any capacity. */
+sppStatus sppReplaySetObsStatsCaps(sppReplayHandle h, int list_cap, int ovf_cap);
 /* Data-parallel update_obs_mean_std over the union of the ranks' replay shards
  * (SURVEY.md §8e): exact global mean / std (fp64 sums about a replicated pivot,
  * e.g. the current obs_mean) and exact global 99th / 1st percentiles (radix select
@@ -298,15 +302,21 @@ sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
  * launch: step k's batch = rows [k*bs, k*bs + bs) of x [nsteps*bs][2ob] / y [nsteps*bs][ac]
  * (acm_cat inputs and targets, e.g. from sppReplayGatherAcm), bs <= 32768.  Parameters stay in
  * LDS, moments in registers (update_acm epochs, update_acm_batches).  loss_sum += sum of the
- * steps' batch losses.  AcM agents (SAC_AcM) only.  bs <= 128: one workgroup; larger batches
- * spread each step over min(ceil(bs / 64), 256) workgroups that sum the step's gradient in a fixed
- * order (deterministic) behind one arrival barrier per step (two past 24 workgroups: a sliced
- * reduction, then the reduced gradient). */
+ * steps' batch losses.  AcM agents (SAC_AcM / PPO_AcM) only.  bs <= 64: one workgroup; larger batches
+ * spread each step over ceil(bs / 64) workgroups (all co-resident: bs <= sppAcmSgdMaxBatch) that sum
+ * the step's gradient in a fixed order (deterministic) behind one arrival barrier per step (two past
+ * 4 workgroups: a sliced reduction, then the reduced gradient). */
 sppStatus sppAcmSgd(sppAgentHandle h, const float* x_dev, const float* y_dev, int nsteps, int bs, float* loss_sum,
                     void* stream);
 /* Synchronous: 1 if a multi-workgroup sppAcmSgd launch timed out waiting for its workgroups (its
  * results are then invalid), else 0. */
 sppStatus sppAcmSgdStatus(sppAgentHandle h, int* timed_out_host);
+/* Stream-ordered form: enqueues a copy of the timeout flag into *timed_out_pinned (pinned host memory,
+ * read after the stream has passed this point); 0 is written when no multi-workgroup launch ran. */
+sppStatus sppAcmSgdStatusAsync(sppAgentHandle h, int* timed_out_pinned, void* stream);
+/* Largest bs sppAcmSgd accepts on this device for this agent: every workgroup of a step must be resident
+ * at once (the arrival barrier), so min(32768, 64 x occupancy x CUs).  Larger batches: SPP_E_SHAPE. */
+int sppAcmSgdMaxBatch(sppAgentHandle h);
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
 
 /* Per-kernel device timing (HIP events on the launch stream), for measurement:

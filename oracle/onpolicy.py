@@ -50,9 +50,9 @@ def actor_dist(p, x, lim):
     return torch.distributions.Independent(normal, 1)
 
 
-def _params(flat, layout):
+def _params(flat, layout, dtype=torch.float32):
     out, o = {}, 0
-    flat = torch.as_tensor(np.asarray(flat), dtype=torch.float32)
+    flat = torch.as_tensor(np.asarray(flat), dtype=dtype)
     for n, shape in layout:
         k = int(np.prod(shape))
         out[n] = flat[o:o + k].reshape(shape).clone().requires_grad_(True)
@@ -64,11 +64,11 @@ def _flat(gs):
     return torch.cat([g.reshape(-1) for g in gs]).numpy()
 
 
-def critic_step(flat, ob, x, q):
-    """Returns (loss, grad) of 0.5 * mean((q - V(x))^2)."""
-    p = _params(flat, critic_layout(ob))
-    v = critic(p, torch.as_tensor(x)).squeeze(-1)
-    adv = torch.as_tensor(q) - v
+def critic_step(flat, ob, x, q, dtype=torch.float32):
+    """Returns (loss, grad) of 0.5 * mean((q - V(x))^2) (dtype float64: a reference for large batches)."""
+    p = _params(flat, critic_layout(ob), dtype)
+    v = critic(p, torch.as_tensor(x, dtype=dtype)).squeeze(-1)
+    adv = torch.as_tensor(q, dtype=dtype) - v
     loss = 0.5 * adv.pow(2).mean()
     return loss.item(), _flat(torch.autograd.grad(loss, list(p.values())))
 
@@ -89,6 +89,39 @@ def actor_step(flat, ob, aout, lim, x, act, lp_old, adv, eps_clip=0.2, entropy_c
     if next_obs is not None:
         out["dist"] = torch.nn.functional.mse_loss(torch.as_tensor(act), torch.as_tensor(next_obs)).item()
     return out, g
+
+
+def update_actor_epochs(flat, ob, aout, lim, x, act, lp_old, adv, next_obs, lr, max_epochs, kl_threshold,
+                        batch_size, eps_clip=0.2, entropy_coef=0.0, custom_loss=0.0, perms=None):
+    """PPO_AcM.update_actor_acm (rltoolkit/acm/on_policy.py:164-216; PPO.update_actor ppo.py:152-192):
+    epochs of minibatch Adam steps on clip_loss - entropy_coef * entropy, stopped when the KL of the
+    previous epoch's LAST minibatch (pre-step log-probs, utils.kl_divergence utils.py:48-59) reached the
+    threshold; losses summed over the steps and divided by i + 1 after the loop (one more than the epochs
+    run when the check broke it).  ``adv`` are the already normalised advantages; ``perms`` one row
+    permutation per epoch (identity by default).  Returns (flat, losses, kls, counter increment)."""
+    from oracle.adam import OracleAdam
+
+    flat = torch.from_numpy(np.array(flat, np.float32, copy=True))
+    opt = OracleAdam([flat], lr)
+    n = len(x)
+    tot = {"actor": 0.0, "entropy": 0.0, "policy": 0.0, "dist": 0.0}
+    kl, kls, i = 0.0, [], 0
+    for i in range(max_epochs):
+        if kl >= kl_threshold:
+            break
+        perm = np.arange(n) if perms is None else np.asarray(perms[i])
+        for s in range(0, n, batch_size):
+            b = perm[s:s + batch_size]
+            out, g = actor_step(flat.numpy(), ob, aout, lim, x[b], act[b], lp_old[b], adv[b], eps_clip=eps_clip,
+                                entropy_coef=entropy_coef, next_obs=next_obs[b])
+            opt.step([torch.from_numpy(g)])
+            tot["actor"] += out["actor"]
+            tot["entropy"] += out["entropy"]
+            tot["dist"] += out["dist"]
+            tot["policy"] += out["actor"] - entropy_coef * out["entropy"] + custom_loss * out["dist"]
+            kl = out["kl"]
+        kls.append(kl)
+    return flat.numpy(), {k: v / (i + 1) for k, v in tot.items()}, kls, i + 1
 
 
 def act(flat, ob, aout, lim, x, eps=None):

@@ -87,6 +87,7 @@ def _compile(src, verbose):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stdout[-8000:]))
+    os.utime(obj, (t0, t0))  # stamped with the compile's start: a source edited meanwhile stays newer
     import json
 
     with open(obj + ".res.json", "w") as f:
@@ -138,7 +139,7 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
             print("libspprl.so up to date")
         return OUT
     os.makedirs(OBJ, exist_ok=True)
-    t0 = time.time()
+    t0 = time.time()  # the library is stamped with this time: a source edited during the build stays newer
     srcs = units()
     jobs = jobs or min(len(srcs), max(1, min(os.cpu_count() or 1, 8)))
     if verbose:
@@ -150,6 +151,7 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
     report_spills(objs, verbose)
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs)
     os.replace(OUT + ".tmp", OUT)
+    os.utime(OUT, (t0, t0))
     if verbose:
         print("built %s in %.0fs" % (OUT, time.time() - t0))
     return OUT

@@ -122,6 +122,7 @@ struct sppReplay {
   uint64_t gen = 0, sf_gen = ~0ull;
   int64_t sf_len = -1;
   bool bounds_dp1 = false;  // sf_bounds holds the union bracket of the last sppReplayObsStatsDP1 phase 1
+  int st_cap_lim = 0, st_ovf_lim = 0;  // sppReplaySetObsStatsCaps (0: the full capacities)
   void* dp_q = nullptr;  // one-pass data-parallel statistics: per (column, target, rank) query state
   uint32_t* dp_cand = nullptr;  // and the compacted local candidates + counts
 };
@@ -454,6 +455,23 @@ static int st_nblk(sppReplayHandle h) {  // every pass workgroup resident at onc
   return std::max(1, std::min(kStNblkMax, 4 * h->num_cu));
 }
 
+// candidate-list capacities of the sample-bracketed statistics (sppReplaySetObsStatsCaps may lower them so
+// the overflow paths run at small sizes; the allocations keep the full strides)
+static int st_cap(sppReplayHandle h) {
+  const int c = st_list_cap(h->d.ob);
+  return h->st_cap_lim > 0 ? std::min(c, h->st_cap_lim) : c;
+}
+static int st_ovf_cap(sppReplayHandle h) {
+  return h->st_ovf_lim > 0 ? std::min(kStOvfCap, h->st_ovf_lim) : kStOvfCap;
+}
+
+sppStatus sppReplaySetObsStatsCaps(sppReplayHandle h, int list_cap, int ovf_cap) {
+  SPP_REQUIRE(h && list_cap >= 0 && ovf_cap >= 0, SPP_E_INVALID_ARG, "set_obs_stats_caps: bad args");
+  h->st_cap_lim = list_cap;
+  h->st_ovf_lim = ovf_cap;
+  return SPP_OK;
+}
+
 static sppStatus stats_fast_alloc(sppReplayHandle h) {
   if (h->sf_bounds) return SPP_OK;
   const int ob = h->d.ob, nb = kStNblkMax;
@@ -497,12 +515,12 @@ sppStatus sppReplayObsStats(sppReplayHandle h, float* mean, float* std, float* m
     h->sf_len = len;
     h->bounds_dp1 = false;
   }
-  const int cap = st_list_cap(ob);
+  const int cap = st_cap(h), ovf_cap = st_ovf_cap(h);
   StPassArgs pa{h->d, len, h->sf_bounds, nullptr, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
-                h->sf_ovf_n, cap};
+                h->sf_ovf_n, cap, ovf_cap};
   st_launch_pass(pa, nblk, st);
   StSelArgs sa{h->d, len, nblk, cap, h->sf_part, h->sf_cpart, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf,
-               h->sf_ovf_n, nullptr, mean, std, max_obs, min_obs, first_update};
+               h->sf_ovf_n, nullptr, mean, std, max_obs, min_obs, first_update, ovf_cap};
   hipLaunchKernelGGL(k_st_select, dim3(ob, 2), dim3(kStSelThreads), 0, st, sa);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
@@ -541,8 +559,8 @@ sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank
   hipStream_t st = S(stream);
   const int Sl = sppReplayObsStatsDP1SampleRows(h, world, n_global);
   uint32_t* mine = samp + (int64_t)rank * ob * Sl;
-  const int cap = st_list_cap(ob);
-  StDpArgs da{h->d, len, n_global, nblk, cap, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf, h->sf_ovf_n,
+  const int cap = st_cap(h), ovf_cap = st_ovf_cap(h);
+  StDpArgs da{h->d, len, n_global, nblk, cap, ovf_cap, h->sf_bounds, h->sf_wgl, h->sf_wgn, h->sf_ovf, h->sf_ovf_n,
               h->dp_cand, dp_ncand, exch, hist, (DpQuery*)h->dp_q, pivot, mean, std, max_obs, min_obs, first_update};
   if (phase == 0) {
     if (len > 0) hipLaunchKernelGGL(k_st_sample, dim3(cdiv(Sl, 256)), dim3(256), 0, st, h->d, len, Sl, mine);
@@ -563,9 +581,10 @@ sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank
       h->sf_gen = ~0ull;  // the N = 1 path must not take these (union) bounds for its own
     }
     StPassArgs pa{h->d, len, h->sf_bounds, pivot, h->sf_part, h->sf_cpart, h->sf_wgl, h->sf_wgn, h->sf_ovf,
-                  h->sf_ovf_n, cap};
+                  h->sf_ovf_n, cap, ovf_cap};
     st_launch_pass(pa, nblk, st);
-    hipLaunchKernelGGL(k_dp_reduce, dim3(ob, 2), dim3(kStSelThreads), 0, st, ob, nblk, cap, (const double*)h->sf_part,
+    hipLaunchKernelGGL(k_dp_reduce, dim3(ob, 2), dim3(kStSelThreads), 0, st, ob, nblk, cap, ovf_cap,
+                       (const double*)h->sf_part,
                        (const uint32_t*)h->sf_cpart, (const uint32_t*)h->sf_wgl, (const uint32_t*)h->sf_wgn,
                        (const uint32_t*)h->sf_ovf, (const uint32_t*)h->sf_ovf_n, exch, h->dp_cand, dp_ncand);
   } else if (phase <= 5) {
@@ -867,9 +886,10 @@ struct sppAgent {
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
   float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
-  // multi-workgroup AcM SGD (sppAcmSgd with bs > kSgdMaxBatch): gradient slabs, {counter, timeout flag}
+  // multi-workgroup AcM SGD (sppAcmSgd with bs > kMfR): gradient slabs, {counter, timeout flag}
   DevArray<float> sgd_slab;
   DevArray<int> sgd_sync;
+  int sgd_max_wg = -1;  // co-resident k_acm_sgd_mf workgroups (acm_sgd_max_wg, cached)
   // per-kernel timing (HIP events on the launch stream)
   bool timing = false;
   std::vector<hipEvent_t> tev[5];
@@ -1888,11 +1908,38 @@ sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
   return SPP_OK;
 }
 
+// co-resident workgroups of the multi-workgroup k_acm_sgd_mf on this device (0: no instantiation)
+static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
+  if (a->sgd_max_wg >= 0) return a->sgd_max_wg;
+  const void* k = nullptr;
+  if (ob == 11 && ac == 3) k = (const void*)k_acm_sgd_mf<22, 3, true>;
+  else if (ob == 17 && ac == 6) k = (const void*)k_acm_sgd_mf<34, 6, true>;
+  else if (ob == 3 && ac == 1) k = (const void*)k_acm_sgd_mf<6, 1, true>;
+  int per_cu = 0;
+  if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kMfTH, 0) != hipSuccess) per_cu = 0;
+  a->sgd_max_wg = std::min(kMfMaxWG, per_cu * a->num_cu);
+  return a->sgd_max_wg;
+}
+
+int sppAcmSgdMaxBatch(sppAgentHandle a) {
+  if (!a || a->ddpg) return 0;
+  return kMfR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
+}
+
+sppStatus sppAcmSgdStatusAsync(sppAgentHandle a, int* timed_out_pinned, void* stream) {
+  SPP_REQUIRE(a && timed_out_pinned, SPP_E_INVALID_ARG, "acm_sgd_status_async: null");
+  if (a->sgd_sync.ptr)
+    SPP_CHECK_HIP(hipMemcpyAsync(timed_out_pinned, a->sgd_sync.ptr + 1, sizeof(int), hipMemcpyDeviceToHost, S(stream)));
+  else
+    *timed_out_pinned = 0;
+  return SPP_OK;
+}
+
 sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps, int bs, float* loss_sum,
                     void* stream) {
   SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
-  SPP_REQUIRE(bs <= kSgdMaxBatch * kSgdMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kSgdMaxBatch * kSgdMaxWG);
+  SPP_REQUIRE(bs <= kMfR * kMfMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kMfR * kMfMaxWG);
   sppStatus s = check_ready(a);
   if (s) return s;
   if (nsteps == 0) return SPP_OK;
@@ -1902,9 +1949,11 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
                bs, nullptr, nullptr, nullptr};
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
-#ifndef SPP_SGD_SCALAR
   // the MFMA form (sgd_mf.hip): 64 rows per workgroup, gradients summed over the workgroups
   const int nwg = cdiv(bs, kMfR);
+  // the per-step arrival barrier needs every workgroup resident at once
+  SPP_REQUIRE(nwg <= acm_sgd_max_wg(a, ob, ac), SPP_E_SHAPE, "acm_sgd: batch %d needs %d co-resident workgroups > %d",
+              bs, nwg, acm_sgd_max_wg(a, ob, ac));
   if (nwg > 1) {
     g.bsl = cdiv(bs, nwg);
     if (!a->sgd_slab.ptr) {
@@ -1921,28 +1970,6 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
 #define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                              \
   if (mw) hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, true>), dim3(nwg), dim3(kMfTH), 0, st, g);    \
   else hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, false>), dim3(1), dim3(kMfTH), 0, st, g)
-#else
-  // batches past one workgroup's rows: ~64 rows per workgroup, gradients summed over the workgroups
-  int nwg = 1;
-  if (bs > kSgdMaxBatch) {
-    nwg = std::min(cdiv(bs, kSgdBigRows), kSgdMaxWG);
-    g.bsl = (int)round_up(cdiv(bs, nwg), 4);
-    nwg = cdiv(bs, g.bsl);
-    if (!a->sgd_slab.ptr) {
-      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)(2 * kSgdMaxWG + 2) * kSlabStride));  // + the reduced slabs
-      SPP_CHECK_HIP(a->sgd_sync.alloc(2));  // {arrival counter, timeout flag}
-      SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, 2 * sizeof(int), st));
-    }
-    g.slab = a->sgd_slab.ptr;
-    g.ctr = a->sgd_sync.ptr;
-    g.err = a->sgd_sync.ptr + 1;
-    SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, sizeof(int), st));
-  }
-  const bool mw = nwg > 1;
-#define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                          \
-  if (mw) hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_, true>), dim3(nwg), dim3(TH_), 0, st, g); \
-  else hipLaunchKernelGGL((k_acm_sgd<IN_, AC_, TH_>), dim3(1), dim3(TH_), 0, st, g)
-#endif
   if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3, 256);
   else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6, 512);
   else if (ob == 3 && ac == 1) SPP_SGD_LAUNCH(6, 1, 512);

@@ -226,9 +226,10 @@ struct StPassArgs {
   uint32_t* cpart;         // [nblk][ob][6]       count partials: per target outside, == lo, == hi
   uint32_t* wgl;           // [nblk][ob][2][cap]  per-workgroup candidate lists
   uint32_t* wgn;           // [nblk][ob][2]       keys in each list (<= cap)
-  uint32_t* ovf;           // [ob][2][kStOvfCap]  keys past a list's capacity
+  uint32_t* ovf;           // [ob][2][kStOvfCap]  keys past a list's capacity (row stride kStOvfCap)
   uint32_t* ovf_n;         // [ob][2]             (zero on entry; k_st_select re-zeroes)
-  int cap;                 // st_list_cap(ob)
+  int cap;                 // st_list_cap(ob), or less (sppReplaySetObsStatsCaps)
+  int ovf_cap;             // keys kept per overflow list: kStOvfCap, or less (sppReplaySetObsStatsCaps)
 };
 
 // WIDE: ob > 64 (two column halves per lane).  OFF32: the obs ring is < 4 GiB, so every load is a
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(kStPassThreads) __attribute__((amdgpu_waves_per_eu(
             lst[ct * cap + f] = key;
           } else {
             const uint32_t o = atomicAdd(&a.ovf_n[ct], 1u);
-            if (o < (uint32_t)kStOvfCap) a.ovf[(int64_t)ct * kStOvfCap + o] = key;
+            if (o < (uint32_t)a.ovf_cap) a.ovf[(int64_t)ct * kStOvfCap + o] = key;
           }
         }
       }
@@ -446,6 +447,7 @@ struct StSelArgs {
   const float* pivot;
   float *mean, *std, *max_out, *min_out;
   int first_update;
+  int ovf_cap;
 };
 
 __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
   const uint32_t off = woff + incl - nb;  // this workgroup list's first slot
   const int64_t n = a.len;
   const uint32_t novf_raw = a.ovf_n[ct];
-  const uint32_t novf = min(novf_raw, (uint32_t)kStOvfCap);
+  const uint32_t novf = min(novf_raw, (uint32_t)a.ovf_cap);
   if (tid == 0) {
     double s1 = 0.0, s2 = 0.0;
     int64_t out = 0, eql = 0, eqh = 0, nl = 0;
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
       nl += rc[3][q];
     }
     const int64_t ncd = nl + novf_raw;
-    const bool cand_ok = novf_raw <= (uint32_t)kStOvfCap;
+    const bool cand_ok = novf_raw <= (uint32_t)a.ovf_cap;
     if (t == 0) {
       const double mu = s1 / (double)n;
       const double var = fmax(s2 / (double)n - mu * mu, 0.0);
@@ -654,7 +656,8 @@ constexpr int kDpCandCap = 32768;  // compacted local candidates per (column, ta
 // Grid (ob, 2), kStSelThreads threads: the pass's slabs -> exch (this rank's moments and counts), and this
 // rank's candidate keys of (column, target) compacted to cand[ct][0 .. ncand) (block prefix sum over the
 // workgroup lists, then the overflow list) so every round reads them with the whole workgroup.
-__global__ __launch_bounds__(kStSelThreads) void k_dp_reduce(int ob, int nblk, int cap, const double* __restrict__ part,
+__global__ __launch_bounds__(kStSelThreads) void k_dp_reduce(int ob, int nblk, int cap, int ovf_cap,
+                                                            const double* __restrict__ part,
                                                             const uint32_t* __restrict__ cpart,
                                                             const uint32_t* __restrict__ wgl,
                                                             const uint32_t* __restrict__ wgn,
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_reduce(int ob, int nblk, i
     if (q < wv) woff += rc[3][q];
     tot += rc[3][q];
   }
-  const uint32_t no_raw = ovf_n[ct], no = min(no_raw, (uint32_t)kStOvfCap);
+  const uint32_t no_raw = ovf_n[ct], no = min(no_raw, (uint32_t)ovf_cap);
   const uint32_t n_all = tot + no;
   uint32_t* dst = cand + (int64_t)ct * kDpCandCap;
   __shared__ uint32_t offs[T + 1];  // exclusive list offsets; offs[nblk] = tot
@@ -750,8 +753,8 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_reduce(int ob, int nblk, i
     e[0] = out;
     e[1] = eql;
     e[2] = eqh;
-    e[3] = (double)n_all;
-    e[4] = no_raw > (uint32_t)kStOvfCap ? 1.0 : 0.0;
+    e[3] = (double)tot + (double)no_raw;  // the true candidate count (a capped overflow list still counts all)
+    e[4] = no_raw > (uint32_t)ovf_cap ? 1.0 : 0.0;
     ncand[ct] = n_all <= (uint32_t)kDpCandCap ? n_all : 0xffffffffu;  // all-ones: walk the lists
   }
 }
@@ -765,7 +768,7 @@ struct StDpArgs {
   ReplayDev r;
   int64_t len;         // local live rows
   int64_t n_global;
-  int nblk, cap;
+  int nblk, cap, ovf_cap;
   const uint32_t* bounds;
   const uint32_t* wgl;
   const uint32_t* wgn;
@@ -959,7 +962,7 @@ __global__ __launch_bounds__(kStSelThreads) void k_dp_round(StDpArgs a, int r) {
       const uint32_t* L = a.wgl + ((int64_t)tid * ob * 2 + ct) * a.cap;
       for (uint32_t i = 0; i < nb; ++i) hit(L[i], 1);
     }
-    const uint32_t no = min(a.ovf_n[ct], (uint32_t)kStOvfCap);
+    const uint32_t no = min(a.ovf_n[ct], (uint32_t)a.ovf_cap);
     const uint32_t* O = a.ovf + (int64_t)ct * kStOvfCap;
     for (uint32_t i = tid; i < no; i += T) hit(O[i], 1);
   }

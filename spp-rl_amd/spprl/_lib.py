@@ -141,6 +141,7 @@ _SIGS = {
     "sppReplayObsStatsDP": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_int, P(c_int), c_void_p]),
     "sppReplayObsStatsDP1SampleRows": (c_int, [c_void_p, c_int, c_int64]),
+    "sppReplaySetObsStatsCaps": (c_int, [c_void_p, c_int, c_int]),
     "sppReplayObsStatsDP1": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "sppObsNormalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
@@ -149,6 +150,8 @@ _SIGS = {
     "sppAdvNormalizeGlobal": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, n, bs
     "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
+    "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "sppAcmSgdMaxBatch": (c_int, [c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -84,7 +84,8 @@ def make_host_allreduce_sum(group=None):
     exchanged as CPU tensors over gloo: no device tensor, so no device synchronisation on the way.  For a
     group on another backend a gloo group over the SAME ranks is created once per distinct rank set (and
     per default group: it is rebuilt after the default group is destroyed and re-initialised); every
-    rank must call this in the same order (the agents' constructors do)."""
+    rank OF THE DEFAULT GROUP must call this in the same order, also for a subgroup it is not in
+    (``dist.new_group`` is collective over the default group; the agents' constructors do)."""
     if not dist.is_available() or not dist.is_initialized():
         return None
     if dist.get_world_size(group) == 1 and not _single_rank_exchange():
@@ -94,10 +95,16 @@ def make_host_allreduce_sum(group=None):
     g = group
     if dist.get_backend(group) != "gloo":
         ranks = tuple(dist.get_process_group_ranks(group if group is not None else dist.group.WORLD))
-        key = (id(dist.group.WORLD), ranks)
-        if key not in _HOST_GROUPS:
-            _HOST_GROUPS[key] = dist.new_group(ranks=list(ranks), backend="gloo")
-        g = _HOST_GROUPS[key]
+        world = dist.group.WORLD
+        ent = _HOST_GROUPS.get(ranks)
+        # keyed by rank set, validated by the identity of the default group it was made under (an id() of a
+        # destroyed default group may be reused by its successor; the object itself is held here)
+        if ent is None or ent[0] is not world:
+            # new_group is collective over the DEFAULT group: every rank of it must reach this line, also
+            # for a subgroup it is not a member of
+            ent = (world, dist.new_group(ranks=list(ranks), backend="gloo"))
+            _HOST_GROUPS[ranks] = ent
+        g = ent[1]
 
     def host_sum(x):
         many = isinstance(x, (list, tuple))

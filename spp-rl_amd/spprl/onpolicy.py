@@ -37,7 +37,7 @@ class OnPolicyNets:
     def __init__(self, ob, aout, ac_lim=1.0, actor_lr=3e-3, critic_lr=3e-4, ppo_epsilon=0.2, entropy_coef=0.0,
                  gamma=0.99, gae_lambda=0.95, critic_num_target_updates=10, num_critic_updates_per_target=10,
                  max_ppo_epochs=50, ppo_batch_size=1000, kl_div_threshold=0.15, normalize_adv=True,
-                 max_batch=4096, device="cuda", seed=None):
+                 max_batch=4096, device="cuda", seed=None, custom_loss=0.0):
         _lib.load()
         self.ob, self.aout, self.device = ob, aout, torch.device(device)
         self.gamma, self.gae_lambda = gamma, gae_lambda
@@ -45,6 +45,8 @@ class OnPolicyNets:
                                                                               num_critic_updates_per_target)
         self.max_ppo_epochs, self.ppo_batch_size, self.kl_div_threshold = max_ppo_epochs, ppo_batch_size, kl_div_threshold
         self.normalize_adv = normalize_adv
+        self.entropy_coef, self.custom_loss = float(entropy_coef), float(custom_loss)
+        self.kl_div_updates_counter = 0  # ppo.py:91, += epochs + 1 of each update_actor (ppo.py:192)
         self.max_batch = int(max_batch)
         cfg = _lib.OnPolicyConfig(ob, aout, actor_lr, critic_lr, ppo_epsilon, entropy_coef, self.max_batch)
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -179,7 +181,15 @@ class OnPolicyNets:
                                 out=outs[k])
             sums += outs.sum(0)
             kl = float(outs[-1, 1].item())  # KL of the epoch's last minibatch (ppo.py:188)
-        self.loss.update(actor=float(sums[0]) / (i + 1), entropy=float(sums[3]) / (i + 1), kl=kl)
+        # the reference divides by i + 1 after the loop: the epochs run when none stopped early, one more than
+        # that when the KL check broke the loop (on_policy.py:210-216, ppo.py:190-192)
+        s = sums.cpu().numpy().astype(np.float64)
+        d = float(i + 1)
+        self.loss.update(actor=s[0] / d, entropy=s[3] / d, kl=kl)
+        if nxt is not None:  # PPO_AcM: dist = mse(actions, next_obs) (data only: no gradient), and
+            # policy = actor - entropy_coef * entropy + custom_loss * dist per minibatch (on_policy.py:188-207)
+            self.loss.update(dist=s[2] / d, policy=(s[0] - self.entropy_coef * s[3] + self.custom_loss * s[2]) / d)
+        self.kl_div_updates_counter += i + 1
         return kl
 
     def act(self, obs, eps=None):

@@ -73,7 +73,8 @@ class PPO_AcM:
                                  num_critic_updates_per_target=num_critic_updates_per_target,
                                  max_ppo_epochs=max_ppo_epochs, ppo_batch_size=ppo_batch_size,
                                  kl_div_threshold=kl_div_threshold, normalize_adv=normalize_adv,
-                                 max_batch=max(Nmax, ppo_batch_size), device=self.device, seed=seed)
+                                 max_batch=max(Nmax, ppo_batch_size), device=self.device, seed=seed,
+                                 custom_loss=custom_loss)
         # the AcM and its replay ring (acm.py:127-141: size = pre-train samples * 1.1)
         ring = int(acm_ring_size or acm_pre_train_samples * 1.1)
         self.acm = SAC_AcM(env_name=env_name, env_spec=(ob, ac, ac_high, max_ep), acm_lr=acm_lr, buffer_size=ring,
@@ -93,6 +94,11 @@ class PPO_AcM:
 
         self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
+        if self.world > 1 and E == 1:
+            # one env per rank collects whole episodes: the ranks' ring-write records ("start" per episode)
+            # then differ in count and kind, which the rank-major all-gather of _flush_ring cannot carry
+            raise ValueError("PPO_AcM data parallel needs n_envs > 1 per rank (vectorized lockstep envs); "
+                             "got n_envs = 1 with world = %d" % self.world)
         if self.nets.allreduce is not None:
             self.acm.allreduce = self.acm.allreduce_sum = self.acm.host_sum = None
         self.acm._perm_seed = int(seed or 0) * 7919 + 17  # rank-independent epoch permutations
@@ -108,6 +114,14 @@ class PPO_AcM:
         self._ret_sums = torch.zeros(2, dtype=torch.float64, device=d)
         self._obs = None
         self._prev_slots = None
+
+    @property
+    def kl_div_updates_counter(self):  # ppo.py:91, on_policy.py:216 (epochs + 1 per update_actor_acm)
+        return self.nets.kl_div_updates_counter
+
+    @kl_div_updates_counter.setter
+    def kl_div_updates_counter(self, v):  # ppo.py:226 resets it after logging
+        self.nets.kl_div_updates_counter = int(v)
 
     # ---------------------------------------------------------------- helpers
     def _randn(self, t):

@@ -231,16 +231,19 @@ class BufferAcMOffPolicy:
         if n_global is None:
             gen = getattr(self, "_gen", 0)
             if getattr(self, "_ng_gen", None) != gen:
-                # (len, gen, 1) summed together: the ranks must be in lockstep (every rank writes timesteps
-                # the same number of times, so every rank reaches this exchange); a rank whose count of
-                # writes differs is caught here, not as a later hang
+                # (len, gen, gen^2, 1) summed together: the ranks must be in lockstep (every rank writes
+                # timesteps the same number of times, so every rank reaches this exchange).  All gens are equal
+                # iff world * sum(gen^2) == sum(gen)^2 (Cauchy-Schwarz), so EVERY rank sees a mismatch and
+                # raises.  The check covers ranks that all wrote since the last exchange; a rank that did not
+                # write at all skips this exchange and the mismatch then shows as a hang of the collective
+                # below (the trainer writes every rank's timesteps in the same vector step, so it cannot).
                 if host_sum is not None:
-                    ng, sgen, world = host_sum([len(self), gen, 1])
+                    ng, sgen, sgen2, world = host_sum([len(self), gen, gen * gen, 1])
                 else:
-                    n = torch.tensor([len(self), gen, 1], dtype=torch.int64, device=self.device)
+                    n = torch.tensor([len(self), gen, gen * gen, 1], dtype=torch.int64, device=self.device)
                     allreduce_sum(n)
-                    ng, sgen, world = (int(v) for v in n.tolist())
-                if sgen != gen * world:
+                    ng, sgen, sgen2, world = (int(v) for v in n.tolist())
+                if sgen * sgen != sgen2 * world:
                     raise RuntimeError("data-parallel replay shards out of lockstep: timestep-write counts "
                                        "differ across ranks (this rank %d, sum %d over %d ranks)" % (gen, sgen, world))
                 self._ng, self._ng_gen = ng, gen

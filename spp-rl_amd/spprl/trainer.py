@@ -38,7 +38,7 @@ import numpy as np
 import torch
 
 from . import config
-from ._lib import call, ptr, stream_handle
+from ._lib import SppError, call, load, ptr, stream_handle
 from .dp import make_allgather, make_allreduce, make_allreduce_sum, make_host_allreduce_sum, stream_key
 
 # ---------------------------------------------------------------- stats
@@ -588,9 +588,14 @@ class OffPolicyLoop:
         self._keep_acm_xy = (idx, x, y)
 
     def _acm_sgd_ok(self, bs):
-        """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank."""
-        return (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None and bs <= 32768
-                and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1)))
+        """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank, and
+        batches whose workgroups are all co-resident on this device (sppAcmSgdMaxBatch)."""
+        if not (getattr(self, "acm_kind", "acm") == "acm" and self.allreduce is None
+                and (self.ob_dim, self.ac_dim) in ((11, 3), (17, 6), (3, 1))):
+            return False
+        if getattr(self, "_sgd_max_bs", None) is None:
+            self._sgd_max_bs = int(load().sppAcmSgdMaxBatch(self._h))
+        return bs <= self._sgd_max_bs
 
     def _acm_sgd(self, idx, nsteps, bs):
         """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd)."""
@@ -602,12 +607,35 @@ class OffPolicyLoop:
         call("sppAcmSgd", self._h, ptr(x), ptr(y), nsteps, bs, ptr(self._acm_loss_acc), st)
         self._keep_sgd = (idx, x, y)
 
+    def _acm_sgd_check(self):
+        """Raise if a multi-workgroup sppAcmSgd launch timed out at its arrival barrier (its AcM
+        weights are then invalid).  The flag is copied stream-ordered into pinned memory after each
+        update_acm and read at the next one (or by check_acm_sgd(sync=True)), so no call blocks."""
+        ev = getattr(self, "_sgd_flag_ev", None)
+        if ev is not None:
+            ev.synchronize()
+            if int(self._sgd_flag[0]):
+                raise SppError("sppAcmSgd: a multi-workgroup step timed out at its arrival barrier; the AcM "
+                               "parameters are invalid")
+        if getattr(self, "_sgd_flag", None) is None:
+            self._sgd_flag = torch.zeros(1, dtype=torch.int32).pin_memory()
+        call("sppAcmSgdStatusAsync", self._h, self._sgd_flag.data_ptr(), stream_handle())
+        self._sgd_flag_ev = torch.cuda.Event()
+        self._sgd_flag_ev.record()
+
+    def check_acm_sgd(self):
+        """Synchronous form of the timeout check (tests, end of training)."""
+        self._acm_sgd_check()
+        self._acm_sgd_check()
+
     def update_acm_batches(self, n_batches):
         """acm.py:356-372: n batches of acm_batch_size uniform samples; loss = batch mean."""
         n = len(self.replay_buffer)
         self._acm_loss_acc.zero_()
         if self._acm_sgd_ok(self.acm_batch_size):
             self._acm_sgd(self._rand_idx(n_batches * self.acm_batch_size, n), n_batches, self.acm_batch_size)
+            if self.acm_batch_size > 64:
+                self._acm_sgd_check()
         else:
             for _ in range(n_batches):
                 self._acm_step_from_idx(self._rand_idx(self.acm_batch_size, n))
@@ -648,6 +676,8 @@ class OffPolicyLoop:
                     self._acm_loss_acc += self._acm_loss
             self._acm_loss_acc /= max(nb, 1)
             self._acm_sched_epochs += 1
+        if self.acm_batch_size > 64 and self._acm_sgd_ok(self.acm_batch_size):  # a multi-workgroup launch ran
+            self._acm_sgd_check()
         self._set_acm_lr(self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step))
 
     # ---------------------------------------------------------- pre-train (acm.py:234-244)

@@ -546,6 +546,71 @@ def gen_onpolicy(seed=51):
     save("onpolicy_hcheetah.npz", **out)
 
 
+def gen_ppo_epochs(seed=71, lr=3e-3, ent=0.05, N=300):
+    """PPO_AcM.update_actor_acm over several epochs with the KL early stop (acm/on_policy.py:164-216): one
+    full-batch minibatch per epoch (so the DataLoader's shuffle only reorders a mean), and a
+    kl_div_threshold placed between the KLs of the 3rd and 4th epochs, read from utils.kl_divergence in a
+    first run without the stop: epochs 0..3 run, the check at i = 4 breaks the loop, the losses are divided
+    by i + 1 = 5 (one more than the epochs run) and kl_div_updates_counter grows by 5."""
+    from rltoolkit import utils
+    from rltoolkit.acm import on_policy as onp_mod
+
+    ob = 17
+    rng = np.random.RandomState(seed)
+    obs, nobs, rew, done = onp_batch(rng, N, ob)
+    acts = rng.uniform(-1.1, 1.1, (N, ob)).astype(np.float32)
+    adv_in = (rng.randn(N) * 2 + 0.5).astype(np.float32)
+    noise = (0.2 * rng.randn(N)).astype(np.float32)
+
+    def run(thr, max_epochs):
+        torch.manual_seed(seed + 2)
+        ppo = PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=lr, critic_lr=3e-4, custom_loss=0.1,
+                      norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True, ppo_batch_size=N,
+                      max_ppo_epochs=max_epochs, entropy_coef=ent, kl_div_threshold=thr, acm_pre_train_samples=10,
+                      use_gpu=False)
+        load(ppo.actor, seed * 100 + 2)
+        p0 = flat_params(ppo.actor)
+        with torch.no_grad():
+            lp_cur = ppo.actor.get_actions_dist(torch.from_numpy(obs)).log_prob(torch.from_numpy(acts)).numpy()
+        lp_old = (lp_cur + noise).astype(np.float32)
+        mem = MemoryAcM(min_max_denormalize=True)
+        prev = mem.add_obs(torch.from_numpy(obs[:1]))
+        for i in range(N):
+            if i:
+                mem.new_rollout()
+                prev = mem.add_obs(torch.from_numpy(obs[i:i + 1]))
+            nxt = mem.add_obs(torch.from_numpy(nobs[i:i + 1]))
+            mem.add_timestep(prev, nxt, torch.from_numpy(acts[i:i + 1]), torch.from_numpy(lp_old[i:i + 1]),
+                             float(rew[i]), bool(done[i]), True)
+        mem.end_rollout()
+        kls = []
+        real = utils.kl_divergence
+
+        def rec(log_p, log_q):
+            v = real(log_p, log_q)
+            kls.append(v)
+            return v
+
+        onp_mod.utils.kl_divergence = rec
+        try:
+            ppo.update_actor_acm(torch.from_numpy(adv_in), mem)
+        finally:
+            onp_mod.utils.kl_divergence = real
+        return ppo, kls, p0, lp_old
+
+    _, kls, _, _ = run(1e9, 6)
+    assert max(kls[:3]) + 2e-3 < kls[3], kls  # a crossing with margin on both sides
+    thr = 0.5 * (max(kls[:3]) + kls[3])
+    ppo, kls2, p0, lp_old = run(thr, 10)
+    assert len(kls2) == 4 and ppo.kl_div_updates_counter == 5, (kls2, ppo.kl_div_updates_counter)
+    print("ppo epochs: kl per epoch", [round(k, 5) for k in kls], "threshold", round(thr, 5))
+    save("ppo_epochs_hcheetah.npz", params0=p0, obs=obs, nobs=nobs, acts=acts, lp_old=lp_old, adv=adv_in,
+         post=flat_params(ppo.actor), losses=np.array([ppo.loss[k] for k in ("actor", "entropy", "policy", "dist")]),
+         kls=np.array(kls2), counter=np.array(ppo.kl_div_updates_counter), threshold=np.array(thr),
+         lr=np.array(lr), eps=np.array(ppo.ppo_epsilon), entropy_coef=np.array(ent), custom_loss=np.array(0.1),
+         max_epochs=np.array(10))
+
+
 # ---------------------------------------------------------------- normalizer KATs + reference checkpoint
 def gen_interop(seed=61):
     """(1) MemoryMeta.normalize / denormalize (memory.py:76-127) and utils.standardize_and_clip /
@@ -621,7 +686,7 @@ def gen_interop(seed=61):
 
 
 GROUPS = {"interop": gen_interop, "randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
-          "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy}
+          "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy, "ppo_epochs": gen_ppo_epochs}
 
 if __name__ == "__main__":
     which = sys.argv[1:] or list(GROUPS) + ["sac"]

@@ -83,3 +83,15 @@ def test_product_never_imports_the_oracle():
                 txt = open(os.path.join(root, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", txt, re.M), f
                 assert "oracle/" not in txt.replace("oracle/_ref", ""), f
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    """bench.py under a launcher whose WORLD_SIZE differs from --gpus exits 2 before touching a GPU."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "WORLD_SIZE=2" in out.stderr

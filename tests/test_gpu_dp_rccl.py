@@ -43,3 +43,24 @@ def test_rccl_one_rank_exchange_matches_single_gpu(config):
     assert set(dp["losses"]) == set(plain["losses"])
     for k, v in plain["losses"].items():
         assert dp["losses"][k] == pytest.approx(v, rel=1e-5, abs=2e-5), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["sac_hopper", "ppo_hcheetah"])
+def test_bench_gpus_two_launches_two_ranks(config):
+    """``bench.py --gpus 2`` with no external launcher starts one rank per GPU itself (torch.distributed.run
+    as a child process) and relays rank 0's JSON line.  Rehearsed on one GPU with the gloo backend (both
+    ranks share cuda:0): two ranks really run (n_gpus 2) and the data-parallel replicas stay bit-identical."""
+    args = ["bench.py", "--config", config, "--gpus", "2", "--steps", "2", "--warmup", "1", "--envs", "512",
+            "--no-cpu-baseline", "--no-pmc", "--no-rocprof"] + (["--buffer", "100000"] if config != "ppo_hcheetah"
+                                                                 else [])
+    env = dict(os.environ, SPP_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable] + args, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
+    if config != "ppo_hcheetah":
+        assert r["replicas_identical"] is True

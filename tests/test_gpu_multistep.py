@@ -10,8 +10,9 @@ each of 3 consecutive updates (sac_acm.py:89-162, fresh batch and eps every step
   - the post-step parameters of every network compared with the float64 oracle run on the same
     batches (oracle/sac_acm.py): fp32 |d| <= 2 lr per step with < 0.2 % of weights beyond 1e-5 after
     step 1 (Adam's first step moves each weight by ~lr sign(g): a gradient sign flip at the fp32
-    rounding level moves it by up to 2 lr); bf16 MLP (bf16 gradients, 8-bit mantissa) |d| <= 2 lr
-    per step and mean |d| <= 0.25 lr per step;
+    rounding level moves it by up to 2 lr); bf16 MLP (bf16 gradients, 8-bit mantissa) at B = 4,096 and
+    at the bench batch 409,600: |d| <= 2 lr per step, mean |d| <= 0.05 lr per step and at most 1 % of
+    the weights per step beyond lr (a sign flip; a wrong path flips about half of them);
   - losses: fp32 rtol 1e-4, bf16 rtol 3e-2.
 """
 import numpy as np
@@ -58,6 +59,7 @@ def check_images(ag, bf16, before):
 
 
 @pytest.mark.parametrize("env_name,ob,ac,B,bf16", [("Ant-v2", 111, 8, 4096, True),
+                                                   ("Ant-v2", 111, 8, 409600, True),  # the sac_ant_bf16 bench batch
                                                    ("Hopper-v2", 11, 3, 65536, False)])
 def test_three_updates_images_and_params_match_oracle(env_name, ob, ac, B, bf16):
     lr, steps = 1e-3, 3
@@ -85,12 +87,15 @@ def test_three_updates_images_and_params_match_oracle(env_name, ob, ac, B, bf16)
         for k in ("actor", "critic_1", "critic_2", "critic_1_targ", "critic_2_targ"):
             got = ag.params[SAC_NETS[k]].cpu().numpy().astype(np.float64)
             d = np.abs(got - o.flat(k).astype(np.float64))
-            stats[k] = (d.max() / lr, d.mean() / lr, float(np.mean(d > 1e-5)))
+            stats[k] = (d.max() / lr, d.mean() / lr, float(np.mean(d > 1e-5)), float(np.mean(d > lr)))
             assert d.max() <= 2 * lr * step * 1.01, (step, k, d.max())
             if bf16:
-                assert d.mean() <= 0.25 * lr * step, (step, k, d.mean())
+                # |d| <= 2 lr per step is saturated by any one sign flip; these two can fail: a wrong operand
+                # or gradient moves ~half the weights by 2 lr (mean ~lr, fraction beyond lr ~0.5)
+                assert d.mean() <= 0.05 * lr * step, (step, k, d.mean())
+                assert np.mean(d > lr) <= 0.01 * step, (step, k, np.mean(d > lr))
             elif step == 1:
                 assert np.mean(d > 1e-5) < 2e-3, (k, np.mean(d > 1e-5))
-        print("step %d: %d images exact; |d|/lr max, mean, frac>1e-5:" % (step, nimg),
+        print("step %d: %d images exact; |d|/lr max, mean, frac>1e-5, frac>lr:" % (step, nimg),
               {k: tuple(round(x, 4) for x in v) for k, v in stats.items()})
         assert ag.current_alpha() == pytest.approx(o.alpha, rel=1e-4 if not bf16 else 1e-2)

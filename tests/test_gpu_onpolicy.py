@@ -54,6 +54,36 @@ def test_value_and_critic_grad(nets, N):
     assert relerr(nets.grads[1].cpu().numpy(), g_ref) < 2e-5
 
 
+def test_critic_full_batch_at_bench_size():
+    """The ppo_hcheetah bench's critic full batch (A2C.update_critic on all N = T x E = 16 x 2048 = 32,768
+    frames of an iteration, a2c.py:186-225): value and one gradient against the float64 oracle --
+    loss rtol 1e-5, gradient relative error < 2e-5 (multi-workgroup partials and the dW reduction at the
+    timed shape)."""
+    from spprl import _lib
+    from spprl.onpolicy import OnPolicyNets
+
+    N = 32768
+    n = OnPolicyNets(OB, AOUT, ac_lim=1.0, max_batch=N, device=DEV)
+    a, c = _setup(n, 13)
+    rng = np.random.RandomState(N)
+    x = (rng.randn(N, OB) * 1.5).astype(np.float32)
+    q = rng.randn(N).astype(np.float32)
+    v = n.value(x).cpu().numpy()
+    with torch.no_grad():
+        want = oo.critic(oo._params(c, oo.critic_layout(OB), torch.float64),
+                         torch.from_numpy(x).double()).squeeze(-1).numpy()
+    np.testing.assert_allclose(v, want, rtol=1e-5, atol=1e-5)
+    xd, qd = torch.from_numpy(x).to(DEV), torch.from_numpy(q).to(DEV)
+    loss = torch.zeros(1, device=DEV)
+    _lib.call("sppOnpCriticGrads", n._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), _lib.stream_handle())
+    torch.cuda.synchronize()
+    l_ref, g_ref = oo.critic_step(c, OB, x, q, dtype=torch.float64)
+    assert loss.item() == pytest.approx(l_ref, rel=1e-5)
+    e = relerr(n.grads[1].cpu().numpy(), g_ref)
+    print("N = %d: critic grad rel err %.2e" % (N, e))
+    assert e < 2e-5, e
+
+
 @pytest.mark.parametrize("N", [1, 500, 2048])
 def test_actor_grad_clip_entropy(nets, N):
     a, c = _setup(nets, 5)
@@ -173,8 +203,8 @@ def test_ppo_acm_actor_epoch_matches_reference_fixture():
     obs, nobs = fx["crit_obs"], fx["crit_nobs"]
     N, ob = obs.shape
     n = OnPolicyNets(ob, ob, actor_lr=float(fx["ppo_lr"]), ppo_epsilon=float(fx["ppo_eps"]),
-                     entropy_coef=float(fx["ppo_entropy_coef"]), max_ppo_epochs=1, ppo_batch_size=N,
-                     normalize_adv=True, max_batch=512, device=DEV)
+                     entropy_coef=float(fx["ppo_entropy_coef"]), custom_loss=float(fx["ppo_custom_loss"]),
+                     max_ppo_epochs=1, ppo_batch_size=N, normalize_adv=True, max_batch=512, device=DEV)
     n.load_net(0, fx["ppo_params0"])
     n.update_actor(fx["ppo_adv"], obs, fx["ppo_acts"], fx["ppo_lp_old"], nobs,
                    generator=torch.Generator().manual_seed(0))
@@ -182,7 +212,47 @@ def test_ppo_acm_actor_epoch_matches_reference_fixture():
     actor, entropy, policy, dist = (float(v) for v in fx["ppo_losses"])
     assert n.loss["actor"] == pytest.approx(actor, rel=1e-4, abs=1e-6)
     assert n.loss["entropy"] == pytest.approx(entropy, rel=1e-5)
+    assert n.loss["policy"] == pytest.approx(policy, rel=1e-4, abs=1e-6)
+    assert n.loss["dist"] == pytest.approx(dist, rel=1e-5)
+    assert n.kl_div_updates_counter == 1
     d = np.abs(n.params[0].cpu().numpy() - fx["ppo_post"])
     lr = float(fx["ppo_lr"])
     assert d.max() <= 2 * lr * 1.01, d.max()
     assert np.mean(d > 1e-6) < 2e-3, np.mean(d > 1e-6)
+
+
+def test_ppo_acm_actor_epochs_kl_stop_match_reference_fixture():
+    """PPO_AcM.update_actor_acm over several epochs with the KL early stop (acm/on_policy.py:164-216,
+    tests/golden/ppo_epochs_hcheetah.npz, make_golden.py gen_ppo_epochs): one full-batch minibatch per
+    epoch; the reference's KL of each epoch is taken on the last minibatch's pre-step log-probs, the
+    threshold sits between the 3rd and 4th epochs' KL, so 4 epochs run, the loop breaks at i = 4 and
+    every loss is divided by i + 1 = 5; kl_div_updates_counter += 5.  Four sequential Adam steps at
+    lr 3e-3: each weight within 2 lr per step of the reference (a sign flip of a near-zero gradient
+    coordinate moves it by 2 lr), most far closer."""
+    from golden_cases import load
+    from spprl.onpolicy import OnPolicyNets
+
+    fx = load("ppo_epochs_hcheetah")
+    obs, nobs = fx["obs"], fx["nobs"]
+    N, ob = obs.shape
+    lr = float(fx["lr"])
+    n = OnPolicyNets(ob, ob, actor_lr=lr, ppo_epsilon=float(fx["eps"]), entropy_coef=float(fx["entropy_coef"]),
+                     custom_loss=float(fx["custom_loss"]), max_ppo_epochs=int(fx["max_epochs"]), ppo_batch_size=N,
+                     kl_div_threshold=float(fx["threshold"]), normalize_adv=True, max_batch=512, device=DEV)
+    n.load_net(0, fx["params0"])
+    kl = n.update_actor(fx["adv"], obs, fx["acts"], fx["lp_old"], nobs, generator=torch.Generator().manual_seed(0))
+    torch.cuda.synchronize()
+    kls = fx["kls"]
+    assert n.last_epochs == len(kls) == 4
+    assert n.kl_div_updates_counter == int(fx["counter"]) == 5
+    assert kl == pytest.approx(float(kls[-1]), rel=1e-4, abs=2e-5)
+    actor, entropy, policy, dist = (float(v) for v in fx["losses"])
+    assert n.loss["actor"] == pytest.approx(actor, rel=1e-4, abs=2e-6)
+    assert n.loss["entropy"] == pytest.approx(entropy, rel=1e-5)
+    assert n.loss["policy"] == pytest.approx(policy, rel=1e-4, abs=2e-6)
+    assert n.loss["dist"] == pytest.approx(dist, rel=1e-5)
+    d = np.abs(n.params[0].cpu().numpy() - fx["post"])
+    print("epochs %d counter %d kl %.6f (ref %.6f); |d|/lr max %.4f mean %.5f frac>1e-5 %.4f" % (
+        n.last_epochs, n.kl_div_updates_counter, kl, kls[-1], d.max() / lr, d.mean() / lr, np.mean(d > 1e-5)))
+    assert d.max() <= 2 * lr * 4 * 1.01, d.max()
+    assert d.mean() <= 0.02 * lr, d.mean()

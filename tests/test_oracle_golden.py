@@ -267,3 +267,25 @@ def test_onpolicy_ppo_acm_actor_step_matches_reference():
     OracleAdam([flat], float(fx["ppo_lr"])).step([torch.from_numpy(g)])
     d = np.abs(flat.numpy() - fx["ppo_post"])
     assert d.max() < 1e-6, d.max()
+
+
+def test_onpolicy_ppo_acm_actor_epochs_with_kl_stop_match_reference():
+    """oracle.onpolicy.update_actor_epochs against the reference's multi-epoch update_actor_acm with the KL
+    stop (tests/golden/ppo_epochs_hcheetah.npz): 4 epochs run, losses / 5, counter + 5, the per-epoch KLs."""
+    from golden_cases import load, normalize_adv_ref
+    from oracle import onpolicy as oo
+
+    fx = load("ppo_epochs_hcheetah")
+    ob = fx["obs"].shape[1]
+    flat, losses, kls, cnt = oo.update_actor_epochs(
+        fx["params0"], ob, ob, np.ones(ob, np.float32), fx["obs"], fx["acts"], fx["lp_old"],
+        normalize_adv_ref(fx["adv"]), fx["nobs"], float(fx["lr"]), int(fx["max_epochs"]), float(fx["threshold"]),
+        len(fx["obs"]), eps_clip=float(fx["eps"]), entropy_coef=float(fx["entropy_coef"]),
+        custom_loss=float(fx["custom_loss"]))
+    assert cnt == int(fx["counter"]) == 5 and len(kls) == 4
+    np.testing.assert_allclose(kls, fx["kls"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose([losses[k] for k in ("actor", "entropy", "policy", "dist")], fx["losses"], rtol=1e-5,
+                               atol=1e-6)
+    d = np.abs(flat - fx["post"])
+    lr = float(fx["lr"])
+    assert d.max() <= 2 * lr * 4 * 1.01 and d.mean() < 0.01 * lr, (d.max(), d.mean())

@@ -105,6 +105,8 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic null)")
     ap.add_argument("--no-rocprof", action="store_true",
                     help="skip the rocprofv3 --kernel-trace child run (roofline.frac_rocprof null)")
+    ap.add_argument("--trace-dir", default=os.path.join(REPO, "gpurun_out"),
+                    help="where the rocprof child run's steady-state kernel summary is written")
     ap.add_argument("--dp-comm", choices=["native", "torch"], default="native",
                     help="N > 1 exchange: libspprl's own RCCL communicator on the compute stream (gradient buckets, "
                          "obs-statistics collectives) or torch.distributed's (its own stream + event waits)")
@@ -253,7 +255,7 @@ def lib_digest():
     return h.hexdigest()[:12]
 
 
-def pmc_traffic(args, E, cap, kernels):
+def pmc_traffic(args, E, cap, kernels, steps=2):
     """HBM bytes per launch of ``kernels`` (name prefixes) from two rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE; counters cannot share a pass) over a short child run of this
     script at the same config / E / buffer.  FETCH_SIZE is doubled: gfx950 counts half the
@@ -266,8 +268,9 @@ def pmc_traffic(args, E, cap, kernels):
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="spp_pmc_", dir="/tmp")
         cmd = ["timeout", "-s", "KILL", "240", rp, "--pmc", c, "-d", d, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "--config", args.config, "--envs", str(E), "--buffer",
-               str(cap), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
+               sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", str(steps), "--warmup",
+               "1", "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
+        cmd += (["--envs", str(E)] if E is not None else []) + (["--buffer", str(cap)] if cap is not None else [])
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             return None, "rocprofv3 --pmc %s exit %d: %s" % (c, r.returncode, r.stdout[-300:])
@@ -290,14 +293,17 @@ def pmc_traffic(args, E, cap, kernels):
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             out[k] = int(2 * d["FETCH_SIZE"] + d["WRITE_SIZE"])
     return out, "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py --config %s " \
-                "--envs %d --steps 2 --warmup 1, same library (sha1 %s); bytes = 2*FETCH + WRITE per launch" % (
-                    args.config, E, lib_digest())
+                "--envs %s --steps %d --warmup 1, same library (sha1 %s); bytes = 2*FETCH + WRITE per launch" % (
+                    args.config, E, steps, lib_digest())
 
 
-def rocprof_kernel_ms(args, E, cap, kname, steps=40, warmup=5):
+def rocprof_kernel_ms(args, E, cap, kname, steps=40, warmup=5, timed_launches=None):
     """Average duration (ms) of ``kname`` over the timed launches of a child run of this script under
     ``rocprofv3 --kernel-trace`` (same config, E, buffer and library): the kernel-trace view of the
-    roofline's launch time, next to the HIP-event average measured in the main run."""
+    roofline's launch time, next to the HIP-event average measured in the main run.  The steady-state
+    window (from the first timed launch of ``kname``: its last ``timed_launches`` (default steps) launches) is
+    summarised per kernel into ``<trace dir>/steady_kernel_stats_<config>.csv`` (Name, Calls, TotalDurationNs,
+    AverageNs), the file the roofline's ``frac_rocprof`` recomputes from (warm-up launches excluded)."""
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not found"
@@ -307,24 +313,45 @@ def rocprof_kernel_ms(args, E, cap, kname, steps=40, warmup=5):
     env = dict(os.environ, TMPDIR="/tmp")
     d = tempfile.mkdtemp(prefix="spp_kt_", dir="/tmp")
     cmd = ["timeout", "-s", "KILL", "300", rp, "--kernel-trace", "-d", d, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.abspath(__file__), "--config", args.config, "--envs", str(E), "--buffer", str(cap),
-           "--steps", str(steps), "--warmup", str(warmup), "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
+           sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", str(steps), "--warmup",
+           str(warmup), "--no-cpu-baseline", "--no-pmc", "--no-rocprof"]
+    if E is not None:
+        cmd += ["--envs", str(E)]
+    if cap is not None:
+        cmd += ["--buffer", str(cap)]
     r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         return None, "rocprofv3 --kernel-trace exit %d: %s" % (r.returncode, r.stdout[-300:])
     files = glob.glob(os.path.join(d, "**", "run_kernel_trace.csv"), recursive=True)
     if not files:
         return None, "no kernel trace csv"
-    rows = [row for row in csv.DictReader(open(files[0])) if kname in row["Kernel_Name"]]
+    rows = list(csv.DictReader(open(files[0])))
     shutil.rmtree(d, ignore_errors=True)
-    rows.sort(key=lambda row: int(row["Start_Timestamp"]))
-    dur = [(int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6 for row in rows]
-    timed = dur[-steps:] if len(dur) >= steps else dur
+    iv = sorted((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row["Kernel_Name"]) for row in rows)
+    mine = [x for x in iv if kname in x[2]]
+    nt = timed_launches or steps
+    timed = mine[-nt:] if len(mine) >= nt else mine
     if not timed:
         return None, "kernel %s not in the trace" % kname
-    return sum(timed) / len(timed), ("rocprofv3 --kernel-trace over bench.py --config %s --envs %d --steps %d "
-                                     "--warmup %d (library sha1 %s): mean of the last %d of %d launches" % (
-                                         args.config, E, steps, warmup, lib_digest(), len(timed), len(dur)))
+    t0 = timed[0][0]
+    per = {}
+    for s0, e0, n in iv:
+        if s0 >= t0:
+            c = per.setdefault(n, [0, 0])
+            c[0] += 1
+            c[1] += e0 - s0
+    out_dir = args.trace_dir
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "steady_kernel_stats_%s.csv" % args.config)
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs"])
+        for n, (c, tot) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+            w.writerow([n, c, tot, "%.1f" % (tot / c)])
+    ms = sum(e0 - s0 for s0, e0, _ in timed) / len(timed) * 1e-6
+    return ms, ("rocprofv3 --kernel-trace over bench.py --config %s --steps %d --warmup %d (library sha1 %s): mean "
+                "of the last %d of %d launches; steady-state per-kernel summary %s" % (
+                    args.config, steps, warmup, lib_digest(), len(timed), len(mine), os.path.relpath(path, REPO)))
 
 
 # ------------------------------------------------------------------ HBM-bound kernels
@@ -440,6 +467,7 @@ def bench_ppo(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     epochs["ppo"], epochs["acm_updates"] = 0, 0
+    ag.acm.sgd_events = []  # HIP events around every ACM epoch launch (the dominant kernel), torch's stream
     t0 = time.perf_counter()
     for _ in range(args.steps):
         iteration()
@@ -485,6 +513,36 @@ def bench_ppo(args, world, rank, dev):
                                 "~64 sequential 512-sample actor steps per epoch bound the iteration by latency"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
+    # the dominant kernel: the ACM epoch (k_mlp_sgd<2 ob, 32, ac, 0>, sequential 64 x s-row Adam steps over the
+    # ring), timed by HIP events around each launch on the stream it runs on
+    ev = ag.acm.sgd_events
+    ag.acm.sgd_events = None
+    if ev:
+        ms_l = [a.elapsed_time(b) for a, b, _ in ev]
+        rows = ev[0][2]
+        kflop = 2.0 * mac["acm_step"] * rows
+        k_ms = sum(ms_l) / len(ms_l)
+        kname = "k_mlp_sgd<%d, 32, %d, 0" % (2 * ob, ac)
+        res["roofline"] = {
+            "bound": "mfma", "kernel": "%s, true> (one ACM epoch: %d sequential Adam steps of %d rows, workgroups "
+                                      "%d)" % (kname, rows // acm_bs, acm_bs, -(-acm_bs // 64)),
+            "achieved": round(kflop / (k_ms * 1e-3) / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(kflop / (k_ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 5), "traffic": None,
+            "flop_per_launch": kflop, "algorithmic": "2 x 3 x %d MAC (AcM forward + both backward GEMMs) per row x %d "
+                                                     "rows per epoch" % (mac["M"], rows),
+            "avg_launch_ms": round(k_ms, 4), "launches": len(ms_l), "us_per_sgd_step": round(k_ms * 1e3 / (rows // acm_bs), 2),
+            "whole_iteration": {"achieved": res["roofline"]["achieved"], "frac": res["roofline"]["frac"],
+                                "note": res["roofline"]["note"]}}
+        if rank == 0 and world == 1 and not args.no_rocprof:
+            kt_ms, kt_src = rocprof_kernel_ms(args, args.envs, None, kname, steps=6, warmup=3, timed_launches=10)
+            rl = res["roofline"]
+            rl["avg_launch_ms_rocprof"] = round(kt_ms, 4) if kt_ms else None
+            rl["frac_rocprof"] = round(kflop / (kt_ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 5) if kt_ms else None
+            rl["rocprof_source"] = kt_src
+        if rank == 0 and world == 1 and not args.no_pmc:
+            traffic, src = pmc_traffic(args, args.envs, None, [kname], steps=3)
+            res["roofline"]["traffic"] = traffic.get(kname) if traffic else None
+            res["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = ppo_cpu_baseline_report(args.cpu_procs or default_cpu_procs())
     if rank == 0:

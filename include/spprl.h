@@ -423,6 +423,22 @@ sppStatus sppOnpCriticApply(sppOnPolicyHandle h, void* stream);
 sppStatus sppOnpActorGrads(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
                            const float* adv, const float* next_obs, int N, float* out4, void* stream);
 sppStatus sppOnpActorApply(sppOnPolicyHandle h, void* stream);
+/* PPO_AcM.update_actor_acm / PPO.update_actor minibatch epoch (rltoolkit/acm/on_policy.py:176-207,
+ * algorithms/ppo/ppo.py:174-190) in ONE launch: nsteps sequential Adam steps of the Gaussian actor on the
+ * clip loss - entropy_coef * entropy; step k's minibatch = rows idx[k*bs .. k*bs + bs) (the epoch's
+ * permutation, DataLoader(shuffle=True)) of x [n][ob] (normalised obs), act [n][aout], lp_old [n], adv [n]
+ * (normalised advantages) and next_obs [n][aout] (the dist loss, data only; NULL: 0).  out4 [nsteps][4]:
+ * each step's actor loss, KL (mean lp_old - lp_new before the step), dist MSE, entropy.  Parameters stay in
+ * LDS for the launch; bs > 64 spreads each step over ceil(bs / 64) co-resident workgroups whose gradients
+ * are summed in a fixed order (deterministic).  Single-process only (data-parallel ranks all-reduce every
+ * minibatch gradient: sppOnpActorGrads / Apply).  Instantiated for (ob, aout) = (17, 17), (11, 11). */
+sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
+                           const float* adv, const float* next_obs, const int64_t* idx, int nsteps, int bs,
+                           float* out4, void* stream);
+/* Largest bs sppOnpActorEpoch accepts on this device (0: no instantiation for the handle's dims). */
+int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);
+/* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch launch timed out at an arrival barrier, else 0. */
+sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
 /* Actor.act (basic_model.py:32-51) continuous: a = mu + exp(log_scale) * eps (eps NULL:
  * deterministic mu), logp = Independent(Normal).log_prob(a). */
 sppStatus sppOnpAct(sppOnPolicyHandle h, const float* x, int N, const float* eps, float* act_out, float* logp_out,

@@ -43,7 +43,7 @@
 #endif
 #include "onp.hip"
 #include "sgd.hip"
-#include "sgd_mf.hip"
+#include "sgd_mlp.hip"
 
 namespace spp {
 
@@ -886,10 +886,10 @@ struct sppAgent {
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
   float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
-  // multi-workgroup AcM SGD (sppAcmSgd with bs > kMfR): gradient slabs, {counter, timeout flag}
+  // multi-workgroup AcM SGD (sppAcmSgd with bs > kMlR): gradient slabs + parameter buffer, {counter, timeout flag}
   DevArray<float> sgd_slab;
   DevArray<int> sgd_sync;
-  int sgd_max_wg = -1;  // co-resident k_acm_sgd_mf workgroups (acm_sgd_max_wg, cached)
+  int sgd_max_wg = -1;  // co-resident k_mlp_sgd workgroups (acm_sgd_max_wg, cached)
   // per-kernel timing (HIP events on the launch stream)
   bool timing = false;
   std::vector<hipEvent_t> tev[5];
@@ -1908,22 +1908,41 @@ sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
   return SPP_OK;
 }
 
-// co-resident workgroups of the multi-workgroup k_acm_sgd_mf on this device (0: no instantiation)
+// co-resident workgroups of the multi-workgroup AcM k_mlp_sgd on this device (0: no instantiation)
+extern "C++" {
+template <int IN, int H2, int OUT, int HEAD>
+static int mlp_sgd_max_wg(int num_cu) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_mlp_sgd<IN, H2, OUT, HEAD, true>, kMlTH,
+                                                   0) != hipSuccess)
+    per_cu = 0;
+  return std::min(kMlMaxWG, per_cu * num_cu);
+}
+}
 static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
   if (a->sgd_max_wg >= 0) return a->sgd_max_wg;
-  const void* k = nullptr;
-  if (ob == 11 && ac == 3) k = (const void*)k_acm_sgd_mf<22, 3, true>;
-  else if (ob == 17 && ac == 6) k = (const void*)k_acm_sgd_mf<34, 6, true>;
-  else if (ob == 3 && ac == 1) k = (const void*)k_acm_sgd_mf<6, 1, true>;
-  int per_cu = 0;
-  if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kMfTH, 0) != hipSuccess) per_cu = 0;
-  a->sgd_max_wg = std::min(kMfMaxWG, per_cu * a->num_cu);
-  return a->sgd_max_wg;
+  int n = 0;
+  if (ob == 11 && ac == 3) n = mlp_sgd_max_wg<22, 32, 3, 0>(a->num_cu);
+  else if (ob == 17 && ac == 6) n = mlp_sgd_max_wg<34, 32, 6, 0>(a->num_cu);
+  else if (ob == 3 && ac == 1) n = mlp_sgd_max_wg<6, 32, 1, 0>(a->num_cu);
+  a->sgd_max_wg = n;
+  return n;
 }
 
 int sppAcmSgdMaxBatch(sppAgentHandle a) {
   if (!a || a->ddpg) return 0;
-  return kMfR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
+  return kMlR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
+}
+
+// slabs [2][kMlMaxWG][kMlSlabMax] + the parameter buffer + {arrival counter, timeout flag}
+static sppStatus mlp_sgd_buffers(DevArray<float>& slab, DevArray<int>& sync, hipStream_t st) {
+  if (!slab.ptr) {
+    SPP_CHECK_HIP(slab.alloc((size_t)(2 * kMlMaxWG + 1) * kMlSlabMax));
+    SPP_CHECK_HIP(sync.alloc(2));
+    SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, 2 * sizeof(int), st));
+  }
+  SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, sizeof(int), st));  // the arrival counter (the flag is sticky)
+  return SPP_OK;
 }
 
 sppStatus sppAcmSgdStatusAsync(sppAgentHandle a, int* timed_out_pinned, void* stream) {
@@ -1939,40 +1958,38 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
                     void* stream) {
   SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
-  SPP_REQUIRE(bs <= kMfR * kMfMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kMfR * kMfMaxWG);
+  SPP_REQUIRE(bs <= kMlR * kMlMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kMlR * kMlMaxWG);
   sppStatus s = check_ready(a);
   if (s) return s;
   if (nsteps == 0) return SPP_OK;
   const NetBufs& n = a->net[SPP_NET_ACM];
   SPP_REQUIRE(n.p && n.m && n.v, SPP_E_STATE, "acm_sgd: ACM buffers not bound");
-  AcmSgdArgs g{x, y, nsteps, bs, n.p, n.m, n.v, a->cfg.acm_lr, a->steps[3], a->limits.ptr + a->cfg.aout, loss_sum,
-               bs, nullptr, nullptr, nullptr};
+  MlpSgdArgs g{};
+  g.x = x; g.y = y; g.nsteps = nsteps; g.bs = bs; g.bsl = bs;
+  g.params = n.p; g.m = n.m; g.v = n.v; g.lr = a->cfg.acm_lr; g.step0 = a->steps[3];
+  g.lim = a->limits.ptr + a->cfg.aout; g.loss_sum = loss_sum;
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
-  // the MFMA form (sgd_mf.hip): 64 rows per workgroup, gradients summed over the workgroups
-  const int nwg = cdiv(bs, kMfR);
-  // the per-step arrival barrier needs every workgroup resident at once
+  // 64 rows per workgroup (sgd_mlp.hip); the per-step arrival barriers need every workgroup resident at once
+  const int nwg = cdiv(bs, kMlR);
   SPP_REQUIRE(nwg <= acm_sgd_max_wg(a, ob, ac), SPP_E_SHAPE, "acm_sgd: batch %d needs %d co-resident workgroups > %d",
               bs, nwg, acm_sgd_max_wg(a, ob, ac));
   if (nwg > 1) {
     g.bsl = cdiv(bs, nwg);
-    if (!a->sgd_slab.ptr) {
-      SPP_CHECK_HIP(a->sgd_slab.alloc((size_t)(2 * kMfMaxWG + 2) * kMfSlab));  // + the reduced slabs
-      SPP_CHECK_HIP(a->sgd_sync.alloc(2));  // {arrival counter, timeout flag}
-      SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, 2 * sizeof(int), st));
-    }
+    s = mlp_sgd_buffers(a->sgd_slab, a->sgd_sync, st);
+    if (s) return s;
     g.slab = a->sgd_slab.ptr;
+    g.pbuf = a->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
     g.ctr = a->sgd_sync.ptr;
     g.err = a->sgd_sync.ptr + 1;
-    SPP_CHECK_HIP(hipMemsetAsync(a->sgd_sync.ptr, 0, sizeof(int), st));
   }
   const bool mw = nwg > 1;
-#define SPP_SGD_LAUNCH(IN_, AC_, TH_)                                                              \
-  if (mw) hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, true>), dim3(nwg), dim3(kMfTH), 0, st, g);    \
-  else hipLaunchKernelGGL((k_acm_sgd_mf<IN_, AC_, false>), dim3(1), dim3(kMfTH), 0, st, g)
-  if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3, 256);
-  else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6, 512);
-  else if (ob == 3 && ac == 1) SPP_SGD_LAUNCH(6, 1, 512);
+#define SPP_SGD_LAUNCH(IN_, AC_)                                                                      \
+  if (mw) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true>), dim3(nwg), dim3(kMlTH), 0, st, g);   \
+  else hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, false>), dim3(1), dim3(kMlTH), 0, st, g)
+  if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3);
+  else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6);
+  else if (ob == 3 && ac == 1) SPP_SGD_LAUNCH(6, 1);
   else SPP_REQUIRE(false, SPP_E_SHAPE, "acm_sgd: no instantiation for ob=%d ac=%d", ob, ac);
 #undef SPP_SGD_LAUNCH
   a->steps[3] += nsteps;
@@ -2106,6 +2123,10 @@ struct sppOnPolicy {
   int Bpmax = 0, pstride = 0;
   DwSet dw[2];  // 0 critic, 1 actor
   DevArray<AdamJob> d_adam;
+  // persistent PPO actor epochs (sppOnpActorEpoch, sgd_mlp.hip HEAD 1): slabs + parameter buffer, {counter, flag}
+  DevArray<float> sgd_slab;
+  DevArray<int> sgd_sync;
+  int sgd_max_wg = -1;
 };
 
 static sppStatus onp_packs(sppOnPolicy* o) {
@@ -2282,6 +2303,7 @@ sppStatus sppOnpDestroy(sppOnPolicyHandle o) {
   hipSetDevice(o->device);
   hipDeviceSynchronize();
   o->lim.release(); o->pk.release(); o->d_pj.release(); o->scratch.release(); o->d_adam.release();
+  o->sgd_slab.release(); o->sgd_sync.release();
   for (auto& D : o->dw) D.release();
   delete o;
   return SPP_OK;
@@ -2373,6 +2395,67 @@ sppStatus sppOnpActorApply(sppOnPolicyHandle o, void* stream) {
   hipLaunchKernelGGL(k_adam, dim3(std::max(1, std::min(cdiv(o->net[0].n, 1024), 1024)), 1), dim3(256), 0, S(stream),
                      (const AdamJob*)o->d_adam.ptr, (float)(-(o->cfg.actor_lr / bc1)), (float)bc2s, 0.f);
   SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// co-resident workgroups of the multi-workgroup PPO actor epoch kernel (0: no instantiation for these dims)
+static int onp_epoch_max_wg(sppOnPolicy* o) {
+  if (o->sgd_max_wg >= 0) return o->sgd_max_wg;
+  const int ob = o->cfg.ob, aout = o->cfg.aout;
+  int n = 0;
+  if (ob == 17 && aout == 17) n = mlp_sgd_max_wg<17, 64, 17, 1>(o->num_cu);
+  else if (ob == 11 && aout == 11) n = mlp_sgd_max_wg<11, 64, 11, 1>(o->num_cu);
+  o->sgd_max_wg = n;
+  return n;
+}
+
+int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
+  if (!o) return 0;
+  const int n = onp_epoch_max_wg(o);
+  return n > 0 ? kMlR * n : 0;
+}
+
+sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old, const float* adv,
+                           const float* next_obs, const int64_t* idx, int nsteps, int bs, float* out4, void* stream) {
+  SPP_REQUIRE(o && x && act && lp_old && adv && idx && out4 && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG,
+              "actor epoch: bad args");
+  SPP_REQUIRE(o->net[0].p && o->net[0].m && o->net[0].v && o->lim.ptr, SPP_E_STATE, "actor epoch: actor not bound");
+  const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o);
+  SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "actor epoch: no instantiation for ob=%d aout=%d", o->cfg.ob, o->cfg.aout);
+  SPP_REQUIRE(nwg <= maxwg, SPP_E_SHAPE, "actor epoch: batch %d needs %d co-resident workgroups > %d", bs, nwg, maxwg);
+  if (nsteps == 0) return SPP_OK;
+  hipStream_t st = S(stream);
+  MlpSgdArgs g{};
+  g.x = x; g.y = act; g.nxt = next_obs ? next_obs : act; g.lp_old = lp_old; g.adv = adv; g.idx = idx;
+  g.nsteps = nsteps; g.bs = bs; g.bsl = bs;
+  const NetBufs& n = o->net[0];
+  g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.actor_lr; g.step0 = o->steps[0];
+  g.lim = o->lim.ptr; g.eps_clip = o->cfg.ppo_epsilon; g.ent_coef = o->cfg.entropy_coef; g.out = out4;
+  if (nwg > 1) {
+    g.bsl = cdiv(bs, nwg);
+    sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
+    if (s) return s;
+    g.slab = o->sgd_slab.ptr;
+    g.pbuf = o->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
+    g.ctr = o->sgd_sync.ptr;
+    g.err = o->sgd_sync.ptr + 1;
+  }
+  const bool mw = nwg > 1;
+#define SPP_EPOCH_LAUNCH(OB_)                                                                          \
+  if (mw) hipLaunchKernelGGL((k_mlp_sgd<OB_, 64, OB_, 1, true>), dim3(nwg), dim3(kMlTH), 0, st, g);     \
+  else hipLaunchKernelGGL((k_mlp_sgd<OB_, 64, OB_, 1, false>), dim3(1), dim3(kMlTH), 0, st, g)
+  if (o->cfg.ob == 17) SPP_EPOCH_LAUNCH(17);
+  else SPP_EPOCH_LAUNCH(11);
+#undef SPP_EPOCH_LAUNCH
+  o->steps[0] += nsteps;
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle o, int* timed_out) {
+  SPP_REQUIRE(o && timed_out, SPP_E_INVALID_ARG, "actor epoch status: null");
+  *timed_out = 0;
+  if (o->sgd_sync.ptr) SPP_CHECK_HIP(hipMemcpy(timed_out, o->sgd_sync.ptr + 1, sizeof(int), hipMemcpyDeviceToHost));
   return SPP_OK;
 }
 

@@ -65,15 +65,9 @@ __device__ __forceinline__ float sum_bf8(const float4& a) {
 }
 
 // ABF / XBF: the A / X operand rows are bf16 (BF only); row pointers are then __bf16* cast to float*.
-// Operand loads: each operand byte is read once per launch; SPP_DW_LD_NT selects nt loads.
-__device__ __forceinline__ float4 dw_ld(const float* p) {
-#ifdef SPP_DW_LD_NT
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p)));
-#else
-  return *reinterpret_cast<const float4*>(p);
-#endif
-}
+// Operand loads use the default cache policy: nt loads were measured slower (both lane
+// halves of a wave reuse each L1 line).
+__device__ __forceinline__ float4 dw_ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 template <int NI, int NJ, bool DB, bool BF = false, bool ABF = false, bool XBF = false>
 __device__ __forceinline__ void dw_tile(const float* const (&ap)[4], const float* const (&xp)[4], int nsteps,
@@ -253,37 +247,44 @@ __device__ __forceinline__ void dw_big_lds(const DwJob& J, int b_begin, int nste
 // (dW2 / db2).
 __device__ __forceinline__ void dw_store(const DwJob& J, int split, int part, int nb0, int kb0, int ni, int nj,
                                          bool db, const f32x16 (&acc)[4][4], const float (&bs)[4]) {
-  const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  // recomputed here, not carried over the tile loop: the prologue's per-row indices, kept live across the
+  // MFMA loop for these stores, were what spilled to scratch
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(nb0), "+v"(kb0), "+v"(ni), "+v"(nj), "+v"(split), "+v"(part), "+v"(tid));
+  const int lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int N = J.N, K = J.K0 + J.K1;
   const bool direct = J.nsplit * J.wsplit == 1;
   float* slab = direct ? nullptr : J.slab + (int64_t)(split * J.wsplit + part) * J.slab_stride;
-  auto out_w = [&](int n, int k, float v) {
-    if (!direct) slab[(int64_t)n * K + k] = v;
-    else if (n < J.nrow2) J.dW[(int64_t)n * K + k] = v;
-    else J.dW2[(int64_t)(n - J.nrow2) * K + k] = v;
-  };
-  auto out_b = [&](int n, float v) {
-    if (!direct) slab[(int64_t)N * K + n] = v;
-    else if (n < J.nrow2) J.db[n] = v;
-    else J.db2[n - J.nrow2] = v;
+  // row n's destination: one 64-bit row pointer live at a time (rows outer, the row's column blocks inner:
+  // precomputing every (row, column) address is what spilled this kernel's VGPRs)
+  auto row_w = [&](int n) -> float* {
+    if (!direct) return slab + (int64_t)n * K;
+    return n < J.nrow2 ? J.dW + (int64_t)n * K : J.dW2 + (int64_t)(n - J.nrow2) * K;
   };
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i >= ni) break;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j >= nj) break;
-      const int k = 32 * (kb0 + j) + c;
+    for (int q = 0; q < 16; ++q) {
+      const int n = 32 * (nb0 + i) + unit_of(q, h);
+      if (n >= N) continue;
+      float* rowp = row_w(n);
+      asm volatile("" : "+v"(rowp));  // keep the row pointer from being hoisted across the unrolled rows
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int n = 32 * (nb0 + i) + unit_of(q, h);
-        if (n < N && k < K) out_w(n, k, acc[i][j][q]);
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nj) break;
+        const int k = 32 * (kb0 + j) + c;
+        if (k < K) rowp[k] = acc[i][j][q];
       }
     }
     if (db) {
       const float tot = bs[i] + __shfl_xor(bs[i], 32, 64);
       const int n = 32 * (nb0 + i) + c;
-      if (h == 0 && n < N) out_b(n, tot);
+      if (h == 0 && n < N) {
+        if (!direct) slab[(int64_t)N * K + n] = tot;
+        else if (n < J.nrow2) J.db[n] = tot;
+        else J.db2[n - J.nrow2] = tot;
+      }
     }
   }
 }

@@ -385,20 +385,15 @@ __global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64
                                                               const uint32_t* __restrict__ state,
                                                               uint32_t* __restrict__ ghist) {
   extern __shared__ uint32_t shk[];  // [ob][4][1 << dbits]
+  // the ranks' (prefix, mask) per (column, rank) in LDS: 64 registers per thread held them before, which
+  // spilled at 1024 threads (128 VGPRs); one broadcast LDS read per (column, rank) and row batch now
+  __shared__ uint2 qpm[16 * kStatsColsPerThread * 4];
   const int ob = r.ob;
   const int bins = 1 << dbits;
   const int nb = ob * 4 * bins;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) shk[i] = 0;
+  for (int i = threadIdx.x; i < ob * 4; i += blockDim.x) qpm[i] = make_uint2(state[i * 3 + 0], state[i * 3 + 1]);
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4, nty = blockDim.x >> 4;
-  uint32_t pre[kStatsColsPerThread][4], msk[kStatsColsPerThread][4];
-#pragma unroll
-  for (int j = 0; j < kStatsColsPerThread; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tx + 16 * j;
-      pre[j][q] = c < ob ? state[(c * 4 + q) * 3 + 0] : 0u;
-      msk[j][q] = c < ob ? state[(c * 4 + q) * 3 + 1] : 0u;
-    }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * nty;
   for (int64_t i0 = (int64_t)blockIdx.x * nty + ty; i0 < len; i0 += stride * kStatsRows) {
@@ -416,12 +411,13 @@ __global__ __launch_bounds__(kStatsPkThreads) void k_stats_pk(ReplayDev r, int64
 #pragma unroll
       for (int k = 0; k < kStatsRows; ++k) kk[k] = base[k] >= 0 ? fkey(r.obs[base[k] + c]) : 0u;
 #pragma unroll
-      for (int k = 0; k < kStatsRows; ++k)
-        if (base[k] >= 0)
+      for (int q = 0; q < 4; ++q) {
+        const uint2 pm = qpm[c * 4 + q];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if ((kk[k] & msk[j][q]) == pre[j][q])
-              atomicAdd(&shk[(c * 4 + q) * bins + ((kk[k] >> shift) & (bins - 1))], 1u);
+        for (int k = 0; k < kStatsRows; ++k)
+          if (base[k] >= 0 && (kk[k] & pm.y) == pm.x)
+            atomicAdd(&shk[(c * 4 + q) * bins + ((kk[k] >> shift) & (bins - 1))], 1u);
+      }
     }
   }
   __syncthreads();

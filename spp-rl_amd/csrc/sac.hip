@@ -559,7 +559,11 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
-    const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
+    // d loss / d logpi_b; the product is formed per tile from the SGPR operands (hoisted, its VGPR stayed
+    // live across the whole tile loop and spilled to scratch in the widest instantiations)
+    float al = alpha;
+    asm volatile("" : "+s"(al));
+    const float g_lp = valid ? al * p.inv_B : 0.f;
     // ---- a, logpi = actor(s)  (sac_acm.py:137)
     uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
     SPP_TP(26);

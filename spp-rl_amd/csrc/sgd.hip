@@ -1,37 +1,11 @@
 // Shared pieces of the persistent AcM regression SGD (rltoolkit/basic_model.py:108-132, 64-32 tanh,
 // out = tanh(fc3) * ac_lim): AcMTrainer.update_acm's inner loop (acm/acm.py:266-303: shuffled
 // minibatches, MSE, Adam) or update_acm_batches (:356-372), many sequential steps in ONE launch.
-// The kernel itself is k_acm_sgd_mf (sgd_mf.hip: every layer on the fp32 matrix cores); this file holds
-// its arguments, the write-through gradient slabs and the bounded arrival barrier of the
-// multi-workgroup form.
+// The kernel itself is k_mlp_sgd (sgd_mlp.hip: every layer on the fp32 matrix cores); this file holds the
+// write-through slab accessors and the bounded arrival barrier of its multi-workgroup form.
 #include "common.h"
 
 namespace spp {
-
-#ifndef SPP_SGD_TWOLEVEL
-#define SPP_SGD_TWOLEVEL 4
-#endif
-constexpr int kSgdTwoLevel = SPP_SGD_TWOLEVEL;  // more workgroups than this: two-level gradient reduction per step
-
-struct AcmSgdArgs {
-  const float* x;      // [nsteps * bs][IN] acm_cat inputs, consumed in order (sppReplayGatherAcm)
-  const float* y;      // [nsteps * bs][AC] targets
-  int nsteps, bs;
-  float* params;       // canonical AcM flat buffer (state_dict order)
-  float* m;            // Adam exp_avg
-  float* v;            // Adam exp_avg_sq
-  float lr;
-  int64_t step0;       // Adam steps already taken
-  const float* lim;    // [ac]
-  float* loss_sum;     // += sum of the steps' batch losses (fp32 scalar)
-  // several workgroups per step (k_acm_sgd_mf<.., true>, bs > kMfR): workgroup g takes rows
-  // [g*bsl, min((g+1)*bsl, bs)) of every step's batch; per-step gradient hand-over through slab
-  // [2][gridDim.x][kMfSlab] (step parity) and the arrival counter ctr (zeroed per launch)
-  int bsl;
-  float* slab;
-  int* ctr;
-  int* err;            // set to 1 if a step's arrival wait timed out (results then invalid)
-};
 
 // Arrival barrier of the multi-workgroup SGD.  The counter address is kept in a VGPR so the add and the
 // polls are vector-memory operations.  Bounded: a wait that times out sets *err and every later wait of

@@ -506,6 +506,8 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
   if (tid == 0) {
     double s1 = 0.0, s2 = 0.0;
     int64_t out = 0, eql = 0, eqh = 0, nl = 0;
+    // rolled: unrolled, the 6 x 16 partials were all loaded up front and spilled to scratch
+#pragma unroll 1
     for (int q = 0; q < NW; ++q) {
       s1 += rd[0][q];
       s2 += rd[1][q];

@@ -150,6 +150,9 @@ _SIGS = {
     "sppAdvNormalizeGlobal": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, n, bs
     "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
+    "sppOnpActorEpoch": (c_int, [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p]),
+    "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),
+    "sppOnpActorEpochStatus": (c_int, [c_void_p, c_void_p]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppAcmSgdMaxBatch": (c_int, [c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),

@@ -162,6 +162,8 @@ class OnPolicyNets:
         kl, i = 0.0, 0
         sums = torch.zeros(4, device=self.device)
         self.last_epochs = 0
+        mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
+        one_launch = self._epoch_kernel_ok(mb)
         for i in range(self.max_ppo_epochs):
             if kl >= self.kl_div_threshold:
                 break
@@ -170,15 +172,25 @@ class OnPolicyNets:
             # device (a host randperm + pageable copy would stall the stream every epoch)
             perm = (torch.randperm(N, generator=generator).to(self.device) if generator is not None
                     else torch.randperm(N, device=self.device))
-            mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
-            # one permuted copy per epoch: every minibatch is then a contiguous slice
-            o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]
-            n_p = nxt[perm] if nxt is not None else None
             outs = torch.empty(-(-N // mb), 4, device=self.device)  # one row per minibatch step
-            for k, s in enumerate(range(0, N, mb)):
-                e = s + mb
-                self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None,
-                                out=outs[k])
+            if one_launch:  # the whole epoch in one persistent launch (full minibatches, then the ragged one)
+                full = N // mb
+                st = stream_handle()
+                if full:
+                    call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
+                         ptr(perm), full, mb, ptr(outs), st)
+                if N % mb:
+                    call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
+                         ptr(perm[full * mb:]), 1, N % mb, ptr(outs[full:]), st)
+                self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
+            else:
+                # one permuted copy per epoch: every minibatch is then a contiguous slice
+                o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]
+                n_p = nxt[perm] if nxt is not None else None
+                for k, s in enumerate(range(0, N, mb)):
+                    e = s + mb
+                    self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None,
+                                    out=outs[k])
             sums += outs.sum(0)
             kl = float(outs[-1, 1].item())  # KL of the epoch's last minibatch (ppo.py:188)
         # the reference divides by i + 1 after the loop: the epochs run when none stopped early, one more than
@@ -191,6 +203,22 @@ class OnPolicyNets:
             self.loss.update(dist=s[2] / d, policy=(s[0] - self.entropy_coef * s[3] + self.custom_loss * s[2]) / d)
         self.kl_div_updates_counter += i + 1
         return kl
+
+    def _epoch_kernel_ok(self, mb):
+        """The one-launch epoch (sppOnpActorEpoch) runs single-process epochs of these dims whose minibatch
+        workgroups are all co-resident; data-parallel ranks all-reduce each minibatch gradient instead."""
+        if self.allreduce is not None:
+            return False
+        if getattr(self, "_epoch_max_bs", None) is None:
+            self._epoch_max_bs = int(_lib.load().sppOnpActorEpochMaxBatch(self._h))
+        return mb <= self._epoch_max_bs
+
+    def check_actor_epochs(self):
+        """Raise if a multi-workgroup sppOnpActorEpoch launch timed out at an arrival barrier."""
+        flag = np.zeros(1, np.int32)
+        call("sppOnpActorEpochStatus", self._h, flag.ctypes.data_as(ctypes.c_void_p))
+        if flag[0]:
+            raise _lib.SppError("sppOnpActorEpoch: a step timed out at its arrival barrier; actor parameters invalid")
 
     def act(self, obs, eps=None):
         """Actor.act: (action, log_prob); eps None -> deterministic mean."""

@@ -604,7 +604,14 @@ class OffPolicyLoop:
         x = torch.empty(n, 2 * self.ob_dim, device=self.device)
         y = torch.empty(n, self.ac_dim, device=self.device)
         call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), n, ptr(x), ptr(y), st)
+        ev = getattr(self, "sgd_events", None)  # measurement: HIP events around each sppAcmSgd launch
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         call("sppAcmSgd", self._h, ptr(x), ptr(y), nsteps, bs, ptr(self._acm_loss_acc), st)
+        if ev is not None:
+            e1.record()
+            ev.append((e0, e1, nsteps * bs))
         self._keep_sgd = (idx, x, y)
 
     def _acm_sgd_check(self):

@@ -256,3 +256,54 @@ def test_ppo_acm_actor_epochs_kl_stop_match_reference_fixture():
         n.last_epochs, n.kl_div_updates_counter, kl, kls[-1], d.max() / lr, d.mean() / lr, np.mean(d > 1e-5)))
     assert d.max() <= 2 * lr * 4 * 1.01, d.max()
     assert d.mean() <= 0.02 * lr, d.mean()
+
+
+@pytest.mark.parametrize("N,mb", [(2048, 512), (2000, 512), (300, 64)])
+def test_actor_epoch_kernel_matches_per_step_path_and_oracle(N, mb):
+    """sppOnpActorEpoch (one launch per PPO epoch: every minibatch step's forward, clip-loss backward, weight
+    gradients, fixed-order sum over the ceil(mb / 64) workgroups and Adam inside the kernel) against (a) the
+    per-minibatch path (sppOnpActorGrads / Apply, six launches per step) and (b) the oracle's epoch loop
+    (oracle.onpolicy.update_actor_epochs, on_policy.py:176-216) on the same permutations: 2 epochs, a ragged
+    last minibatch for N = 2000.  Losses / KL rtol 1e-4; parameters within 2 lr per Adam step of the oracle
+    (a sign flip of a near-zero gradient coordinate), mean far below that."""
+    from spprl.onpolicy import OnPolicyNets
+
+    lr, ent, cl = 3e-4, 0.01, 0.1
+    rng = np.random.RandomState(N + mb)
+    a0 = oo.init_flat(oo.actor_layout(OB, AOUT), 21)
+    a0[:AOUT] += rng.uniform(-0.3, 0.3, AOUT).astype(np.float32)
+    x = (rng.randn(N, OB) * 1.2).astype(np.float32)
+    act = rng.uniform(-1.1, 1.1, (N, AOUT)).astype(np.float32)
+    nxt = rng.randn(N, AOUT).astype(np.float32)
+    with torch.no_grad():
+        lp_cur = oo.actor_dist(oo._params(a0, oo.actor_layout(OB, AOUT)), torch.from_numpy(x),
+                               torch.ones(AOUT)).log_prob(torch.from_numpy(act)).numpy()
+    lp_old = (lp_cur + 0.2 * rng.randn(N)).astype(np.float32)
+    adv = rng.randn(N).astype(np.float32)
+    adv = ((adv - adv.mean()) / adv.std()).astype(np.float32)  # already normalised (normalize_adv off)
+    res = []
+    for one_launch in (True, False):
+        n = OnPolicyNets(OB, AOUT, ac_lim=1.0, actor_lr=lr, entropy_coef=ent, custom_loss=cl, max_ppo_epochs=2,
+                         ppo_batch_size=mb, kl_div_threshold=1e9, normalize_adv=False, max_batch=max(N, 512),
+                         device=DEV)
+        n.load_net(0, a0)
+        if not one_launch:
+            n._epoch_max_bs = 0
+        assert n._epoch_kernel_ok(mb) == one_launch
+        kl = n.update_actor(adv, x, act, lp_old, nxt, generator=torch.Generator().manual_seed(7))
+        torch.cuda.synchronize()
+        if one_launch:
+            n.check_actor_epochs()
+        res.append((n.params[0].cpu().numpy().copy(), dict(n.loss), kl))
+    g = torch.Generator().manual_seed(7)
+    perms = [torch.randperm(N, generator=g).numpy() for _ in range(2)]
+    flat, losses, kls, cnt = oo.update_actor_epochs(a0, OB, AOUT, np.ones(AOUT, np.float32), x, act, lp_old, adv, nxt,
+                                                    lr, 2, 1e9, mb, entropy_coef=ent, custom_loss=cl, perms=perms)
+    nsteps = 2 * -(-N // mb)
+    for p, loss, kl in res:
+        for k in ("actor", "entropy", "policy", "dist"):
+            assert loss[k] == pytest.approx(losses[k], rel=1e-4, abs=1e-6), (k, loss[k], losses[k])
+        assert kl == pytest.approx(kls[-1], rel=1e-3, abs=2e-6)
+        d = np.abs(p - flat)
+        print("N %d mb %d: |d|/lr max %.4f mean %.6f" % (N, mb, d.max() / lr, d.mean() / lr))
+        assert d.max() <= 2 * lr * nsteps * 1.01 and d.mean() <= 0.01 * lr, (d.max(), d.mean())

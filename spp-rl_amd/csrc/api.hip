@@ -407,7 +407,8 @@ static sppStatus stats_alloc(sppReplayHandle h) {
     static bool attr = false;
     if (!attr) {  // > 64 KiB dynamic LDS for wide observations
       hipFuncSetAttribute((const void*)k_stats_p1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void*)k_stats_pk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      // (k_stats_pk: at most [32][4][256] or [128][4][64] counters = 128 KiB, beside its 4 KiB static table)
+      hipFuncSetAttribute((const void*)k_stats_pk, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
       attr = true;
     }
   }
@@ -422,23 +423,14 @@ static void stats_pass1(sppReplayHandle h, uint32_t* hist, const float* pivot, h
 
 // digit pass p (0-based) after the top byte, all columns: 8-bit digits at bits 16, 8, 0 when the
 // [ob][4][256] LDS histogram fits 128 KiB (ob <= 32), else 6-bit digits at bits 18, 12, 6, 0
-static int stats_dbits(sppReplayHandle h) {
-#ifdef SPP_STATS_DBITS6  // A/B build: 6-bit digits for every ob
-  return 6;
-#else
-  return h->d.ob <= 32 ? 8 : 6;
-#endif
-}
+static int stats_dbits(sppReplayHandle h) { return h->d.ob <= 32 ? 8 : 6; }
 static int stats_npass(sppReplayHandle h) { return 24 / stats_dbits(h); }
 static int stats_shift(sppReplayHandle h, int p) { return 24 - stats_dbits(h) * (p + 1); }
 
 static void stats_pk(sppReplayHandle h, int p, uint32_t* hist, hipStream_t st) {
   const size_t ldsk = sizeof(uint32_t) * h->d.ob * 4 * (1u << stats_dbits(h));
-#ifndef SPP_STATS_PK_PER_CU
-#define SPP_STATS_PK_PER_CU 1
-#endif
-  // 1024-thread blocks per CU (each flushes its LDS histogram with device atomics at the end)
-  const int resident = std::max(1, std::min(SPP_STATS_PK_PER_CU, (int)((160 * 1024) / ldsk)));
+  // one 1024-thread block per CU (each flushes its LDS histogram with device atomics at the end)
+  const int resident = 1;
   hipLaunchKernelGGL(k_stats_pk, dim3(h->num_cu * resident), dim3(kStatsPkThreads), ldsk, st, h->d, h->len,
                      stats_shift(h, p), stats_dbits(h), (const uint32_t*)h->st_state, hist);
 }
@@ -885,6 +877,8 @@ struct sppAgent {
   DwSet dws[2];
   DevArray<AdamJob> d_adam;  // [critic1, critic2 | actor | acm]
   int cur_B = -1;            // staged batch size
+  float* w3p[2] = {};         // SAC critics' fused fc3 gradient partials (slabs of the reduce-only dW jobs)
+  int64_t w3p_stride = 0;
   float* alpha_grad = nullptr;  // bound operand (defaults to internal scratch)
   // multi-workgroup AcM SGD (sppAcmSgd with bs > kMlR): gradient slabs + parameter buffer, {counter, timeout flag}
   DevArray<float> sgd_slab;
@@ -1104,10 +1098,11 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
   auto assign_splits = [&](int first, int count) {
     double big[2] = {0.0, 0.0};  // MACs of the large jobs per launch
     for (int i = first; i < first + count; ++i)
-      if (is_big(jobs[i]))
+      if (!jobs[i].fused && is_big(jobs[i]))
         big[lds_big(jobs[i]) ? 0 : 1] += (double)round_up(jobs[i].N, 32) * round_up(jobs[i].K0 + jobs[i].K1, 32);
     for (int i = first; i < first + count; ++i) {
       DwJob& j = jobs[i];
+      if (j.fused) continue;  // nsplit = the phase kernel's waves, set by the caller
       const double pm = (double)round_up(j.N, 32) * round_up(j.K0 + j.K1, 32);
       // outputs that fit one 128x128 wave quadrant: the 4 waves split each item's samples
       const bool thin_n = j.N <= 128, thin_k = j.K0 + j.K1 <= 128;
@@ -1157,7 +1152,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
     for (int pass = 0; pass < 3; ++pass)
       for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
         const int cls = lds_big(jobs[j]) ? 0 : (is_big(jobs[j]) ? 1 : 2);
-        if (cls != pass) continue;
+        if (cls != pass || jobs[j].fused) continue;
         for (int sp = 0; sp < jobs[j].nsplit; ++sp) {
           jj.push_back(j - D.j0[ph]);
           ss.push_back(sp);
@@ -1187,6 +1182,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
 
 // (Re)build a weight-gradient job set for batch size B.
 //   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
+static int phase_grid(sppAgent* a, int Bp);
 static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int Bp = (int)round_up(B, 32);
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
@@ -1220,7 +1216,16 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       float *gW1 = G, *gb1 = gW1 + 256 * cin, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gw3 = gb2 + 256, *gb3 = gw3 + 256;
       J(a->D1[0], 256, a->S, ob, a->cfg.acm_critic ? a->AENV : a->ACT, ca, gW1, gb1);
       J(a->D2[0], 256, a->H1[0], 256, nullptr, 0, gW2, gb2);
-      J(a->DQ[0], 1, a->H2[0], 256, nullptr, 0, gw3, gb3);
+      int fused0 = -1;
+      if (ob <= 32) {  // fc3: fused into k_ddpg_critic_phase (reduce only; its kFuse3)
+        J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
+        jobs.back().fused = 1;
+        jobs.back().nsplit = phase_grid(a, Bp) * kWavesPerWG;
+        jobs.back().wsplit = 1;
+        fused0 = (int)jobs.size() - 1;
+      } else {
+        J(a->DQ[0], 1, a->H2[0], 256, nullptr, 0, gw3, gb3);
+      }
       D.j0[0] = 0;
       D.nj[0] = (int)jobs.size();
       // actor phase (:187-196): fc1 (delta1 x s), fc2 (delta2 x h1), fc3 (dhead x h2)
@@ -1233,6 +1238,10 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       D.j0[1] = D.nj[0];
       D.nj[1] = (int)jobs.size() - D.nj[0];
       nph = 2;
+      sppStatus s = finalize_dw(D, jobs, nph, Bp, B, a->num_cu);
+      a->w3p[0] = a->w3p[1] = fused0 >= 0 ? jobs[fused0].slab : nullptr;
+      a->w3p_stride = fused0 >= 0 ? jobs[fused0].slab_stride : 0;
+      return s;
     } else {
       // BasicAcM regression (acm.py:246-258): fc1, fc2, fc21 (grad of its output = t * dz), fc3;
       // t / t1 come from the per-tile partials (k_finalize_bacm)
@@ -1249,13 +1258,19 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       nph = 1;
     }
   } else if (set == 0) {
-    // critic phase: fc1 (delta1 x [s|a]), fc2 (delta2 x h1), fc3 (dq x h2)  per critic
+    // critic phase: fc1 (delta1 x [s|a]), fc2 (delta2 x h1) per critic; fc3 (dq x h2) is fused into the
+    // critic-phase kernel, which writes one [256 | 1] partial per wave: a reduce-only job
+    int fused_idx[2];
     for (int i = 0; i < 2; ++i) {
       float* G = a->net[SPP_NET_CRITIC1 + i].g;
       float *gW1 = G, *gb1 = gW1 + 256 * cin, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gw3 = gb2 + 256, *gb3 = gw3 + 256;
       J(a->D1[i], 256, a->S, ob, a->cfg.acm_critic ? a->AENV : a->ACT, ca, gW1, gb1);
       J(a->D2[i], 256, a->H1[i], 256, nullptr, 0, gW2, gb2);
-      J(a->DQ[i], 1, a->H2[i], 256, nullptr, 0, gw3, gb3);
+      J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
+      jobs.back().fused = 1;
+      jobs.back().nsplit = phase_grid(a, Bp) * kWavesPerWG;
+      jobs.back().wsplit = 1;
+      fused_idx[i] = (int)jobs.size() - 1;
     }
     D.j0[0] = 0;
     D.nj[0] = (int)jobs.size();
@@ -1268,6 +1283,10 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     D.j0[1] = D.nj[0];
     D.nj[1] = (int)jobs.size() - D.nj[0];
     nph = 2;
+    sppStatus s = finalize_dw(D, jobs, nph, Bp, B, a->num_cu);
+    for (int i = 0; i < 2; ++i) a->w3p[i] = jobs[fused_idx[i]].slab;
+    a->w3p_stride = jobs[fused_idx[0]].slab_stride;
+    return s;
   } else {
     float* G = a->net[SPP_NET_ACM].g;
     const int in = 2 * ob;
@@ -1335,7 +1354,9 @@ static SacArgs make_args(sppAgent* a, int B) {
     p.critic[i] = a->critic[i];
     p.targ[i] = a->targ[i];
     p.H1[i] = a->H1[i]; p.H2[i] = a->H2[i]; p.D1[i] = a->D1[i]; p.D2[i] = a->D2[i]; p.DQ[i] = a->DQ[i];
+    p.W3P[i] = a->w3p[i];
   }
+  p.w3p_stride = a->w3p_stride;
   p.acm = a->acm;
   p.bacm = a->bacm;
   p.actor_targ = a->actor_targ;

@@ -183,11 +183,19 @@ template <class C>
 __global__ __launch_bounds__(256, 1) void k_ddpg_critic_phase(SacArgs p, BAcmScratch z) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  __shared__ float s_dq[kWavesPerWG][32];  // the tile's d loss / dq, for the fused fc3 weight gradient
+  // this wave's fused fc3 gradient partials [256 | bias], in LDS.  Narrow observations only: in the 111-dim
+  // ACM instantiation the fused loop spills VGPRs to scratch, so that one keeps the (DQ, H2) k_dw job.
+  constexpr bool kFuse3 = C::OB <= 32;
+  __shared__ float s_w3[kWavesPerWG][257];
   load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* big = smem + w * kLdsPerWave;
   float* small = big + kSmallRow * 32;
   const int ntiles = p.Bp / 32;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s_w3[w][lane + 64 * k] = 0.f;
+  if (lane == 0) s_w3[w][256] = 0.f;
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
     const Lane L = make_lane(big, small, tbl, p.Bp, tile * 32 + (lane & 31));
     const int b = L.b;
@@ -218,11 +226,32 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_critic_phase(SacArgs p, BAcmScr
     f32x16 xin[C::NB_CIN];
     load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, L.ld4, L.vo);
     const CriticDev& Q = p.critic[0];
-    const float q = critic_forward<C, true>(Q, xin, L, p.H1[0], p.H2[0], m1lo, m1hi, m2lo, m2hi);
+    const float q = critic_forward<C, true, 30, kFuse3>(Q, xin, L, p.H1[0], p.H2[0], m1lo, m1hi, m2lo, m2hi);
     const float diff = fsub_rn(q, y);
     const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;
     const float lq = (valid && L.h == 0) ? diff * diff : 0.f;
-    if (L.h == 0) p.DQ[0][b] = dq;
+    if constexpr (kFuse3) {
+      // fc3's weight gradient, fused as in k_sac_critic_phase (h2 in the image; per-wave partials)
+      if (L.h == 0) s_dq[w][L.s] = dq;
+      SPP_XLANE_SYNC();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int u = lane + 64 * k;
+        const float* row = big + u * 32;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) {
+          const int s2 = (j + u) & 31;
+          acc = fmaf(row[s2], s_dq[w][s2], acc);
+        }
+        s_w3[w][u] += acc;  // (each lane owns its units)
+      }
+      const float dsum = wave_sum(L.h == 0 ? dq : 0.f);
+      if (lane == 0) s_w3[w][256] += dsum;
+      SPP_XLANE_SYNC();  // the image rows are rewritten by the delta2 staging below
+    } else if (L.h == 0) {
+      p.DQ[0][b] = dq;  // the fc3 job of k_dw reads (DQ, H2)
+    }
     const rsrc_t d2r = rsrc(p.D2[0]);
     const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
@@ -245,6 +274,12 @@ __global__ __launch_bounds__(256, 1) void k_ddpg_critic_phase(SacArgs p, BAcmScr
     });
     const float s0 = wave_sum(lq);
     if (lane == 0) p.part[tile * kParts + 0] = s0;
+  }
+  if constexpr (kFuse3) {  // this wave's fc3 partials [256 weights | bias]
+    float* o0 = p.W3P[0] + ((int64_t)blockIdx.x * kWavesPerWG + w) * p.w3p_stride;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o0[lane + 64 * k] = s_w3[w][lane + 64 * k];
+    if (lane == 0) o0[256] = s_w3[w][256];
   }
 }
 

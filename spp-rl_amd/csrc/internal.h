@@ -21,6 +21,7 @@ struct DwJob {
   int wsplit;       // 4: output <= 128x128, the 4 waves of an item split its samples (one slab each); else 1
   int bf16;         // 1: bf16 MFMA (operands rounded to bf16 in registers, fp32 accumulation)
   int a_bf, x_bf;   // (bf16 only) A / X rows hold bf16 elements ([rows][Bp] __bf16), else fp32
+  int fused;        // 1: no work items -- a phase kernel writes the nsplit slabs (per wave); only reduced
 };
 
 // dw.hip (own translation unit, ks_dw.hip): the split-K weight-gradient launch + fixed-order reduce

@@ -73,6 +73,12 @@ __shared__ unsigned long long s_tlast[4];
 #else
 #define SPP_TPD(k)
 #endif
+// markers between the dense layers of the critics' backward (only with -DSPP_PROF_NODENSE)
+#if defined(SPP_PROF) && defined(SPP_PROF_NODENSE)
+#define SPP_TPN(k) SPP_TP(k)
+#else
+#define SPP_TPN(k)
+#endif
 
 // ---------------------------------------------------------------- layout maps
 // How (block, register, half) positions of a tile map to logical indices of a

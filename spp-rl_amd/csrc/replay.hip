@@ -296,10 +296,7 @@ __device__ __forceinline__ float funkey(uint32_t k) {
 // numpy's 'linear' percentile, running max / min and mean / std.
 constexpr int kStatsBlocks = 1024;      // pass-1 workgroups (moment partials)
 constexpr int kStatsColsPerThread = 8;  // columns per tx lane (ob <= 128)
-#ifndef SPP_STATS_ROWS
-#define SPP_STATS_ROWS 8
-#endif
-constexpr int kStatsRows = SPP_STATS_ROWS;  // rows in flight per thread (index then row loads)
+constexpr int kStatsRows = 8;  // rows in flight per thread (index then row loads)
 
 // Non-zero LDS bins -> the global histogram (device atomics; sparse after pass 1).
 __device__ __forceinline__ void flush_hist(const uint32_t* sh, int n, uint32_t* g) {

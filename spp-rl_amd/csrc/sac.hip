@@ -345,7 +345,9 @@ __device__ __forceinline__ void acm_forward(const SacArgs& p, const f32x16 (&xin
 
 // Critic forward through L2 with q = w3 . relu(h2) + b3 reduced per sample.
 // ST: store h1 / h2 feature-major.
-template <class C, bool ST, int R = 30>
+// H2L: h2 goes to the wave's LDS image (the caller's fused layer-3 weight gradient reads it there) instead
+// of to HBM.
+template <class C, bool ST, int R = 30, bool H2L = false>
 __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN], const Lane& L,
                                                 float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
                                                 uint64_t& m2lo, uint64_t& m2hi) {
@@ -372,7 +374,8 @@ __device__ __forceinline__ float critic_forward(const CriticDev& Q, const f32x16
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float v = fmaxf(acc[q], 0.f);
-      if constexpr (ST) op_st<C::BF>(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
+      if constexpr (H2L) L.bl[(32 * ob + ru(q)) * 32] = v;  // the image's h1 reads are done (dense_lds)
+      else if constexpr (ST) op_st<C::BF>(h2r, 32 * ob + ru(q), L.ld4, L.vo, v);
       qp = fmaf(v, tv[q], qp);
       bits |= (uint32_t)(v > 0.f) << q;
     }
@@ -444,6 +447,7 @@ template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
   __shared__ float smem[kWavesPerWG * kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  __shared__ float s_dq[kWavesPerWG][32];  // the tile's d loss / dq, for the fused layer-3 weight gradient
   SPP_TP_INIT();
   load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -452,6 +456,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
   const int ntiles = p.Bp / 32;
   const int ld = p.Bp;
   const float alpha = *p.alpha;
+  float w3a[4] = {0.f, 0.f, 0.f, 0.f}, w3b[4] = {0.f, 0.f, 0.f, 0.f}, b3a = 0.f, b3b = 0.f;  // fused fc3 grads
   for (int tile = blockIdx.x * kWavesPerWG + w; tile < ntiles; tile += gridDim.x * kWavesPerWG) {
     const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
@@ -492,12 +497,34 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
       SPP_TP(10);
-      const float q = critic_forward<C, true, 11>(Q, xin, L, p.H1[i], p.H2[i], m1lo, m1hi, m2lo, m2hi);
+      const float q = critic_forward<C, true, 11, true>(Q, xin, L, p.H1[i], nullptr, m1lo, m1hi, m2lo, m2hi);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;  // d mse / dq
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
       if (i == 0) lq0 = lqi; else lq1 = lqi;
-      if (L.h == 0) p.DQ[i][b] = dq;
+      // fc3's weight gradient, fused (sac_acm.py:117-131; dW3 = dq . h2^T, db3 = sum dq): h2 is in the image;
+      // lane l sums units l + 64k over the tile's 32 samples (rotated column order: conflict-free rows)
+      // into registers that carry over the wave's tiles; the per-wave partials are reduced in a fixed order
+      // by k_dw_reduce (no h2 / dq written to HBM and read back)
+      if (L.h == 0) s_dq[w][L.s] = dq;
+      SPP_XLANE_SYNC();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int u = lane + 64 * k;
+        const float* row = big + u * 32;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) {
+          const int s2 = (j + u) & 31;
+          acc = fmaf(row[s2], s_dq[w][s2], acc);
+        }
+        if (i == 0) w3a[k] += acc;
+        else w3b[k] += acc;
+      }
+      const float dsum = wave_sum(L.h == 0 ? dq : 0.f);
+      if (i == 0) b3a += dsum;
+      else b3b += dsum;
+      SPP_XLANE_SYNC();  // the image rows are rewritten by the delta2 staging below
       // delta2 = dq * w3 * relu'(h2): staged through the LDS image, stored feature-major
       const rsrc_t d2r = rsrc(p.D2[i]);
       const float* w3 = tbl + Q.tw3;
@@ -530,6 +557,21 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     }
     SPP_TP(15);
   }
+  // this wave's fc3 partials [256 weights | bias] per critic (every wave writes, tiles or not)
+  {
+    const int64_t wg = (int64_t)blockIdx.x * kWavesPerWG + w;
+    float* o0 = p.W3P[0] + wg * p.w3p_stride;
+    float* o1 = p.W3P[1] + wg * p.w3p_stride;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o0[lane + 64 * k] = w3a[k];
+      o1[lane + 64 * k] = w3b[k];
+    }
+    if (lane == 0) {
+      o0[256] = b3a;
+      o1[256] = b3b;
+    }
+  }
   SPP_TP_FLUSH();
 }
 
@@ -559,11 +601,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
     const Lane L = make_lane(big, small, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
-    // d loss / d logpi_b; the product is formed per tile from the SGPR operands (hoisted, its VGPR stayed
-    // live across the whole tile loop and spilled to scratch in the widest instantiations)
-    float al = alpha;
-    asm volatile("" : "+s"(al));
-    const float g_lp = valid ? al * p.inv_B : 0.f;
+    const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
     // ---- a, logpi = actor(s)  (sac_acm.py:137)
     uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
     SPP_TP(26);
@@ -626,24 +664,18 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tv[q] : 0.f;
       }
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(20);  // delta staging
-#endif
+      SPP_TPN(20);  // delta staging
       dense_lds<8, C::BF>(Q.W2T, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
       });
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(21);  // W2T
-#endif
+      SPP_TPN(21);  // W2T
       dense_lds<C::NB_CA, C::BF>(Q.W1Ta, big, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int ib = 0; ib < C::NB_CA; ++ib)
           if (ib == ob) dca[ib] += acc;
       });
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(22);  // W1Ta
-#endif
+      SPP_TPN(22);  // W1Ta
     }
     SPP_TP(31);  // critics backward
     // ---- through the frozen ACM to d a_d  (basic_model.py:118-126 backward)
@@ -684,9 +716,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
         const float t = t3v[q];
         dp3[0][q] = u < C::AC ? dca[0][q] * limv[q] * (1.f - t * t) : 0.f;
       }
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(23);  // ACM bwd input
-#endif
+      SPP_TPN(23);  // ACM bwd input
       dense<1, C::RV_AC, C::BF>(p.acm.W3T, 1, dp3, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -694,9 +724,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           L.sl[ru(q) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(24);  // ACM W3T
-#endif
+      SPP_TPN(24);  // ACM W3T
       f32x16 dp2[1];
       lds_load<1>(dp2, small);
       dense<1, C::RV_Z2, C::BF>(p.acm.W2T, 2, dp2, nullptr, [&](int ob, const f32x16& acc) {
@@ -706,9 +734,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_phase(SacArgs p, AcmScratc
           L.sl[(32 * ob + ru(q)) * 32] = acc[q] * (1.f - zz * zz);
         }
       });
-#ifdef SPP_PROF_NODENSE
-      SPP_TP(25);  // ACM W2T
-#endif
+      SPP_TPN(25);  // ACM W2T
       f32x16 dp1[2];
       lds_load<2>(dp1, small);
       dense<2, C::RV_Z1, C::BF>(p.acm.W1Ta, C::NB_AOUT, dp1, nullptr, [&](int ob, const f32x16& acc) {

@@ -62,6 +62,9 @@ struct SacArgs {
   // actor-phase outputs
   float *AH1, *AH2, *AD1, *AD2, *ADH;
   float *part;  // per-tile partial sums [ntiles][8]
+  // SAC critic phase: per-wave partials of the fused fc3 weight gradient, [waves][w3p_stride] per critic
+  float* W3P[2];
+  int64_t w3p_stride;
   // per-workgroup LDS constant table (biases, critic fc3 weights; then the limits and the
   // normaliser vectors at t_lim / t_alim / t_n0 / t_n1: lo, hi or mean, std)
   TabSeg seg[kTabSegs];

@@ -518,19 +518,21 @@ def bench_ppo(args, world, rank, dev):
     ev = ag.acm.sgd_events
     ag.acm.sgd_events = None
     if ev:
+        # one launch per epoch (sppAcmSgdEpoch: the ragged last batch inside it); rows = the ring's live rows
         ms_l = [a.elapsed_time(b) for a, b, _ in ev]
-        rows = ev[0][2]
+        rows = sum(n for _, _, n in ev) / len(ev)
         kflop = 2.0 * mac["acm_step"] * rows
         k_ms = sum(ms_l) / len(ms_l)
         kname = "k_mlp_sgd<%d, 32, %d, 0" % (2 * ob, ac)
         res["roofline"] = {
             "bound": "mfma", "kernel": "%s, true> (one ACM epoch: %d sequential Adam steps of %d rows, workgroups "
-                                      "%d)" % (kname, rows // acm_bs, acm_bs, -(-acm_bs // 64)),
+                                      "%d)" % (kname, -(-rows // acm_bs), acm_bs, -(-acm_bs // 64)),
             "achieved": round(kflop / (k_ms * 1e-3) / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(kflop / (k_ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 5), "traffic": None,
             "flop_per_launch": kflop, "algorithmic": "2 x 3 x %d MAC (AcM forward + both backward GEMMs) per row x %d "
-                                                     "rows per epoch" % (mac["M"], rows),
-            "avg_launch_ms": round(k_ms, 4), "launches": len(ms_l), "us_per_sgd_step": round(k_ms * 1e3 / (rows // acm_bs), 2),
+                                                     "rows per epoch" % (mac["M"], round(rows)),
+            "avg_launch_ms": round(k_ms, 4), "launches": len(ms_l),
+            "us_per_sgd_step": round(k_ms * 1e3 / -(-rows // acm_bs), 2),
             "whole_iteration": {"achieved": res["roofline"]["achieved"], "frac": res["roofline"]["frac"],
                                 "note": res["roofline"]["note"]}}
         if rank == 0 and world == 1 and not args.no_rocprof:

@@ -304,10 +304,16 @@ sppStatus sppAcmRegressApply(sppAgentHandle h, void* stream);
  * LDS, moments in registers (update_acm epochs, update_acm_batches).  loss_sum += sum of the
  * steps' batch losses.  AcM agents (SAC_AcM / PPO_AcM) only.  bs <= 64: one workgroup; larger batches
  * spread each step over ceil(bs / 64) workgroups (all co-resident: bs <= sppAcmSgdMaxBatch) that sum
- * the step's gradient in a fixed order (deterministic) behind one arrival barrier per step (two past
- * 4 workgroups: a sliced reduction, then the reduced gradient). */
+ * the step's gradient in a fixed order (deterministic): a reduce-scatter of per-workgroup gradient slabs,
+ * Adam on each workgroup's shard, the new parameters gathered back (two arrival barriers per step). */
 sppStatus sppAcmSgd(sppAgentHandle h, const float* x_dev, const float* y_dev, int nsteps, int bs, float* loss_sum,
                     void* stream);
+/* One update_acm epoch (acm.py:270-297: DataLoader(batch_size=bs, shuffle=True), drop_last=False) in ONE
+ * launch: ceil(nrows / bs) steps over rows [0, nrows) of x / y (gathered through the epoch's permutation),
+ * the last step over the nrows % bs ragged remainder when there is one (its loss is that batch's mean, as
+ * the reference's last DataLoader batch).  Otherwise as sppAcmSgd. */
+sppStatus sppAcmSgdEpoch(sppAgentHandle h, const float* x_dev, const float* y_dev, int nrows, int bs,
+                         float* loss_sum, void* stream);
 /* Synchronous: 1 if a multi-workgroup sppAcmSgd launch timed out waiting for its workgroups (its
  * results are then invalid), else 0. */
 sppStatus sppAcmSgdStatus(sppAgentHandle h, int* timed_out_host);
@@ -425,15 +431,16 @@ sppStatus sppOnpActorGrads(sppOnPolicyHandle h, const float* x, const float* act
 sppStatus sppOnpActorApply(sppOnPolicyHandle h, void* stream);
 /* PPO_AcM.update_actor_acm / PPO.update_actor minibatch epoch (rltoolkit/acm/on_policy.py:176-207,
  * algorithms/ppo/ppo.py:174-190) in ONE launch: nsteps sequential Adam steps of the Gaussian actor on the
- * clip loss - entropy_coef * entropy; step k's minibatch = rows idx[k*bs .. k*bs + bs) (the epoch's
- * permutation, DataLoader(shuffle=True)) of x [n][ob] (normalised obs), act [n][aout], lp_old [n], adv [n]
+ * clip loss - entropy_coef * entropy over nsteps = ceil(nrows / bs) minibatches: step k's minibatch = rows
+ * idx[k*bs .. min(k*bs + bs, nrows)) (the epoch's permutation, DataLoader(shuffle=True): the last minibatch
+ * is the ragged remainder) of x [n][ob] (normalised obs), act [n][aout], lp_old [n], adv [n]
  * (normalised advantages) and next_obs [n][aout] (the dist loss, data only; NULL: 0).  out4 [nsteps][4]:
  * each step's actor loss, KL (mean lp_old - lp_new before the step), dist MSE, entropy.  Parameters stay in
  * LDS for the launch; bs > 64 spreads each step over ceil(bs / 64) co-resident workgroups whose gradients
  * are summed in a fixed order (deterministic).  Single-process only (data-parallel ranks all-reduce every
  * minibatch gradient: sppOnpActorGrads / Apply).  Instantiated for (ob, aout) = (17, 17), (11, 11). */
 sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
-                           const float* adv, const float* next_obs, const int64_t* idx, int nsteps, int bs,
+                           const float* adv, const float* next_obs, const int64_t* idx, int nrows, int bs,
                            float* out4, void* stream);
 /* Largest bs sppOnpActorEpoch accepts on this device (0: no instantiation for the handle's dims). */
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);

@@ -1937,7 +1937,7 @@ static int mlp_sgd_max_wg(int num_cu) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_mlp_sgd<IN, H2, OUT, HEAD, true>, kMlTH,
                                                    0) != hipSuccess)
     per_cu = 0;
-  return std::min(kMlMaxWG, per_cu * num_cu);
+  return std::min(MlCfg<IN, H2, OUT, HEAD>::MAXG, per_cu * num_cu);
 }
 }
 static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
@@ -1975,9 +1975,11 @@ sppStatus sppAcmSgdStatusAsync(sppAgentHandle a, int* timed_out_pinned, void* st
   return SPP_OK;
 }
 
-sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps, int bs, float* loss_sum,
-                    void* stream) {
-  SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd: bad args");
+// nsteps sequential steps: bs rows each, the last one bs_last (<= bs) rows
+static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, int nsteps, int bs, int bs_last,
+                             float* loss_sum, void* stream) {
+  SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0 && bs_last > 0 && bs_last <= bs, SPP_E_INVALID_ARG,
+              "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
   SPP_REQUIRE(bs <= kMlR * kMlMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kMlR * kMlMaxWG);
   sppStatus s = check_ready(a);
@@ -1986,7 +1988,7 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
   const NetBufs& n = a->net[SPP_NET_ACM];
   SPP_REQUIRE(n.p && n.m && n.v, SPP_E_STATE, "acm_sgd: ACM buffers not bound");
   MlpSgdArgs g{};
-  g.x = x; g.y = y; g.nsteps = nsteps; g.bs = bs; g.bsl = bs;
+  g.x = x; g.y = y; g.nsteps = nsteps; g.bs = bs; g.bsl = bs; g.bs_last = bs_last;
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = a->cfg.acm_lr; g.step0 = a->steps[3];
   g.lim = a->limits.ptr + a->cfg.aout; g.loss_sum = loss_sum;
   const int ob = a->cfg.ob, ac = a->cfg.ac;
@@ -2016,6 +2018,19 @@ sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps
   a->steps[3] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
+}
+
+sppStatus sppAcmSgd(sppAgentHandle a, const float* x, const float* y, int nsteps, int bs, float* loss_sum,
+                    void* stream) {
+  return acm_sgd_run(a, x, y, nsteps, bs, bs, loss_sum, stream);
+}
+
+sppStatus sppAcmSgdEpoch(sppAgentHandle a, const float* x, const float* y, int nrows, int bs, float* loss_sum,
+                         void* stream) {
+  SPP_REQUIRE(nrows >= 0 && bs > 0, SPP_E_INVALID_ARG, "acm_sgd_epoch: bad args");
+  if (nrows == 0) return SPP_OK;
+  const int nsteps = cdiv(nrows, bs);
+  return acm_sgd_run(a, x, y, nsteps, bs, nrows - (nsteps - 1) * bs, loss_sum, stream);
 }
 
 sppStatus sppAcmSgdStatus(sppAgentHandle a, int* timed_out) {
@@ -2437,9 +2452,10 @@ int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
 }
 
 sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old, const float* adv,
-                           const float* next_obs, const int64_t* idx, int nsteps, int bs, float* out4, void* stream) {
-  SPP_REQUIRE(o && x && act && lp_old && adv && idx && out4 && nsteps >= 0 && bs > 0, SPP_E_INVALID_ARG,
+                           const float* next_obs, const int64_t* idx, int nrows, int bs, float* out4, void* stream) {
+  SPP_REQUIRE(o && x && act && lp_old && adv && idx && out4 && nrows >= 0 && bs > 0, SPP_E_INVALID_ARG,
               "actor epoch: bad args");
+  const int nsteps = cdiv(nrows, bs);
   SPP_REQUIRE(o->net[0].p && o->net[0].m && o->net[0].v && o->lim.ptr, SPP_E_STATE, "actor epoch: actor not bound");
   const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o);
   SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "actor epoch: no instantiation for ob=%d aout=%d", o->cfg.ob, o->cfg.aout);
@@ -2448,7 +2464,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
   hipStream_t st = S(stream);
   MlpSgdArgs g{};
   g.x = x; g.y = act; g.nxt = next_obs ? next_obs : act; g.lp_old = lp_old; g.adv = adv; g.idx = idx;
-  g.nsteps = nsteps; g.bs = bs; g.bsl = bs;
+  g.nsteps = nsteps; g.bs = bs; g.bsl = bs; g.bs_last = nrows - (nsteps - 1) * bs;
   const NetBufs& n = o->net[0];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.actor_lr; g.step0 = o->steps[0];
   g.lim = o->lim.ptr; g.eps_clip = o->cfg.ppo_epsilon; g.ent_coef = o->cfg.entropy_coef; g.out = out4;

@@ -17,7 +17,9 @@
 // reduce-scatter with sharded Adam -- each workgroup writes its gradient slab (write-through sc1 stores), one
 // arrival barrier, workgroup g sums ITS 1/G of the slab over the G slabs in a fixed order and applies Adam to
 // that shard (its Adam moments live in its registers for the whole launch), publishes the new parameters,
-// a second arrival barrier, every workgroup reloads the parameters into its LDS images.  Sums in a fixed order:
+// a second arrival barrier, every workgroup reloads the parameters into its LDS images.  The shard's G slab
+// chunks are fetched by all 256 threads at once into LDS (one memory round trip, not G dependent ones) and
+// summed from there; the reload issues all of its loads before the first LDS write.  Sums in a fixed order:
 // every workgroup (and every data-parallel replica running the same launch) holds identical parameters.
 // Adam follows torch.optim.Adam's operation order (IEEE divide / sqrt), as k_adam.
 #pragma once
@@ -40,6 +42,7 @@ struct MlpSgdArgs {
   const float* adv;      // HEAD 1: normalised advantages [n]
   const int64_t* idx;    // HEAD 1: row of step k's r-th sample = idx[k * bs + r]
   int nsteps, bs, bsl;   // bsl: rows per workgroup (G > 1)
+  int bs_last;           // rows of the last step (<= bs: an epoch's ragged last minibatch in the same launch)
   float* params;         // canonical flat parameters (state_dict order)
   float* m;              // Adam exp_avg
   float* v;              // Adam exp_avg_sq
@@ -84,6 +87,11 @@ struct MlCfg {
   static constexpr int K4 = (NP4 + kMlTH - 1) / kMlTH;  // float4 slots per thread (G = 1: all of them)
   static constexpr int NXP = (kMlR * IN + kMlTH - 1) / kMlTH, NYP = (kMlR * OUT + kMlTH - 1) / kMlTH;
   static_assert(NPS <= 64 * kMlS * 2, "gradient staging fits the H1L | D1L alias");
+  // G > 1: the shard's G slab chunks are staged in the same alias, at most NP4 + G - 1 float4
+  static constexpr int RED4 = 64 * kMlS * 2 / 4;
+  static constexpr int MAXG = RED4 - NP4 + 1 < kMlMaxWG ? RED4 - NP4 + 1 : kMlMaxWG;
+  static constexpr int RLC = HEAD ? 4 : 8;  // slab float4 loads in flight per thread (register budget)
+  static constexpr int NL = (NP4 + kMlTH - 1) / kMlTH;   // reloaded float4 per thread
   static_assert(SLAB <= kMlSlabMax, "slab");
 };
 
@@ -126,9 +134,11 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, l32 = lane & 31;
   const int sb = w & 1, hb = w >> 1;
   const int G = MW ? (int)gridDim.x : 1, g = MW ? (int)blockIdx.x : 0;
-  const int bsg = a.bs;
   const int r0 = MW ? g * a.bsl : 0;
-  const int bs = MW ? min(a.bsl, bsg - r0) : bsg;  // this workgroup's rows (<= 64)
+  auto step_rows = [&](int st) { return st == a.nsteps - 1 ? a.bs_last : a.bs; };  // the step's batch
+  auto wg_rows = [&](int st) {  // this workgroup's rows of step st (<= 64)
+    return MW ? max(0, min(a.bsl, step_rows(st) - r0)) : step_rows(st);
+  };
   if (t == 0) s_dead = 0;
   // ---- the canonical element c (< NP) of the parameters inside the LDS images
   auto pref = [&](int c) -> float& {
@@ -154,9 +164,12 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   for (int c = t; c < NP; c += kMlTH) pref(c) = a.params[c];
   // ---- Adam moments of the owned float4 slots: slot f = f0 + t + 256 k (this workgroup's shard)
   const int C4 = (C::NP4 + G - 1) / G, f0 = g * C4, f1 = min(f0 + C4, C::NP4);
-  float mom[C::K4][4], vel[C::K4][4];
+  const int c4n = max(f1 - f0, 0);  // this shard's float4 slots
+  // (MW: G >= 2, so a shard holds at most ceil(NP4 / 2) slots)
+  constexpr int K4 = MW ? ((C::NP4 + 1) / 2 + kMlTH - 1) / kMlTH : C::K4;
+  float mom[K4][4], vel[K4][4];
 #pragma unroll
-  for (int k = 0; k < C::K4; ++k)
+  for (int k = 0; k < K4; ++k)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = f0 + t + kMlTH * k, c = 4 * f + i;
@@ -180,10 +193,11 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   float xp[C::NXP], yp[C::NYP], lpp = 0.f, advp = 0.f, dsum = 0.f;
   auto row_of = [&](int st, int r) -> int64_t {
     if constexpr (HEAD) return IDX[(st & 1) * R + r];
-    else return (int64_t)st * bsg + r0 + r;
+    else return (int64_t)st * a.bs + r0 + r;
   };
   auto prefetch = [&](int st) {
     const bool live = st < a.nsteps;
+    const int bs = wg_rows(st);
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
       const int i = t + kMlTH * k, r = i / IN;
@@ -206,17 +220,19 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   };
   auto load_idx = [&](int st) {  // HEAD 1: step st's row indices -> IDX[st & 1]
     if constexpr (HEAD)
-      if (t < R) IDX[(st & 1) * R + t] = (st < a.nsteps && t < bs) ? a.idx[(int64_t)st * bsg + r0 + t] : 0;
+      if (t < R) IDX[(st & 1) * R + t] = (st < a.nsteps && t < wg_rows(st)) ? a.idx[(int64_t)st * a.bs + r0 + t] : 0;
   };
   load_idx(0);
   if (t == kMlTH - 1) adam_scalars(0);
   __syncthreads();
   prefetch(0);
   load_idx(1);
+  SPP_TP_INIT();
   float loss_acc = 0.f;  // HEAD 0: the scalar slot's owner sums the steps' losses  // HEAD 0: sum over steps (the scalar shard's owner)
-  const float inv_bs = 1.f / (float)bsg;
   const float lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
   for (int st = 0; st < a.nsteps; ++st) {
+    const int bsg = step_rows(st), bs = wg_rows(st);
+    const float inv_bs = 1.f / (float)bsg;
     // ---- the step's rows into LDS (rows >= bs: zeros)
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
@@ -240,6 +256,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     __syncthreads();  // (also: IDX[(st + 1) & 1] written)
     prefetch(st + 1);
     load_idx(st + 2);  // IDX[st & 1]: its last reader was prefetch(st), issued a step ago
+    SPP_TP(0);
     // ---- fc1: block (hb, sb) of h1 = tanh(W1 x + b1)
     f32x16 h1r;
     {
@@ -257,6 +274,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       }
     }
     __syncthreads();
+    SPP_TP(1);
     // ---- fc2: block (hb, sb) of h2 = tanh(W2 h1 + b2) (H2 = 32: waves hb = 0)
     f32x16 h2r;
     const bool l2w = hb < C::NB2;
@@ -374,6 +392,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       for (int r = 0; r < 16; ++r) D2L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = acc[r] * (1.f - h2r[r] * h2r[r]);
     }
     __syncthreads();
+    SPP_TP(2);
     // ---- dz1 = (W2^T dz2) * (1 - h1^2), block (hb, sb)
     {
       f32x16 acc;
@@ -387,6 +406,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       for (int r = 0; r < 16; ++r) D1L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = acc[r] * (1.f - h1r[r] * h1r[r]);
     }
     __syncthreads();
+    SPP_TP(3);
     // ---- weight-gradient tiles over the 64 samples: tile q = w + 4k
     f32x16 gt[C::TPW];
 #pragma unroll
@@ -421,6 +441,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       if (HEAD && g == 0 && t >= H2 + OUT && t < H2 + 2 * OUT) bg -= a.ent_coef;  // - ent_coef * d entropy / d ls
     }
     __syncthreads();  // every read of the activations is done: H1L | D1L becomes the gradient staging area
+    SPP_TP(4);
     // ---- the step's gradient in canonical order -> GR[0 .. NP), scalars -> GR[NP ..]
 #pragma unroll
     for (int k = 0; k < C::TPW; ++k) {
@@ -460,6 +481,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       for (int j = 0; j < OUT; ++j) ent += 0.5 + 0.91893853320467274178 + (double)LS[j];
       entropy = (float)ent;
     }
+    SPP_TP(5);
     const auto all = sgd_rsrc(a.slab + (int64_t)(st & 1) * G * C::SLAB);  // (G = 1: unused)
     if constexpr (MW) {
       const auto mine = sgd_rsrc(a.slab + ((int64_t)(st & 1) * G + g) * C::SLAB);
@@ -468,20 +490,41 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         slab_st4(mine, 4 * f, v4);
       }
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead);
+      // this shard's chunk of every slab -> the alias, [q][c4n] (G > 1: the staged gradient is dead)
+      const int nit = c4n * G;
+      for (int i0 = 0; i0 < nit; i0 += C::RLC * kMlTH) {  // (G = 17, 64-wide AcM: one round)
+        float4 ld[C::RLC];
+#pragma unroll
+        for (int k = 0; k < C::RLC; ++k) {
+          const int i = i0 + t + kMlTH * k;
+          if (i < nit) {
+            const int q = i / c4n;
+            ld[k] = slab_ld4(all, q * C::SLAB + 4 * (f0 + i - q * c4n));
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < C::RLC; ++k) {
+          const int i = i0 + t + kMlTH * k;
+          if (i < nit) reinterpret_cast<float4*>(H1D1)[i] = ld[k];
+        }
+      }
+      __syncthreads();
     }
+    SPP_TP(6);
     const float neg_step = adam_s[st & 1][0], bc2s = adam_s[st & 1][1];
     if (t == kMlTH - 1) adam_scalars(st + 1);
     const float omb1 = 0.1f, b2c = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     const auto pub = sgd_rsrc(a.pbuf);
 #pragma unroll
-    for (int k = 0; k < C::K4; ++k) {
+    for (int k = 0; k < K4; ++k) {
       const int f = f0 + t + kMlTH * k;
       if (f < f1) {
         float4 gg4;
         if constexpr (MW) {
+          const float4* red = reinterpret_cast<const float4*>(H1D1) + (f - f0);
           gg4 = make_float4(0.f, 0.f, 0.f, 0.f);
           for (int q = 0; q < G; ++q) {
-            const float4 x4 = slab_ld4(all, q * C::SLAB + 4 * f);
+            const float4 x4 = red[q * c4n];
             gg4.x += x4.x; gg4.y += x4.y; gg4.z += x4.z; gg4.w += x4.w;
           }
         } else {
@@ -515,24 +558,35 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       }
     }
     if (HEAD && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
+    SPP_TP(7);
     if constexpr (MW) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead);
-      for (int f = t; f < C::NP4; f += kMlTH) {
-        if (f >= f0 && f < f1) continue;  // this shard's values are already in the images
-        const float4 v4 = slab_ld4(pub, 4 * f);
-        const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+      float4 rv[C::NL];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (4 * f + i < NP) pref(4 * f + i) = vv[i];
+      for (int k = 0; k < C::NL; ++k) {  // (this shard's values are already in the images)
+        const int f = t + kMlTH * k;
+        if (f < C::NP4 && (f < f0 || f >= f1)) rv[k] = slab_ld4(pub, 4 * f);
+      }
+#pragma unroll
+      for (int k = 0; k < C::NL; ++k) {
+        const int f = t + kMlTH * k;
+        if (f < C::NP4 && (f < f0 || f >= f1)) {
+          const float vv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (4 * f + i < NP) pref(4 * f + i) = vv[i];
+        }
       }
     }
     __syncthreads();
+    SPP_TP(8);
   }
+  SPP_TP_FLUSH();
   // ---- write back: parameters (workgroup 0, from its images), moments (each shard's owner)
   if (g == 0)
     for (int c = t; c < NP; c += kMlTH) a.params[c] = pref(c);
 #pragma unroll
-  for (int k = 0; k < C::K4; ++k)
+  for (int k = 0; k < K4; ++k)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = f0 + t + kMlTH * k, c = 4 * f + i;

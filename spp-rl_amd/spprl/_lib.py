@@ -149,6 +149,7 @@ _SIGS = {
     "sppAdvSums": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAdvNormalizeGlobal": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "sppAcmSgd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, n, bs
+    "sppAcmSgdEpoch": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, rows, bs
     "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
     "sppOnpActorEpoch": (c_int, [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p]),
     "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),

@@ -173,15 +173,9 @@ class OnPolicyNets:
             perm = (torch.randperm(N, generator=generator).to(self.device) if generator is not None
                     else torch.randperm(N, device=self.device))
             outs = torch.empty(-(-N // mb), 4, device=self.device)  # one row per minibatch step
-            if one_launch:  # the whole epoch in one persistent launch (full minibatches, then the ragged one)
-                full = N // mb
-                st = stream_handle()
-                if full:
-                    call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
-                         ptr(perm), full, mb, ptr(outs), st)
-                if N % mb:
-                    call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
-                         ptr(perm[full * mb:]), 1, N % mb, ptr(outs[full:]), st)
+            if one_launch:  # the whole epoch in one persistent launch (the ragged last minibatch included)
+                call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
+                     ptr(perm), N, mb, ptr(outs), stream_handle())
                 self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
             else:
                 # one permuted copy per epoch: every minibatch is then a contiguous slice

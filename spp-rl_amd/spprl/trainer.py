@@ -597,9 +597,10 @@ class OffPolicyLoop:
             self._sgd_max_bs = int(load().sppAcmSgdMaxBatch(self._h))
         return bs <= self._sgd_max_bs
 
-    def _acm_sgd(self, idx, nsteps, bs):
-        """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd)."""
-        n = nsteps * bs
+    def _acm_sgd(self, idx, nsteps, bs, nrows=None):
+        """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd); with nrows,
+        one epoch over idx[:nrows] whose last batch is the ragged remainder (sppAcmSgdEpoch)."""
+        n = nsteps * bs if nrows is None else nrows
         st = stream_handle()
         x = torch.empty(n, 2 * self.ob_dim, device=self.device)
         y = torch.empty(n, self.ac_dim, device=self.device)
@@ -608,10 +609,13 @@ class OffPolicyLoop:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        call("sppAcmSgd", self._h, ptr(x), ptr(y), nsteps, bs, ptr(self._acm_loss_acc), st)
+        if nrows is None:
+            call("sppAcmSgd", self._h, ptr(x), ptr(y), nsteps, bs, ptr(self._acm_loss_acc), st)
+        else:
+            call("sppAcmSgdEpoch", self._h, ptr(x), ptr(y), nrows, bs, ptr(self._acm_loss_acc), st)
         if ev is not None:
             e1.record()
-            ev.append((e0, e1, nsteps * bs))
+            ev.append((e0, e1, n))
         self._keep_sgd = (idx, x, y)
 
     def _acm_sgd_check(self):
@@ -672,11 +676,8 @@ class OffPolicyLoop:
             self._acm_loss_acc.zero_()
             bs = self.acm_batch_size
             nb = -(-n // bs)
-            if self._acm_sgd_ok(bs):  # one launch for the full batches, one for the ragged last batch
-                full = n // bs
-                self._acm_sgd(perm[:full * bs].contiguous(), full, bs)
-                if n % bs:
-                    self._acm_sgd(perm[full * bs:].contiguous(), 1, n % bs)
+            if self._acm_sgd_ok(bs):  # the whole epoch in one launch, the ragged last batch included
+                self._acm_sgd(perm, nb, bs, nrows=n)
             else:
                 for s in range(0, n, bs):
                     self._acm_step_from_idx(perm[s:s + bs].contiguous())

@@ -258,13 +258,13 @@ def test_ppo_acm_actor_epochs_kl_stop_match_reference_fixture():
     assert d.mean() <= 0.02 * lr, d.mean()
 
 
-@pytest.mark.parametrize("N,mb", [(2048, 512), (2000, 512), (300, 64)])
+@pytest.mark.parametrize("N,mb", [(2048, 512), (2000, 512), (2050, 512), (300, 64)])
 def test_actor_epoch_kernel_matches_per_step_path_and_oracle(N, mb):
     """sppOnpActorEpoch (one launch per PPO epoch: every minibatch step's forward, clip-loss backward, weight
     gradients, fixed-order sum over the ceil(mb / 64) workgroups and Adam inside the kernel) against (a) the
     per-minibatch path (sppOnpActorGrads / Apply, six launches per step) and (b) the oracle's epoch loop
     (oracle.onpolicy.update_actor_epochs, on_policy.py:176-216) on the same permutations: 2 epochs, a ragged
-    last minibatch for N = 2000.  Losses / KL rtol 1e-4; parameters within 2 lr per Adam step of the oracle
+    last minibatch (inside the same launch) for N = 2000 and 2050 (2 rows: 7 of its 8 workgroups hold none).  Losses / KL rtol 1e-4; parameters within 2 lr per Adam step of the oracle
     (a sign flip of a near-zero gradient coordinate), mean far below that."""
     from spprl.onpolicy import OnPolicyNets
 

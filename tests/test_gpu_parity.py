@@ -409,6 +409,37 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     assert flag[0] == 0
 
 
+@pytest.mark.parametrize("bs,nrows", [(1049, 3 * 1049 + 2), (700, 2 * 700 + 650), (64, 5 * 64 + 1)])
+def test_acm_sgd_epoch_ragged_last_batch_matches_oracle(bs, nrows):
+    """sppAcmSgdEpoch: one update_acm epoch (DataLoader batches of bs, drop_last=False: acm.py:270-297) in
+    ONE launch, the ragged last batch included: at 3 x 1049 + 2 rows the last step has 2 rows, so 16 of
+    its 17 workgroups hold none; its loss is that batch's own mean.  Same tolerance as above."""
+    ag = _filled_agent("HalfCheetah-v2", 17, 6, 4000, seed=8)
+    rb = ag.replay_buffer
+    params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}
+    o = OracleAcmTrainer(34, 6, lr=ag.acm_lr, ac_lim=ag.ac_lim.numpy(), params=params)
+    idx = torch.from_numpy(np.random.RandomState(12).randint(0, 4000, nrows)).to(DEV)
+    loss = torch.zeros(1, device=DEV)
+    xg = torch.empty(nrows, 34, device=DEV)
+    yg = torch.empty(nrows, 6, device=DEV)
+    _lib.call("sppReplayGatherAcm", rb._h, _lib.ptr(idx), nrows, _lib.ptr(xg), _lib.ptr(yg), _lib.stream_handle())
+    _lib.call("sppAcmSgdEpoch", ag._h, _lib.ptr(xg), _lib.ptr(yg), nrows, bs, _lib.ptr(loss), _lib.stream_handle())
+    x_all, y_all = xg.cpu().numpy(), yg.cpu().numpy()
+    losses = [o.batch_update(x_all[s:s + bs], y_all[s:s + bs]) for s in range(0, nrows, bs)]
+    torch.cuda.synchronize()
+    assert float(loss.item()) == pytest.approx(sum(losses), rel=1e-4)
+    got = ag.params[_lib.SPP_NET_ACM].cpu().numpy()
+    ref = o.flat()
+    d = np.abs(got - ref)
+    assert np.mean(d > 1e-5 * np.maximum(1, np.abs(ref))) < 5e-3 and d.max() < 4 * len(losses) * ag.acm_lr
+    steps = np.zeros(4, np.int64)
+    _lib.call("sppAgentGetSteps", ag._h, steps.ctypes.data_as(__import__("ctypes").c_void_p))
+    assert steps[3] == len(losses)
+    flag = np.ones(1, np.int32)
+    _lib.call("sppAcmSgdStatus", ag._h, flag.ctypes.data)
+    assert flag[0] == 0
+
+
 def test_acm_multi_workgroup_sgd_is_deterministic():
     """The multi-workgroup sppAcmSgd sums the workgroups' gradients in a fixed order: two agents with
     the same initial AcM and the same batches end bit-identical (what lets data-parallel ranks run

@@ -1,6 +1,7 @@
-"""Region timing of the persistent AcM SGD kernel (k_acm_sgd) at the PPO HalfCheetah shape (AcM in 34,
-out 6, 64-sample batches).  Profiling build: python spp-rl_amd/build.py --prof --hopper-only --hcheetah, then
-SPPRL_LIB=spp-rl_amd/spprl/libspprl_prof.so python tools/sgd_prof.py"""
+"""Region timing of the persistent MLP SGD kernel (k_mlp_sgd<34, 32, 6, 0>) at the PPO HalfCheetah AcM shape
+(AcM in 34, out 6; argv[1] = batch rows, 1049 = the bench's).  Profiling build:
+python spp-rl_amd/build.py --prof --hopper-only --hcheetah, then
+SPPRL_LIB=spp-rl_amd/spprl/libspprl_prof.so python tools/sgd_prof.py [bs]"""
 import ctypes
 import os
 import sys
@@ -15,14 +16,15 @@ import torch  # noqa: E402
 import spprl  # noqa: E402
 from spprl import _lib  # noqa: E402
 
-NAMES = {0: "stage batch", 1: "fc1", 2: "fc2, fc3, loss, dz3, dz2", 3: "dz1", 4: "gradient tiles",
-         5: "slab, barrier, reduce", 6: "Adam"}
+NAMES = {0: "stage rows, prefetch", 1: "fc1", 2: "fc2, fc3, loss, dz2", 3: "dz1", 4: "gradient tiles, bias sums",
+         5: "canonical staging", 6: "slab stores, barrier 1", 7: "shard reduce, Adam, publish",
+         8: "barrier 2, reload"}
 
 
 def main():
     dev = torch.device("cuda", 0)
     ob, ac, K = 17, 6, 400
-    bs = int(sys.argv[1]) if len(sys.argv) > 1 else 64  # > 128: the multi-workgroup form
+    bs = int(sys.argv[1]) if len(sys.argv) > 1 else 1049  # > 64: the multi-workgroup form
     ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", max_batch=max(4096, bs), buffer_size=40_000, device=dev, seed=0)
     rb = ag.replay_buffer
     n = 20_000
@@ -45,11 +47,12 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     _lib.call("sppDebugReadProf", buf, 1)
-    v = np.array(buf[:32], dtype=np.float64) / (4 * K)  # waves 0..3 recorded
+    G = -(-bs // 64)
+    v = np.array(buf[:32], dtype=np.float64) / (4 * K * G)  # waves 0..3 of every workgroup recorded
     tot = v.sum()
-    print("k_acm_sgd_mf<34, 6>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
+    print("k_mlp_sgd<34, 32, 6, 0>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
           % (K, bs, el * 1e3, el * 1e6 / K, tot))
-    for k in range(7):
+    for k in range(9):
         print("  %2d %-20s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
 
 

@@ -7,12 +7,18 @@
 //           log_prob of the stored actions under Normal(mu, exp(log_scale)), clip loss - ent_coef * entropy;
 //           rows gathered through the epoch's permutation; per step {actor loss, KL, dist, entropy} out.
 //
-// One step of bs rows runs on G = ceil(bs / 64) workgroups of 4 waves (64 rows each); wave w = (sample block
-// sb = w & 1, unit block hb = w >> 1).  Every layer, delta and weight gradient is a v_mfma_f32_32x32x2_f32
-// tile from LDS images laid out conflict-free (odd row strides):
-//   X [64 samples][SX]   the step's inputs (+ a constant-1 column IN: b1's gradient is dW1's column IN)
-//   H1L / D1L [64 units][65], H2L / D2L [H2][65], D3L / LSL [32][65]  activations and deltas ([unit][sample])
-//   W1 [64][SW1], W2 [H2][65], W3 [32][H2 + 1]  parameters (row = output unit; rows >= OUT zero)
+// One step of bs rows runs on G = ceil(bs / 64) workgroups of 4 waves; wave w owns 16 of the workgroup's 64
+// rows (image column 16 w + n, n = lane & 15) through every layer.  Forward and backward are
+// v_mfma_f32_16x16x4_f32 tiles with units on the rows and the wave's samples on the columns: a result tile
+// (lane (q = lane >> 4, n), register i = unit 4q + i of sample n) is the next layer's B operand as it stands
+// (k-step (T, j) of lane group q = unit 16T + 4q + j), so activations and deltas stay in registers from
+// layer to layer and the waves never wait for each other until the weight gradient.  fc1's bias is a
+// column of W1 against a constant-1 input row.  The activations and deltas are also written to
+// [unit][64 sample] LDS images (row stride 68: the result-layout stores hit 64 distinct banks); the weight
+// gradients dW = delta . act^T are 16x16 tiles over all 64 samples (sample 16q + ks on k-step ks), spread
+// over the 4 waves, two tiles in flight per wave; b2 / b3 / log_scale gradients are 16-lane row sums of the
+// delta registers (per wave), added over the waves in a fixed order.
+//
 // The step's gradient is staged in canonical (state_dict) order in LDS.  G = 1: Adam in place.  G > 1: a
 // reduce-scatter with sharded Adam -- each workgroup writes its gradient slab (write-through sc1 stores), one
 // arrival barrier, workgroup g sums ITS 1/G of the slab over the G slabs in a fixed order and applies Adam to
@@ -23,14 +29,14 @@
 // every workgroup (and every data-parallel replica running the same launch) holds identical parameters.
 // Adam follows torch.optim.Adam's operation order (IEEE divide / sqrt), as k_adam.
 #pragma once
-// (included by api.hip after sgd.hip: AcmSgdArgs' slab helpers and the bounded arrival barrier)
+// (included by api.hip after sgd.hip: the slab helpers and the bounded arrival barrier)
 
 namespace spp {
 
-constexpr int kMlR = 64;      // rows per workgroup and step
-constexpr int kMlTH = 256;    // 4 waves
-constexpr int kMlS = 65;      // row stride of the [unit][sample] images
-constexpr int kMlMaxWG = 512;  // workgroups per step (bs <= 32,768)
+constexpr int kMlR = 64;          // rows per workgroup and step (4 waves x 16)
+constexpr int kMlTH = 256;        // 4 waves
+constexpr int kMlRS = 68;         // row stride of the [unit][64 sample] images
+constexpr int kMlMaxWG = 512;     // workgroups per step (bs <= 32,768)
 constexpr int kMlSlabMax = 8192;  // slab floats per workgroup (>= MlCfg::SLAB)
 
 struct MlpSgdArgs {
@@ -62,15 +68,17 @@ template <int IN, int H2, int OUT, int HEAD>
 struct MlCfg {
   static_assert(H2 == 32 || H2 == 64, "H2");
   static_assert(OUT >= 1 && OUT <= 32, "OUT");
-  static constexpr int NKS1 = (IN + 1) / 2;        // fc1 k-steps (pairs of inputs)
-  static constexpr int NIB1 = (IN + 1 + 31) / 32;  // dW1 input blocks (input IN: the constant 1)
-  static constexpr int SX = ((2 * NKS1 > 32 * NIB1 ? 2 * NKS1 : 32 * NIB1)) | 1;
-  static constexpr int SW1 = (2 * NKS1) | 1;
-  static constexpr int SW3 = H2 + 1;
-  static constexpr int NB2 = H2 / 32;              // unit blocks of layer 2
-  static constexpr int NKS3 = (OUT + 1) / 2;       // k-steps over fc3's outputs (dz2)
-  static constexpr int NTILE = 2 * NIB1 + 2 * NB2 + NB2;  // dW1 | dW2 | dW3
-  static constexpr int TPW = (NTILE + 3) / 4;
+  static constexpr int KQ1 = (IN + 1 + 3) / 4;     // fc1 k-steps (the inputs and the constant-1 row)
+  static constexpr int SW1 = 4 * (KQ1 | 1);        // W1 row stride (odd multiple of 4: conflict-free A reads)
+  static constexpr int NIT1 = (IN + 1 + 15) / 16;  // dW1 column tiles (inputs + the bias column)
+  static constexpr int XTR = 16 * NIT1 > 4 * KQ1 ? 16 * NIT1 : 4 * KQ1;  // rows of the transposed input image
+  static constexpr int NB2 = H2 / 16;              // layer-2 unit tiles
+  static constexpr int NO = (OUT + 15) / 16;       // output tiles
+  static constexpr int SW2 = 68;                   // W2 row stride (64 h1 units + 4)
+  static constexpr int SW3 = H2 + 4;               // W3 row stride
+  static constexpr int NT1 = 4 * NIT1, NT2 = NB2 * 4, NT3 = NO * NB2, NT = NT1 + NT2 + NT3;  // dW tiles
+  static constexpr int IMGR = 128 + 2 * H2 + 16 * NO;  // image rows: H1, D1, H2, D2, D3
+  static constexpr int NBP = H2 + 16 * NO + (HEAD ? 16 * NO : 0);  // per-wave bias partials: b2, b3 (, ls)
   // canonical layout: [log_scale (HEAD 1)] fc1.weight fc1.bias fc2.weight fc2.bias fc3.weight fc3.bias
   static constexpr int O_W1 = HEAD ? OUT : 0;
   static constexpr int O_B1 = O_W1 + 64 * IN;
@@ -86,53 +94,83 @@ struct MlCfg {
   static constexpr int SLAB = (NPS + 63) / 64 * 64;     // slab stride (floats)
   static constexpr int K4 = (NP4 + kMlTH - 1) / kMlTH;  // float4 slots per thread (G = 1: all of them)
   static constexpr int NXP = (kMlR * IN + kMlTH - 1) / kMlTH, NYP = (kMlR * OUT + kMlTH - 1) / kMlTH;
-  static_assert(NPS <= 64 * kMlS * 2, "gradient staging fits the H1L | D1L alias");
-  // G > 1: the shard's G slab chunks are staged in the same alias, at most NP4 + G - 1 float4
-  static constexpr int RED4 = 64 * kMlS * 2 / 4;
+  static_assert(SLAB <= kMlSlabMax, "slab");
+  // G > 1: the shard's G slab chunks are staged in the image region, at most NP4 + G - 1 float4
+  static constexpr int RED4 = IMGR * kMlRS / 4;
   static constexpr int MAXG = RED4 - NP4 + 1 < kMlMaxWG ? RED4 - NP4 + 1 : kMlMaxWG;
   static constexpr int RLC = HEAD ? 4 : 8;  // slab float4 loads in flight per thread (register budget)
   static constexpr int NL = (NP4 + kMlTH - 1) / kMlTH;   // reloaded float4 per thread
-  static_assert(SLAB <= kMlSlabMax, "slab");
 };
 
-__device__ __forceinline__ constexpr int ml_ru(int r) { return (r & 3) + 8 * (r >> 2); }
-__device__ __forceinline__ f32x16 ml_mfma(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 ml_mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-
-template <class C>
-__device__ __forceinline__ void ml_tile(int t, int& layer, int& r0, int& c0) {
-  if (t < 2 * C::NIB1) {
-    layer = 0; r0 = 32 * (t & 1); c0 = 32 * (t >> 1);
-  } else if (t < 2 * C::NIB1 + 2 * C::NB2) {
-    const int q = t - 2 * C::NIB1;
-    layer = 1; r0 = 32 * (q >> 1); c0 = 32 * (q & 1);
-  } else {
-    layer = 2; r0 = 0; c0 = 32 * (t - 2 * C::NIB1 - 2 * C::NB2);
-  }
+// tanh without branches: |x| < 0.625 the odd polynomial of ocml's tanhf, else 1 - 2 / (e^{2|x|} + 1) with
+// e^{2|x|} = 2^h (1 + l ln 2) from the split product 2|x| log2(e) = h + l (v_exp_f32, v_rcp_f32); within a few
+// ulp of tanhf, no divergent branch (the SGD's fp32 tolerance: tests/test_gpu_parity.py, test_gpu_onpolicy.py)
+__device__ __forceinline__ float ml_tanh(float x) {
+  const float ax = fabsf(x);
+  const float t2 = ax + ax;
+  const float h = t2 * 1.44269504088896341f;
+  const float l = fmaf(t2, 1.44269504088896341f, -h) + t2 * 1.925963033500e-8f;
+  const float e = __builtin_amdgcn_exp2f(h) * fmaf(l, 0.693147180559945309f, 1.f);
+  const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+  const float x2 = x * x;
+  float p = fmaf(x2, -0.00570002059f, 0.0206340719f);
+  p = fmaf(x2, p, -0.0537379310f);
+  p = fmaf(x2, p, 0.133314162f);
+  p = fmaf(x2, p, -0.333332807f);
+  const float small = fmaf(x2, ax * p, ax);
+  return copysignf(ax < 0.625f ? small : big, x);
+}
+// sum over the 16 lanes of a lane's DPP row (row_ror 8, 4, 2, 1: every lane ends with a row sum; callers take
+// lane 0 of the row, so the order is fixed)
+template <int CTRL>
+__device__ __forceinline__ float ml_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float ml_row16_sum(float v) {
+  v += ml_dpp<0x128>(v);
+  v += ml_dpp<0x124>(v);
+  v += ml_dpp<0x122>(v);
+  v += ml_dpp<0x121>(v);
+  return v;
+}
+// sum over the wave: the 4 row sums (lanes 0, 16, 32, 48) added in a fixed order (uniform result)
+__device__ __forceinline__ float ml_wave_sum(float v) {
+  v = ml_row16_sum(v);
+  const int b = __builtin_bit_cast(int, v);
+  auto lane_v = [&](int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, l)); };
+  return (lane_v(0) + lane_v(16)) + (lane_v(32) + lane_v(48));
 }
 
 template <int IN, int H2, int OUT, int HEAD, bool MW>
 __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   using C = MlCfg<IN, H2, OUT, HEAD>;
-  constexpr int SX = C::SX, SW1 = C::SW1, SW3 = C::SW3, S = kMlS, R = kMlR, NP = C::NP;
-  __shared__ float X[R * SX];
-  __shared__ __attribute__((aligned(16))) float H1D1[2 * 64 * S];  // H1L | D1L; then the step's gradient
-  __shared__ float H2L[H2 * S], D2L[H2 * S], D3L[32 * S];
-  __shared__ float LSL[HEAD ? 32 * S : 1];
-  __shared__ float W1[64 * SW1], W2[H2 * S], W3[32 * SW3];
-  __shared__ float B1[64], B2[H2], B3[32], LS[32];
+  constexpr int RS = kMlRS, R = kMlR, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
+                NO = C::NO;
+  __shared__ __attribute__((aligned(16))) float IMG[C::IMGR * RS];  // H1 | D1 | H2 | D2 | D3; G > 1: the slab chunks
+  __shared__ __attribute__((aligned(16))) float XT[C::XTR * RS];    // [input][sample]; row IN = 1 (rows < bs)
+  __shared__ __attribute__((aligned(16))) float GR[C::NPS];         // the step's gradient, canonical order
+  __shared__ __attribute__((aligned(16))) float W1[64 * SW1];       // [unit][input]; column IN = b1
+  __shared__ __attribute__((aligned(16))) float W2[H2 * SW2];
+  __shared__ __attribute__((aligned(16))) float W3[16 * NO * SW3];  // rows >= OUT zero
+  __shared__ float B2[H2], B3[16 * NO], LS[32], LIM[32];
   __shared__ float Y[R * OUT];
   __shared__ float LPO[HEAD ? R : 1], ADV[HEAD ? R : 1];
   __shared__ int64_t IDX[HEAD ? 2 * R : 1];
+  __shared__ float BP[4][C::NBP];   // per wave: bias (and log_scale) gradient partials over its 16 samples
   __shared__ float SCP[4][4];       // per wave: scalar partials
   __shared__ float adam_s[2][2];
   __shared__ int s_dead;
-  float* const H1L = H1D1;
-  float* const D1L = H1D1 + 64 * S;
-  float* const GR = H1D1;  // staging alias (after the gradient tiles)
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, l32 = lane & 31;
-  const int sb = w & 1, hb = w >> 1;
+  float* const H1I = IMG;
+  float* const D1I = IMG + 64 * RS;
+  float* const H2I = IMG + 128 * RS;
+  float* const D2I = H2I + H2 * RS;
+  float* const D3I = D2I + H2 * RS;
+  const int t = threadIdx.x, lane = t & 63, q = lane >> 4, n = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: the tile choices below are scalar
+  const int col = 16 * w + n;  // this lane's sample (image column)
   const int G = MW ? (int)gridDim.x : 1, g = MW ? (int)blockIdx.x : 0;
   const int r0 = MW ? g * a.bsl : 0;
   auto step_rows = [&](int st) { return st == a.nsteps - 1 ? a.bs_last : a.bs; };  // the step's batch
@@ -143,23 +181,23 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   // ---- the canonical element c (< NP) of the parameters inside the LDS images
   auto pref = [&](int c) -> float& {
     if (HEAD && c < C::O_W1) return LS[c];
-    if (c < C::O_B1) { const int q = c - C::O_W1; return W1[(q / IN) * SW1 + q % IN]; }
-    if (c < C::O_W2) return B1[c - C::O_B1];
-    if (c < C::O_B2) { const int q = c - C::O_W2; return W2[(q >> 6) * S + (q & 63)]; }
+    if (c < C::O_B1) { const int p = c - C::O_W1; return W1[(p / IN) * SW1 + p % IN]; }
+    if (c < C::O_W2) return W1[(c - C::O_B1) * SW1 + IN];
+    if (c < C::O_B2) { const int p = c - C::O_W2; return W2[(p >> 6) * SW2 + (p & 63)]; }
     if (c < C::O_W3) return B2[c - C::O_B2];
-    if (c < C::O_B3) { const int q = c - C::O_W3; return W3[(q / H2) * SW3 + q % H2]; }
+    if (c < C::O_B3) { const int p = c - C::O_W3; return W3[(p / H2) * SW3 + p % H2]; }
     return B3[c - C::O_B3];
   };
-  // ---- parameter images (zero padding)
+  // ---- images (zero padding)
   for (int i = t; i < 64 * SW1; i += kMlTH) W1[i] = 0.f;
-  for (int i = t; i < H2 * S; i += kMlTH) W2[i] = 0.f;
-  for (int i = t; i < 32 * SW3; i += kMlTH) W3[i] = 0.f;
-  if (t < 32) { B3[t] = 0.f; LS[t] = 0.f; }
-  for (int i = t; i < 32 * S; i += kMlTH) {
-    D3L[i] = 0.f;  // rows >= OUT stay zero
-    if constexpr (HEAD) LSL[i] = 0.f;
+  for (int i = t; i < H2 * SW2; i += kMlTH) W2[i] = 0.f;
+  for (int i = t; i < 16 * NO * SW3; i += kMlTH) W3[i] = 0.f;
+  for (int i = t; i < C::XTR * RS; i += kMlTH) XT[i] = 0.f;  // rows > IN stay zero
+  if (t < 16 * NO) B3[t] = 0.f;
+  if (t < 32) {
+    LS[t] = 0.f;
+    LIM[t] = t < OUT ? a.lim[t] : 0.f;
   }
-  for (int i = t; i < R * SX; i += kMlTH) X[i] = 0.f;  // padding columns / rows past bs stay zero
   __syncthreads();
   for (int c = t; c < NP; c += kMlTH) pref(c) = a.params[c];
   // ---- Adam moments of the owned float4 slots: slot f = f0 + t + 256 k (this workgroup's shard)
@@ -222,24 +260,15 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     if constexpr (HEAD)
       if (t < R) IDX[(st & 1) * R + t] = (st < a.nsteps && t < wg_rows(st)) ? a.idx[(int64_t)st * a.bs + r0 + t] : 0;
   };
-  load_idx(0);
-  if (t == kMlTH - 1) adam_scalars(0);
-  __syncthreads();
-  prefetch(0);
-  load_idx(1);
-  SPP_TP_INIT();
-  float loss_acc = 0.f;  // HEAD 0: the scalar slot's owner sums the steps' losses  // HEAD 0: sum over steps (the scalar shard's owner)
-  const float lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
-  for (int st = 0; st < a.nsteps; ++st) {
-    const int bsg = step_rows(st), bs = wg_rows(st);
-    const float inv_bs = 1.f / (float)bsg;
-    // ---- the step's rows into LDS (rows >= bs: zeros)
+  // ---- a prefetched step's rows into LDS: inputs transposed (rows >= bs: zeros), the constant-1 row
+  float dist_next = 0.f;
+  auto stage = [&](int st) {
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
       const int i = t + kMlTH * k;
-      if (i < R * IN) X[(i / IN) * SX + (i % IN)] = xp[k];
+      if (i < R * IN) XT[(i % IN) * RS + i / IN] = xp[k];
     }
-    if (t < R) X[t * SX + IN] = t < bs ? 1.f : 0.f;  // the bias input
+    if (t < R) XT[IN * RS + t] = t < wg_rows(st) ? 1.f : 0.f;
 #pragma unroll
     for (int k = 0; k < C::NYP; ++k) {
       const int i = t + kMlTH * k;
@@ -251,105 +280,139 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         ADV[t] = advp;
       }
     }
-    const float dist_step = dsum;
+    dist_next = dsum;
     dsum = 0.f;
-    __syncthreads();  // (also: IDX[(st + 1) & 1] written)
-    prefetch(st + 1);
+  };
+  load_idx(0);
+  if (t == kMlTH - 1) adam_scalars(0);
+  __syncthreads();
+  prefetch(0);
+  load_idx(1);
+  stage(0);
+  __syncthreads();
+  SPP_TP_INIT();
+  float loss_acc = 0.f;  // HEAD 0: sum over steps of the batch loss (the scalar slot's owner)
+  const float lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
+  for (int st = 0; st < a.nsteps; ++st) {
+    const int bsg = step_rows(st), bs = wg_rows(st);
+    const float inv_bs = 1.f / (float)bsg;
+    const float dist_step = dist_next;
+    prefetch(st + 1);  // (IDX[(st + 1) & 1]: written a step ago, behind the last step's barrier)
     load_idx(st + 2);  // IDX[st & 1]: its last reader was prefetch(st), issued a step ago
     SPP_TP(0);
-    // ---- fc1: block (hb, sb) of h1 = tanh(W1 x + b1)
-    f32x16 h1r;
+    const bool svalid = col < bs;
+    // ---- fc1: h1 = tanh(W1 [x; 1]), 4 unit tiles of this wave's 16 samples
+    f32x4 h1r[4];
     {
-      f32x16 acc;
+      f32x4 acc[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = B1[32 * hb + ml_ru(r) + 4 * h];
-      const float* pa = W1 + (32 * hb + l32) * SW1 + h;
-      const float* pb = X + (32 * sb + l32) * SX + h;
+      for (int T = 0; T < 4; ++T) acc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < C::NKS1; ++ks) acc = ml_mfma(pa[2 * ks], pb[2 * ks], acc);
+      for (int ks = 0; ks < C::KQ1; ++ks) {
+        const float xb = XT[(4 * ks + q) * RS + col];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        h1r[r] = tanhf(acc[r]);
-        H1L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = h1r[r];
+        for (int T = 0; T < 4; ++T) acc[T] = ml_mfma16(W1[(16 * T + n) * SW1 + 4 * ks + q], xb, acc[T]);
       }
+#pragma unroll
+      for (int T = 0; T < 4; ++T)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          h1r[T][i] = ml_tanh(acc[T][i]);
+          H1I[(16 * T + 4 * q + i) * RS + col] = h1r[T][i];
+        }
     }
-    __syncthreads();
     SPP_TP(1);
-    // ---- fc2: block (hb, sb) of h2 = tanh(W2 h1 + b2) (H2 = 32: waves hb = 0)
-    f32x16 h2r;
-    const bool l2w = hb < C::NB2;
-    if (l2w) {
-      f32x16 acc;
+    // ---- fc2: h2 = tanh(W2 h1 + b2); k-step (T, j) of lane group q = h1 unit 16T + 4q + j (h1r[T][j])
+    f32x4 h2r[NB2];
+    {
+      f32x4 acc[NB2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = B2[32 * hb + ml_ru(r) + 4 * h];
-      const float* pa = W2 + (32 * hb + l32) * S + h;
-      const float* pb = H1L + h * S + 32 * sb + l32;
-#pragma unroll 8
-      for (int ks = 0; ks < 32; ++ks) acc = ml_mfma(pa[2 * ks], pb[2 * ks * S], acc);
+      for (int T2 = 0; T2 < NB2; ++T2)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        h2r[r] = tanhf(acc[r]);
-        H2L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = h2r[r];
-      }
+        for (int i = 0; i < 4; ++i) acc[T2][i] = B2[16 * T2 + 4 * q + i];
+#pragma unroll
+      for (int T = 0; T < 4; ++T)
+#pragma unroll
+        for (int T2 = 0; T2 < NB2; ++T2) {
+          const float4 w4 = *reinterpret_cast<const float4*>(W2 + (16 * T2 + n) * SW2 + 16 * T + 4 * q);
+          acc[T2] = ml_mfma16(w4.x, h1r[T][0], acc[T2]);
+          acc[T2] = ml_mfma16(w4.y, h1r[T][1], acc[T2]);
+          acc[T2] = ml_mfma16(w4.z, h1r[T][2], acc[T2]);
+          acc[T2] = ml_mfma16(w4.w, h1r[T][3], acc[T2]);
+        }
+#pragma unroll
+      for (int T2 = 0; T2 < NB2; ++T2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          h2r[T2][i] = ml_tanh(acc[T2][i]);
+          H2I[(16 * T2 + 4 * q + i) * RS + col] = h2r[T2][i];
+        }
     }
-    // H2 = 64: fc3 of sample block sb reads both unit blocks; H2 = 32: the same wave's other lanes (a compiler
-    // memory barrier keeps their reads below these stores)
-    if constexpr (H2 == 64) __syncthreads();
-    else asm volatile("" ::: "memory");
-    // ---- fc3 and the head (waves hb = 0): D3L = d loss / d z3
-    if (hb == 0) {
-      f32x16 acc;
+    // ---- fc3 and the head: d3r = d loss / d z3 (rows >= OUT zero)
+    f32x4 d3r[NO];
+    {
+      f32x4 acc[NO];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int u = ml_ru(r) + 4 * h;
-        acc[r] = u < OUT ? B3[u] : 0.f;
-      }
-      const float* pa = W3 + l32 * SW3 + h;
-      const float* pb = H2L + h * S + 32 * sb + l32;
-#pragma unroll 8
-      for (int ks = 0; ks < H2 / 2; ++ks) acc = ml_mfma(pa[2 * ks], pb[2 * ks * S], acc);
-      const int sm = 32 * sb + l32;
-      const bool valid = sm < bs;
+      for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[T3][i] = B3[16 * T3 + 4 * q + i];
+#pragma unroll
+      for (int T = 0; T < NB2; ++T)
+#pragma unroll
+        for (int T3 = 0; T3 < NO; ++T3) {
+          const float4 w4 = *reinterpret_cast<const float4*>(W3 + (16 * T3 + n) * SW3 + 16 * T + 4 * q);
+          acc[T3] = ml_mfma16(w4.x, h2r[T][0], acc[T3]);
+          acc[T3] = ml_mfma16(w4.y, h2r[T][1], acc[T3]);
+          acc[T3] = ml_mfma16(w4.z, h2r[T][2], acc[T3]);
+          acc[T3] = ml_mfma16(w4.w, h2r[T][3], acc[T3]);
+        }
       if constexpr (HEAD == 0) {
         float lpart = 0.f;
         const float inv_n = 1.f / (float)(bsg * OUT);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int u = ml_ru(r) + 4 * h;
-          if (u < OUT) {
-            const float th = tanhf(acc[r]), lm = a.lim[u];
-            const float e = th * lm - Y[sm * OUT + u];
+        for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int u = 16 * T3 + 4 * q + i;
             float d = 0.f;
-            if (valid) {
-              lpart = fmaf(e, e, lpart);
-              d = 2.f * e * inv_n * lm * (1.f - th * th);
+            if (u < OUT) {
+              const float th = ml_tanh(acc[T3][i]), lm = LIM[u];
+              const float e = th * lm - Y[col * OUT + u];
+              if (svalid) {
+                lpart = fmaf(e, e, lpart);
+                d = 2.f * e * inv_n * lm * (1.f - th * th);
+              }
             }
-            D3L[u * S + sm] = d;
+            d3r[T3][i] = d;
           }
-        }
-        lpart = wave_sum(lpart);
+        lpart = ml_wave_sum(lpart);
         if (lane == 0) SCP[w][0] = lpart;
       } else {
-        // log_prob of the stored action (torch Normal: -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi)), summed)
-        float th[16], dd[16], lp = 0.f;
+        // log_prob of the stored action (torch Normal: -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi)), summed
+        // over the outputs: this lane's registers, then the sample's 4 lane groups)
+        float th[NO][4], dd[NO][4], lp = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int u = ml_ru(r) + 4 * h;
-          th[r] = 0.f;
-          dd[r] = 0.f;
-          if (u < OUT) {
-            const float sc = expf(LS[u]);
-            th[r] = tanhf(acc[r]);
-            const float mu = fmul_rn(th[r], a.lim[u]);
-            dd[r] = fsub_rn(Y[sm * OUT + u], mu);
-            lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(dd[r], dd[r]), 2.f * fmul_rn(sc, sc)), logf(sc)), kLogSqrt2PiO);
+        for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int u = 16 * T3 + 4 * q + i;
+            th[T3][i] = 0.f;
+            dd[T3][i] = 0.f;
+            if (u < OUT) {
+              const float sc = expf(LS[u]);
+              th[T3][i] = ml_tanh(acc[T3][i]);
+              const float mu = fmul_rn(th[T3][i], LIM[u]);
+              dd[T3][i] = fsub_rn(Y[col * OUT + u], mu);
+              lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(dd[T3][i], dd[T3][i]), 2.f * fmul_rn(sc, sc)), logf(sc)),
+                            kLogSqrt2PiO);
+            }
           }
-        }
+        lp += __shfl_xor(lp, 16, 64);
         lp += __shfl_xor(lp, 32, 64);
         // clip objective (ppo.py:194-204) and its gradient wrt lp_new (torch minimum / clamp rules)
         float mterm = 0.f, kl = 0.f, glp = 0.f;
-        if (valid) {
-          const float lpo = LPO[sm], A = ADV[sm];
+        if (svalid) {
+          const float lpo = LPO[col], A = ADV[col];
           const float rt = expf(fsub_rn(lp, lpo));
           const float rc = fminf(fmaxf(rt, lo), hi);
           const float u1 = fmul_rn(rt, A), u2 = fmul_rn(rc, A);
@@ -360,118 +423,163 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           glp = -(wu * A * rt + (1.f - wu) * A * pass * rt) * inv_bs;
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int u = ml_ru(r) + 4 * h;
-          if (u < OUT) {
-            const float sc = expf(LS[u]);
-            const float var = fmul_rn(sc, sc);
-            const float gmu = glp * dd[r] / var;
-            LSL[u * S + sm] = glp * (dd[r] * dd[r] / var - 1.f);
-            D3L[u * S + sm] = gmu * a.lim[u] * (1.f - th[r] * th[r]);
+        for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int u = 16 * T3 + 4 * q + i;
+            float d = 0.f, lsg = 0.f;
+            if (u < OUT) {
+              const float sc = expf(LS[u]);
+              const float var = fmul_rn(sc, sc);
+              const float gmu = glp * dd[T3][i] / var;
+              lsg = glp * (dd[T3][i] * dd[T3][i] / var - 1.f);
+              d = gmu * LIM[u] * (1.f - th[T3][i] * th[T3][i]);
+            }
+            d3r[T3][i] = d;
+            lsg = ml_row16_sum(lsg);  // the log_scale gradient over this wave's 16 samples
+            if (n == 0 && u < OUT) BP[w][H2 + 16 * NO + u] = lsg;
           }
-        }
-        const float sm_ = wave_sum(h == 0 ? mterm : 0.f), sk = wave_sum(h == 0 ? kl : 0.f);
+        const float sm_ = ml_wave_sum(q == 0 ? mterm : 0.f), sk = ml_wave_sum(q == 0 ? kl : 0.f);
         if (lane == 0) {
           SCP[w][0] = sm_;
           SCP[w][1] = sk;
         }
       }
+#pragma unroll
+      for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          D3I[(16 * T3 + 4 * q + i) * RS + col] = d3r[T3][i];
+          const float s = ml_row16_sum(d3r[T3][i]);  // b3's gradient over this wave's samples
+          if (n == 0) BP[w][H2 + 16 * T3 + 4 * q + i] = s;
+        }
     }
-    if constexpr (H2 == 64) __syncthreads();  // dz2 block (hb, sb) reads sample block sb's D3L
-    else asm volatile("" ::: "memory");
-    // ---- dz2 = (W3^T dz3) * (1 - h2^2), block (hb, sb)
-    if (l2w) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const float* pa = W3 + h * SW3 + 32 * hb + l32;
-      const float* pb = D3L + h * S + 32 * sb + l32;
-#pragma unroll
-      for (int ks = 0; ks < C::NKS3; ++ks) acc = ml_mfma(pa[2 * ks * SW3], pb[2 * ks * S], acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) D2L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = acc[r] * (1.f - h2r[r] * h2r[r]);
-    }
-    __syncthreads();
     SPP_TP(2);
-    // ---- dz1 = (W2^T dz2) * (1 - h1^2), block (hb, sb)
+    // ---- dz2 = (W3^T dz3) * (1 - h2^2); k-step (T3, j) = output 16 T3 + 4q + j
+    f32x4 d2r[NB2];
     {
-      f32x16 acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const float* pa = W2 + h * S + 32 * hb + l32;
-      const float* pb = D2L + h * S + 32 * sb + l32;
-#pragma unroll 8
-      for (int ks = 0; ks < H2 / 2; ++ks) acc = ml_mfma(pa[2 * ks * S], pb[2 * ks * S], acc);
+      for (int T2 = 0; T2 < NB2; ++T2) d2r[T2] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) D1L[(32 * hb + ml_ru(r) + 4 * h) * S + 32 * sb + l32] = acc[r] * (1.f - h1r[r] * h1r[r]);
+      for (int T3 = 0; T3 < NO; ++T3)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int T2 = 0; T2 < NB2; ++T2)
+            d2r[T2] = ml_mfma16(W3[(16 * T3 + 4 * q + j) * SW3 + 16 * T2 + n], d3r[T3][j], d2r[T2]);
+#pragma unroll
+      for (int T2 = 0; T2 < NB2; ++T2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          d2r[T2][i] *= 1.f - h2r[T2][i] * h2r[T2][i];
+          D2I[(16 * T2 + 4 * q + i) * RS + col] = d2r[T2][i];
+          const float s = ml_row16_sum(d2r[T2][i]);  // b2's gradient over this wave's samples
+          if (n == 0) BP[w][16 * T2 + 4 * q + i] = s;
+        }
     }
-    __syncthreads();
+    // ---- dz1 = (W2^T dz2) * (1 - h1^2)
+    {
+      f32x4 acc[4];
+#pragma unroll
+      for (int T = 0; T < 4; ++T) acc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int T2 = 0; T2 < NB2; ++T2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int T = 0; T < 4; ++T)
+            acc[T] = ml_mfma16(W2[(16 * T2 + 4 * q + j) * SW2 + 16 * T + n], d2r[T2][j], acc[T]);
+#pragma unroll
+      for (int T = 0; T < 4; ++T)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) D1I[(16 * T + 4 * q + i) * RS + col] = acc[T][i] * (1.f - h1r[T][i] * h1r[T][i]);
+    }
+    __syncthreads();  // the images hold all 64 samples
     SPP_TP(3);
-    // ---- weight-gradient tiles over the 64 samples: tile q = w + 4k
-    f32x16 gt[C::TPW];
+    // ---- weight gradients: 16x16 tiles over the 64 samples (k-step ks of lane group q = sample 16q + ks),
+    // tiles w, w + 4, ... of this wave two at a time; each finished tile goes to GR in canonical order
+    auto tile_rows = [&](int tt, const float*& ar, const float*& br, int& layer, int& mt, int& nt) {
+      if (tt < C::NT1) {
+        layer = 0; mt = tt / C::NIT1; nt = tt - mt * C::NIT1;
+        ar = D1I; br = XT;
+      } else if (tt < C::NT1 + C::NT2) {
+        const int p = tt - C::NT1;
+        layer = 1; mt = p >> 2; nt = p & 3;
+        ar = D2I; br = H1I;
+      } else {
+        const int p = tt - C::NT1 - C::NT2;
+        layer = 2; mt = p / NB2; nt = p - mt * NB2;
+        ar = D3I; br = H2I;
+      }
+      ar += (16 * mt + n) * RS + 16 * q;
+      br += (16 * nt + n) * RS + 16 * q;
+    };
+    auto tile_store = [&](const f32x4& acc, int layer, int mt, int nt) {
 #pragma unroll
-    for (int k = 0; k < C::TPW; ++k) {
-      const int q = w + 4 * k;
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * mt + 4 * q + i, cu = 16 * nt + n;
+        int c = -1;
+        if (layer == 0) c = cu < IN ? C::O_W1 + row * IN + cu : (cu == IN ? C::O_B1 + row : -1);
+        else if (layer == 1) c = C::O_W2 + row * 64 + cu;
+        else c = row < OUT ? C::O_W3 + row * H2 + cu : -1;
+        if (c >= 0) GR[c] = acc[i];
+      }
+    };
+    for (int tt = w; tt < C::NT; tt += 8) {  // (wave-uniform; a missing second tile repeats the first, unstored)
+      const bool two = tt + 4 < C::NT;
+      const float *a0, *b0, *a1, *b1;
+      int l0, m0, n0, l1, m1, n1;
+      tile_rows(tt, a0, b0, l0, m0, n0);
+      tile_rows(two ? tt + 4 : tt, a1, b1, l1, m1, n1);
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      float4 x0 = reinterpret_cast<const float4*>(a0)[0], y0 = reinterpret_cast<const float4*>(b0)[0];
+      float4 x1 = reinterpret_cast<const float4*>(a1)[0], y1 = reinterpret_cast<const float4*>(b1)[0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) gt[k][r] = 0.f;
-      if (q < C::NTILE) {
-        int layer, rr, cc;
-        ml_tile<C>(q, layer, rr, cc);
-        if (layer == 0) {
-          const float* pa = D1L + (rr + l32) * S + h;
-          const float* pb = X + h * SX + cc + l32;
-#pragma unroll 8
-          for (int ks = 0; ks < 32; ++ks) gt[k] = ml_mfma(pa[2 * ks], pb[2 * ks * SX], gt[k]);
-        } else {
-          const float* pa = layer == 1 ? D2L + (rr + l32) * S + h : D3L + l32 * S + h;
-          const float* pb = (layer == 1 ? H1L : H2L) + (cc + l32) * S + h;
-#pragma unroll 8
-          for (int ks = 0; ks < 32; ++ks) gt[k] = ml_mfma(pa[2 * ks], pb[2 * ks], gt[k]);
+      for (int cq = 0; cq < 4; ++cq) {
+        float4 nx0, ny0, nx1, ny1;
+        if (cq < 3) {  // the next 4 samples' operands in flight under this group's MFMAs
+          nx0 = reinterpret_cast<const float4*>(a0)[cq + 1];
+          ny0 = reinterpret_cast<const float4*>(b0)[cq + 1];
+          nx1 = reinterpret_cast<const float4*>(a1)[cq + 1];
+          ny1 = reinterpret_cast<const float4*>(b1)[cq + 1];
+        }
+        c0 = ml_mfma16(x0.x, y0.x, c0);
+        c1 = ml_mfma16(x1.x, y1.x, c1);
+        c0 = ml_mfma16(x0.y, y0.y, c0);
+        c1 = ml_mfma16(x1.y, y1.y, c1);
+        c0 = ml_mfma16(x0.z, y0.z, c0);
+        c1 = ml_mfma16(x1.z, y1.z, c1);
+        c0 = ml_mfma16(x0.w, y0.w, c0);
+        c1 = ml_mfma16(x1.w, y1.w, c1);
+        if (cq < 3) {
+          x0 = nx0; y0 = ny0; x1 = nx1; y1 = ny1;
         }
       }
+      tile_store(c0, l0, m0, n0);
+      if (two) tile_store(c1, l1, m1, n1);
     }
-    // b2 / b3 (and log_scale) gradients: row sums over the 64 samples
-    float bg = 0.f;
-    {
-      const float* row = t < H2 ? D2L + t * S : (t < H2 + OUT ? D3L + (t - H2) * S : LSL + (t - H2 - OUT) * S);
-      if (t < H2 + OUT * (HEAD ? 2 : 1)) {
-#pragma unroll 16
-        for (int s2 = 0; s2 < R; ++s2) bg += row[s2];
-      }
-      if (HEAD && g == 0 && t >= H2 + OUT && t < H2 + 2 * OUT) bg -= a.ent_coef;  // - ent_coef * d entropy / d ls
-    }
-    __syncthreads();  // every read of the activations is done: H1L | D1L becomes the gradient staging area
     SPP_TP(4);
-    // ---- the step's gradient in canonical order -> GR[0 .. NP), scalars -> GR[NP ..]
-#pragma unroll
-    for (int k = 0; k < C::TPW; ++k) {
-      const int q = w + 4 * k;
-      if (q < C::NTILE) {
-        int layer, rr, cc;
-        ml_tile<C>(q, layer, rr, cc);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = rr + ml_ru(e) + 4 * h, col = cc + l32;
-          int c = -1;
-          if (layer == 0) c = col < IN ? C::O_W1 + row * IN + col : (col == IN ? C::O_B1 + row : -1);
-          else if (layer == 1) c = C::O_W2 + row * 64 + col;
-          else c = row < OUT ? C::O_W3 + row * H2 + col : -1;
-          if (c >= 0) GR[c] = gt[k][e];
-        }
+    // ---- bias (and log_scale) gradients: the waves' partials in a fixed order; scalars -> GR[O_SC ..]
+    {
+      auto wsum = [&](int j) { return ((BP[0][j] + BP[1][j]) + BP[2][j]) + BP[3][j]; };
+      if (t < H2) GR[C::O_B2 + t] = wsum(t);
+      else if (t < H2 + OUT) GR[C::O_B3 + t - H2] = wsum(t);
+      else if (HEAD && t >= 128 && t < 128 + OUT) {  // - ent_coef * d entropy / d log_scale (once: workgroup 0)
+        const int u = t - 128;
+        const float s = wsum(H2 + 16 * NO + u);
+        GR[u] = (g == 0) ? s - a.ent_coef : s;
       }
     }
-    if (t < H2) GR[C::O_B2 + t] = bg;
-    else if (t < H2 + OUT) GR[C::O_B3 + t - H2] = bg;
-    else if (HEAD && t < H2 + 2 * OUT) GR[t - H2 - OUT] = bg;
-    if (t < 4) GR[C::O_SC + t] = t == 0 ? SCP[0][0] + SCP[1][0] : (HEAD && t == 1 ? SCP[0][1] + SCP[1][1] : 0.f);
+    if (t < 4) GR[C::O_SC + t] = t == 0 ? ((SCP[0][0] + SCP[1][0]) + SCP[2][0]) + SCP[3][0]
+                                        : (HEAD && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f);
     if constexpr (HEAD) {  // the dist partials of every thread (this step's rows)
-      const float ds = wave_sum(dist_step);
+      const float ds = ml_wave_sum(dist_step);
       if (lane == 0) SCP[w][2] = ds;
     }
-    if (t < C::O_SC - NP) GR[NP + t] = 0.f;
+    if (t >= 192 && t - 192 < C::O_SC - NP) GR[NP + t - 192] = 0.f;
     __syncthreads();
     if constexpr (HEAD) {
-      if (t == 0) GR[C::O_SC + 2] = SCP[0][2] + SCP[1][2] + SCP[2][2] + SCP[3][2];
+      if (t == 0) GR[C::O_SC + 2] = ((SCP[0][2] + SCP[1][2]) + SCP[2][2]) + SCP[3][2];
       __syncthreads();
     }
     // ---- exchange (G > 1) and Adam on this workgroup's shard
@@ -490,7 +598,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         slab_st4(mine, 4 * f, v4);
       }
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead);
-      // this shard's chunk of every slab -> the alias, [q][c4n] (G > 1: the staged gradient is dead)
+      // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
       const int nit = c4n * G;
       for (int i0 = 0; i0 < nit; i0 += C::RLC * kMlTH) {  // (G = 17, 64-wide AcM: one round)
         float4 ld[C::RLC];
@@ -498,14 +606,14 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         for (int k = 0; k < C::RLC; ++k) {
           const int i = i0 + t + kMlTH * k;
           if (i < nit) {
-            const int q = i / c4n;
-            ld[k] = slab_ld4(all, q * C::SLAB + 4 * (f0 + i - q * c4n));
+            const int p = i / c4n;
+            ld[k] = slab_ld4(all, p * C::SLAB + 4 * (f0 + i - p * c4n));
           }
         }
 #pragma unroll
         for (int k = 0; k < C::RLC; ++k) {
           const int i = i0 + t + kMlTH * k;
-          if (i < nit) reinterpret_cast<float4*>(H1D1)[i] = ld[k];
+          if (i < nit) reinterpret_cast<float4*>(IMG)[i] = ld[k];
         }
       }
       __syncthreads();
@@ -521,10 +629,10 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       if (f < f1) {
         float4 gg4;
         if constexpr (MW) {
-          const float4* red = reinterpret_cast<const float4*>(H1D1) + (f - f0);
+          const float4* red = reinterpret_cast<const float4*>(IMG) + (f - f0);
           gg4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int q = 0; q < G; ++q) {
-            const float4 x4 = red[q * c4n];
+          for (int p = 0; p < G; ++p) {
+            const float4 x4 = red[p * c4n];
             gg4.x += x4.x; gg4.y += x4.y; gg4.z += x4.z; gg4.w += x4.w;
           }
         } else {
@@ -558,6 +666,9 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       }
     }
     if (HEAD && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
+    // the next step's rows into LDS while the other workgroups publish (XT, Y, LPO, ADV: last read by this
+    // step's head and dW tiles, before the gradient staging barrier)
+    stage(st + 1);
     SPP_TP(7);
     if constexpr (MW) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead);

@@ -53,6 +53,13 @@ sppStatus sppMTDestroy(sppMTHandle h);
 sppStatus sppRandNormal(float* out_dev, int64_t n, uint64_t seed, uint64_t offset, void* stream);
 sppStatus sppRandIndex(int64_t* out_dev, int64_t n, int64_t high, uint64_t seed, uint64_t offset,
                        void* stream);
+/* Uniform random permutation of [0, n) on the device (the shuffle of a DataLoader(shuffle=True) epoch:
+ * acm/acm.py:275, acm/on_policy.py:176-190): 64-bit Philox keys (counters offset + i), stable radix sort of
+ * (key, index); out_dev [n] = the sorted indices.  scratch: device bytes >= sppRandPermScratchBytes(n).
+ * Stream-ordered, no host synchronisation (replaces torch.randperm on the device). */
+int64_t sppRandPermScratchBytes(int64_t n);
+sppStatus sppRandPerm(int64_t* out_dev, int64_t n, uint64_t seed, uint64_t offset, void* scratch_dev,
+                      int64_t scratch_bytes, void* stream);
 
 /* ------------------------------------------------------------------ replay ring
  * BufferAcMOffPolicy (rltoolkit/buffer/replay_buffer.py:303-401) with the
@@ -444,8 +451,18 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act
                            float* out4, void* stream);
 /* Largest bs sppOnpActorEpoch accepts on this device (0: no instantiation for the handle's dims). */
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);
-/* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch launch timed out at an arrival barrier, else 0. */
+/* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch / sppOnpCriticSteps launch timed out at an arrival
+ * barrier, else 0. */
 sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
+/* A2C.update_critic's inner loop (rltoolkit/algorithms/a2c/a2c.py:186-225): nsteps sequential full-batch
+ * steps of 0.5 * mean((q - V(x))^2) + Adam at critic_lr on the same N rows (x [N][ob] normalised obs, q [N]
+ * targets), in ONE launch: every workgroup runs ceil(rows / 64) passes of its share of the N rows, the
+ * gradient is summed over the workgroups in a fixed order (deterministic), parameters stay in LDS.
+ * loss_sum += sum over the steps of each step's loss.  Single-process only (data-parallel ranks all-reduce
+ * each step: sppOnpCriticGrads / Apply).  N <= sppOnpCriticStepsMaxBatch; ob 17 and 11 instantiated. */
+sppStatus sppOnpCriticSteps(sppOnPolicyHandle h, const float* x, const float* q, int N, int nsteps, float* loss_sum,
+                            void* stream);
+int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle h);
 /* Actor.act (basic_model.py:32-51) continuous: a = mu + exp(log_scale) * eps (eps NULL:
  * deterministic mu), logp = Independent(Normal).log_prob(a). */
 sppStatus sppOnpAct(sppOnPolicyHandle h, const float* x, int N, const float* eps, float* act_out, float* logp_out,

@@ -6,7 +6,7 @@ Networks (rltoolkit/basic_model.py:7-76), flat buffers in state_dict order:
   Critic:             fc1 ob->64, fc2 64->64, fc3 64->1 (tanh hidden)
 Steps:
   critic_step   A2C.update_critic inner step (rltoolkit/algorithms/a2c/a2c.py:209-219):
-                loss = 0.5 * mean((q - V(x))^2)
+                loss = 0.5 * mean((q - V(x))^2); critic_steps: nsteps of them with Adam
   actor_step    PPO.update_actor / PPO_AcM.update_actor_acm minibatch body
                 (algorithms/ppo/ppo.py:174-190, acm/on_policy.py:189-205):
                 loss = clip_loss(lp_old, lp_new, A) - entropy_coef * entropy
@@ -71,6 +71,21 @@ def critic_step(flat, ob, x, q, dtype=torch.float32):
     adv = torch.as_tensor(q, dtype=dtype) - v
     loss = 0.5 * adv.pow(2).mean()
     return loss.item(), _flat(torch.autograd.grad(loss, list(p.values())))
+
+
+def critic_steps(flat, ob, x, q, lr, nsteps, dtype=torch.float32):
+    """A2C.update_critic's inner loop for one target (a2c.py:209-219): nsteps full-batch Adam steps on
+    0.5 * mean((q - V(x))^2) over the same rows.  Returns (flat, per-step losses)."""
+    from oracle.adam import OracleAdam
+
+    p = torch.from_numpy(np.array(flat, np.float64 if dtype == torch.float64 else np.float32, copy=True))
+    opt = OracleAdam([p], lr)
+    losses = []
+    for _ in range(nsteps):
+        loss, g = critic_step(p.numpy(), ob, x, q, dtype=dtype)
+        opt.step([torch.from_numpy(g)])
+        losses.append(loss)
+    return p.numpy(), losses
 
 
 def actor_step(flat, ob, aout, lim, x, act, lp_old, adv, eps_clip=0.2, entropy_coef=0.0, next_obs=None):

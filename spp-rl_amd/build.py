@@ -111,6 +111,8 @@ SCRATCH_ALLOWED = {
     # the ACM regression kernels: 8 bytes of SGPR-spill staging, no VGPR spills
     "k_acm_regress": 8,
     "k_bacm_regress": 8,
+    # rocprim's onesweep radix sort (ks_perm.hip, sppRandPerm): a 48-byte private array, no VGPR spills
+    "radix_sort_onesweep": 48,
 }
 
 

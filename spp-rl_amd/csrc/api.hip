@@ -2163,6 +2163,7 @@ struct sppOnPolicy {
   DevArray<float> sgd_slab;
   DevArray<int> sgd_sync;
   int sgd_max_wg = -1;
+  int crit_max_wg = -1;  // co-resident persistent-critic workgroups (onp_critic_max_wg, cached)
 };
 
 static sppStatus onp_packs(sppOnPolicy* o) {
@@ -2485,6 +2486,60 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
   else SPP_EPOCH_LAUNCH(11);
 #undef SPP_EPOCH_LAUNCH
   o->steps[0] += nsteps;
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+// persistent critic steps (HEAD 2): co-resident workgroups, passes of 64 rows per workgroup and step
+constexpr int kCriticMaxPasses = 8;
+static int onp_critic_max_wg(sppOnPolicy* o) {
+  if (o->crit_max_wg >= 0) return o->crit_max_wg;
+  const int ob = o->cfg.ob;
+  int n = 0;
+  if (ob == 17) n = mlp_sgd_max_wg<17, 64, 1, 2>(o->num_cu);
+  else if (ob == 11) n = mlp_sgd_max_wg<11, 64, 1, 2>(o->num_cu);
+  o->crit_max_wg = n;
+  return n;
+}
+
+int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle o) {
+  if (!o) return 0;
+  return kMlR * kCriticMaxPasses * onp_critic_max_wg(o);
+}
+
+sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
+                            void* stream) {
+  SPP_REQUIRE(o && x && q && loss_sum && N > 0 && nsteps >= 0, SPP_E_INVALID_ARG, "critic steps: bad args");
+  SPP_REQUIRE(o->net[1].p && o->net[1].m && o->net[1].v && o->lim.ptr, SPP_E_STATE, "critic steps: critic not bound");
+  const int maxwg = onp_critic_max_wg(o);
+  SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "critic steps: no instantiation for ob=%d", o->cfg.ob);
+  // fewest passes per workgroup the co-resident grid allows, then the fewest workgroups for that many passes
+  const int tiles = cdiv(N, kMlR), passes = cdiv(tiles, maxwg), nwg = cdiv(tiles, passes);
+  SPP_REQUIRE(passes <= kCriticMaxPasses, SPP_E_SHAPE, "critic steps: batch %d > %d", N, kMlR * kCriticMaxPasses * maxwg);
+  if (nsteps == 0) return SPP_OK;
+  hipStream_t st = S(stream);
+  MlpSgdArgs g{};
+  g.x = x; g.y = q; g.nsteps = nsteps; g.bs = N; g.bsl = N; g.bs_last = N;
+  const NetBufs& n = o->net[1];
+  g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.critic_lr; g.step0 = o->steps[1];
+  g.lim = o->lim.ptr; g.loss_sum = loss_sum;
+  if (nwg > 1) {
+    g.bsl = cdiv(N, nwg);
+    sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
+    if (s) return s;
+    g.slab = o->sgd_slab.ptr;
+    g.pbuf = o->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
+    g.ctr = o->sgd_sync.ptr;
+    g.err = o->sgd_sync.ptr + 1;
+  }
+  const bool mw = nwg > 1;
+#define SPP_CRITIC_LAUNCH(OB_)                                                                        \
+  if (mw) hipLaunchKernelGGL((k_mlp_sgd<OB_, 64, 1, 2, true>), dim3(nwg), dim3(kMlTH), 0, st, g);     \
+  else hipLaunchKernelGGL((k_mlp_sgd<OB_, 64, 1, 2, false>), dim3(1), dim3(kMlTH), 0, st, g)
+  if (o->cfg.ob == 17) SPP_CRITIC_LAUNCH(17);
+  else SPP_CRITIC_LAUNCH(11);
+#undef SPP_CRITIC_LAUNCH
+  o->steps[1] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

@@ -1,0 +1,63 @@
+// Device random permutation of [0, n): the shuffle of a DataLoader(shuffle=True) epoch
+// (rltoolkit/acm/acm.py:275 for update_acm, acm/on_policy.py:176-190 / algorithms/ppo/ppo.py:174-188 for the
+// PPO minibatch epochs) drawn on the device: one 64-bit Philox4x32-10 key per index (counter = offset + i under
+// the caller's seed), then a stable LSD radix sort of (key, index) pairs; the permutation is the sorted index
+// column.  torch.randperm on the device stalls the stream for 0.3-0.7 ms of host-side work per call (merge /
+// duplicate-key passes between launches, measured in the PPO kernel trace); this is two launches and a sort
+// with no host round trip.  Deterministic for a (seed, offset); not the reference's CPU generator stream
+// (its permutation values are never reproduced: DESIGN.md §2).
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.h"
+#include "spprl.h"
+
+namespace spp {
+
+__global__ void k_perm_keys(uint64_t* keys, int64_t* idx, int64_t n, uint64_t seed, uint64_t offset) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const u32x4 r = philox(seed, 0x5045524dULL, offset + (uint64_t)i);  // "PERM" stream of the seed
+    keys[i] = ((uint64_t)r.x << 32) | r.y;
+    idx[i] = i;
+  }
+}
+
+static size_t perm_sort_bytes(int64_t n) {
+  size_t bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const int64_t*)nullptr,
+                            (int64_t*)nullptr, (size_t)n, 0, 64, (hipStream_t)0, false);
+  return bytes;
+}
+
+}  // namespace spp
+
+using namespace spp;
+
+extern "C" {
+
+// scratch layout: keys_in [n] u64 | keys_out [n] u64 | idx_in [n] i64 | the sort's temporary storage
+int64_t sppRandPermScratchBytes(int64_t n) {
+  if (n <= 0) return 0;
+  return (int64_t)(3 * (size_t)n * 8 + ((perm_sort_bytes(n) + 255) / 256) * 256);
+}
+
+sppStatus sppRandPerm(int64_t* out, int64_t n, uint64_t seed, uint64_t offset, void* scratch, int64_t scratch_bytes,
+                      void* stream) {
+  if (n == 0) return SPP_OK;
+  if (!out || n < 0 || !scratch || scratch_bytes < sppRandPermScratchBytes(n)) return SPP_E_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  char* base = static_cast<char*>(scratch);
+  uint64_t* keys_in = reinterpret_cast<uint64_t*>(base);
+  uint64_t* keys_out = keys_in + n;
+  int64_t* idx_in = reinterpret_cast<int64_t*>(keys_out + n);
+  void* tmp = idx_in + n;
+  size_t tmp_bytes = (size_t)scratch_bytes - 3 * (size_t)n * 8;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_perm_keys, dim3((unsigned)blocks), dim3(256), 0, st, keys_in, idx_in, n, seed, offset);
+  if (hipGetLastError() != hipSuccess) return SPP_E_HIP;
+  if (rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, idx_in, out, (size_t)n, 0, 64, st, false) !=
+      hipSuccess)
+    return SPP_E_HIP;
+  return hipGetLastError() == hipSuccess ? SPP_OK : SPP_E_HIP;
+}
+
+}  // extern "C"

@@ -6,6 +6,10 @@
 //           Gaussian Actor of basic_model.py:7-51): IN -> 64 -> 64 (tanh) -> OUT, mu = tanh(fc3) * lim,
 //           log_prob of the stored actions under Normal(mu, exp(log_scale)), clip loss - ent_coef * entropy;
 //           rows gathered through the epoch's permutation; per step {actor loss, KL, dist, entropy} out.
+//   HEAD 2  A2C.update_critic's full-batch steps (a2c.py:186-225; the Critic of basic_model.py:55-76):
+//           IN -> 64 -> 64 (tanh) -> 1 (linear), loss = 0.5 mean((q - V)^2); x / q rows contiguous.  A step's
+//           rows may exceed 64 per workgroup: each workgroup runs ceil(rows / 64) passes of 64 and adds the
+//           passes' gradients before the exchange.
 //
 // One step of bs rows runs on G = ceil(bs / 64) workgroups of 4 waves; wave w owns 16 of the workgroup's 64
 // rows (image column 16 w + n, n = lane & 15) through every layer.  Forward and backward are
@@ -41,8 +45,9 @@ constexpr int kMlSlabMax = 8192;  // slab floats per workgroup (>= MlCfg::SLAB)
 
 struct MlpSgdArgs {
   // rows
-  const float* x;        // HEAD 0: [nsteps * bs][IN] contiguous; HEAD 1: normalised obs [n][IN] (through idx)
-  const float* y;        // HEAD 0: targets [nsteps * bs][OUT]; HEAD 1: actions [n][OUT]
+  const float* x;        // HEAD 0: [nsteps * bs][IN] contiguous; HEAD 1: normalised obs [n][IN] (through idx);
+                         // HEAD 2: [bs][IN], the same full batch every step (bs_last = bs)
+  const float* y;        // HEAD 0: targets [nsteps * bs][OUT]; HEAD 1: actions [n][OUT]; HEAD 2: q [bs]
   const float* nxt;      // HEAD 1: next obs [n][OUT] (the dist loss, data only)
   const float* lp_old;   // HEAD 1: [n]
   const float* adv;      // HEAD 1: normalised advantages [n]
@@ -56,7 +61,7 @@ struct MlpSgdArgs {
   int64_t step0;         // Adam steps already taken
   const float* lim;      // [OUT]
   float eps_clip, ent_coef;
-  float* loss_sum;       // HEAD 0: += sum over steps of the batch loss
+  float* loss_sum;       // HEAD 0 / 2: += sum over steps of the batch loss
   float* out;            // HEAD 1: [nsteps][4] actor loss, KL, dist, entropy
   float* slab;           // G > 1: [2][G][slab floats] gradient slabs (step parity)
   float* pbuf;           // G > 1: [param floats] the new parameters of each step
@@ -78,9 +83,9 @@ struct MlCfg {
   static constexpr int SW3 = H2 + 4;               // W3 row stride
   static constexpr int NT1 = 4 * NIT1, NT2 = NB2 * 4, NT3 = NO * NB2, NT = NT1 + NT2 + NT3;  // dW tiles
   static constexpr int IMGR = 128 + 2 * H2 + 16 * NO;  // image rows: H1, D1, H2, D2, D3
-  static constexpr int NBP = H2 + 16 * NO + (HEAD ? 16 * NO : 0);  // per-wave bias partials: b2, b3 (, ls)
+  static constexpr int NBP = H2 + 16 * NO + (HEAD == 1 ? 16 * NO : 0);  // per-wave bias partials: b2, b3 (, ls)
   // canonical layout: [log_scale (HEAD 1)] fc1.weight fc1.bias fc2.weight fc2.bias fc3.weight fc3.bias
-  static constexpr int O_W1 = HEAD ? OUT : 0;
+  static constexpr int O_W1 = HEAD == 1 ? OUT : 0;
   static constexpr int O_B1 = O_W1 + 64 * IN;
   static constexpr int O_W2 = O_B1 + 64;
   static constexpr int O_B2 = O_W2 + H2 * 64;
@@ -98,7 +103,7 @@ struct MlCfg {
   // G > 1: the shard's G slab chunks are staged in the image region, at most NP4 + G - 1 float4
   static constexpr int RED4 = IMGR * kMlRS / 4;
   static constexpr int MAXG = RED4 - NP4 + 1 < kMlMaxWG ? RED4 - NP4 + 1 : kMlMaxWG;
-  static constexpr int RLC = HEAD ? 4 : 8;  // slab float4 loads in flight per thread (register budget)
+  static constexpr int RLC = HEAD == 1 ? 4 : 8;  // slab float4 loads in flight per thread (register budget)
   static constexpr int NL = (NP4 + kMlTH - 1) / kMlTH;   // reloaded float4 per thread
 };
 
@@ -147,6 +152,8 @@ __device__ __forceinline__ float ml_wave_sum(float v) {
 template <int IN, int H2, int OUT, int HEAD, bool MW>
 __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   using C = MlCfg<IN, H2, OUT, HEAD>;
+  constexpr bool GAUSS = HEAD == 1, VALUE = HEAD == 2;
+  static_assert(!VALUE || OUT == 1, "value head");
   constexpr int RS = kMlRS, R = kMlR, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
                 NO = C::NO;
   __shared__ __attribute__((aligned(16))) float IMG[C::IMGR * RS];  // H1 | D1 | H2 | D2 | D3; G > 1: the slab chunks
@@ -157,8 +164,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   __shared__ __attribute__((aligned(16))) float W3[16 * NO * SW3];  // rows >= OUT zero
   __shared__ float B2[H2], B3[16 * NO], LS[32], LIM[32];
   __shared__ float Y[R * OUT];
-  __shared__ float LPO[HEAD ? R : 1], ADV[HEAD ? R : 1];
-  __shared__ int64_t IDX[HEAD ? 2 * R : 1];
+  __shared__ float LPO[GAUSS ? R : 1], ADV[GAUSS ? R : 1];
+  __shared__ int64_t IDX[GAUSS ? 2 * R : 1];
   __shared__ float BP[4][C::NBP];   // per wave: bias (and log_scale) gradient partials over its 16 samples
   __shared__ float SCP[4][4];       // per wave: scalar partials
   __shared__ float adam_s[2][2];
@@ -174,18 +181,24 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   const int G = MW ? (int)gridDim.x : 1, g = MW ? (int)blockIdx.x : 0;
   const int r0 = MW ? g * a.bsl : 0;
   auto step_rows = [&](int st) { return st == a.nsteps - 1 ? a.bs_last : a.bs; };  // the step's batch
-  auto wg_rows = [&](int st) {  // this workgroup's rows of step st (<= 64)
+  auto wg_rows = [&](int st) {  // this workgroup's rows of step st
     return MW ? max(0, min(a.bsl, step_rows(st) - r0)) : step_rows(st);
+  };
+  // passes of <= 64 rows: pass p = step p / nsub, rows [64 (p % nsub), +64) of the workgroup's rows
+  const int nsub = (MW && VALUE) ? (a.bsl + R - 1) / R : 1;  // (HEAD 0 / 1: one pass; the host keeps bsl <= 64)
+  auto pass_rows = [&](int p) {
+    const int st = p / nsub;
+    return st < a.nsteps ? max(0, min(R, wg_rows(st) - R * (p - st * nsub))) : 0;
   };
   if (t == 0) s_dead = 0;
   // ---- the canonical element c (< NP) of the parameters inside the LDS images
   auto pref = [&](int c) -> float& {
-    if (HEAD && c < C::O_W1) return LS[c];
-    if (c < C::O_B1) { const int p = c - C::O_W1; return W1[(p / IN) * SW1 + p % IN]; }
+    if (GAUSS && c < C::O_W1) return LS[c];
+    if (c < C::O_B1) { const int e = c - C::O_W1; return W1[(e / IN) * SW1 + e % IN]; }
     if (c < C::O_W2) return W1[(c - C::O_B1) * SW1 + IN];
-    if (c < C::O_B2) { const int p = c - C::O_W2; return W2[(p >> 6) * SW2 + (p & 63)]; }
+    if (c < C::O_B2) { const int e = c - C::O_W2; return W2[(e >> 6) * SW2 + (e & 63)]; }
     if (c < C::O_W3) return B2[c - C::O_B2];
-    if (c < C::O_B3) { const int p = c - C::O_W3; return W3[(p / H2) * SW3 + p % H2]; }
+    if (c < C::O_B3) { const int e = c - C::O_W3; return W3[(e / H2) * SW3 + e % H2]; }
     return B3[c - C::O_B3];
   };
   // ---- images (zero padding)
@@ -227,54 +240,57 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     adam_s[st & 1][0] = (float)(-((double)a.lr / (1.0 - pw1)));
     adam_s[st & 1][1] = (float)sqrt(1.0 - pw2);
   };
-  // ---- register prefetch of one step's rows (HEAD 1: through the step's indices in IDX)
+  // ---- register prefetch of one pass's rows (HEAD 1: through the step's indices in IDX)
   float xp[C::NXP], yp[C::NYP], lpp = 0.f, advp = 0.f, dsum = 0.f;
-  auto row_of = [&](int st, int r) -> int64_t {
-    if constexpr (HEAD) return IDX[(st & 1) * R + r];
-    else return (int64_t)st * a.bs + r0 + r;
+  auto row_of = [&](int p, int r) -> int64_t {
+    if constexpr (GAUSS) return IDX[(p & 1) * R + r];
+    else {
+      const int st = p / nsub;
+      return (VALUE ? 0 : (int64_t)st * a.bs) + r0 + R * (p - st * nsub) + r;  // (HEAD 2: the same batch)
+    }
   };
-  auto prefetch = [&](int st) {
-    const bool live = st < a.nsteps;
-    const int bs = wg_rows(st);
+  auto prefetch = [&](int p) {
+    const int bs = pass_rows(p);
+    const bool live = bs > 0;
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
       const int i = t + kMlTH * k, r = i / IN;
-      xp[k] = (live && i < bs * IN) ? a.x[row_of(st, r) * IN + i % IN] : 0.f;
+      xp[k] = (live && i < bs * IN) ? a.x[row_of(p, r) * IN + i % IN] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < C::NYP; ++k) {
       const int i = t + kMlTH * k, r = i / OUT;
       const bool ok = live && i < bs * OUT;
-      yp[k] = ok ? a.y[row_of(st, r) * OUT + i % OUT] : 0.f;
-      if constexpr (HEAD) {  // the dist loss is data only: its per-step sum is taken here
-        const float e = ok ? yp[k] - a.nxt[row_of(st, r) * OUT + i % OUT] : 0.f;
+      yp[k] = ok ? a.y[row_of(p, r) * OUT + i % OUT] : 0.f;
+      if constexpr (GAUSS) {  // the dist loss is data only: its per-step sum is taken here
+        const float e = ok ? yp[k] - a.nxt[row_of(p, r) * OUT + i % OUT] : 0.f;
         dsum = fmaf(e, e, dsum);
       }
     }
-    if constexpr (HEAD) {
-      lpp = (live && t < bs) ? a.lp_old[row_of(st, t)] : 0.f;
-      advp = (live && t < bs) ? a.adv[row_of(st, t)] : 0.f;
+    if constexpr (GAUSS) {
+      lpp = (live && t < bs) ? a.lp_old[row_of(p, t)] : 0.f;
+      advp = (live && t < bs) ? a.adv[row_of(p, t)] : 0.f;
     }
   };
-  auto load_idx = [&](int st) {  // HEAD 1: step st's row indices -> IDX[st & 1]
-    if constexpr (HEAD)
-      if (t < R) IDX[(st & 1) * R + t] = (st < a.nsteps && t < wg_rows(st)) ? a.idx[(int64_t)st * a.bs + r0 + t] : 0;
+  auto load_idx = [&](int p) {  // HEAD 1 (one pass per step): step p's row indices -> IDX[p & 1]
+    if constexpr (GAUSS)
+      if (t < R) IDX[(p & 1) * R + t] = t < pass_rows(p) ? a.idx[(int64_t)p * a.bs + r0 + t] : 0;
   };
   // ---- a prefetched step's rows into LDS: inputs transposed (rows >= bs: zeros), the constant-1 row
   float dist_next = 0.f;
-  auto stage = [&](int st) {
+  auto stage = [&](int p) {
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
       const int i = t + kMlTH * k;
       if (i < R * IN) XT[(i % IN) * RS + i / IN] = xp[k];
     }
-    if (t < R) XT[IN * RS + t] = t < wg_rows(st) ? 1.f : 0.f;
+    if (t < R) XT[IN * RS + t] = t < pass_rows(p) ? 1.f : 0.f;
 #pragma unroll
     for (int k = 0; k < C::NYP; ++k) {
       const int i = t + kMlTH * k;
       if (i < R * OUT) Y[i] = yp[k];
     }
-    if constexpr (HEAD) {
+    if constexpr (GAUSS) {
       if (t < R) {
         LPO[t] = lpp;
         ADV[t] = advp;
@@ -291,16 +307,21 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   stage(0);
   __syncthreads();
   SPP_TP_INIT();
-  float loss_acc = 0.f;  // HEAD 0: sum over steps of the batch loss (the scalar slot's owner)
+  float loss_acc = 0.f;  // HEAD 0 / 2: sum over steps of the batch loss (the scalar slot's owner)
   const float lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
+  int p = 0;  // pass
   for (int st = 0; st < a.nsteps; ++st) {
-    const int bsg = step_rows(st), bs = wg_rows(st);
+    const int bsg = step_rows(st);
     const float inv_bs = 1.f / (float)bsg;
-    const float dist_step = dist_next;
-    prefetch(st + 1);  // (IDX[(st + 1) & 1]: written a step ago, behind the last step's barrier)
-    load_idx(st + 2);  // IDX[st & 1]: its last reader was prefetch(st), issued a step ago
+    float dist_step = 0.f;
+   for (int sb = 0; sb < nsub; ++sb, ++p) {
+    const int bs = pass_rows(p);
+    dist_step = dist_next;
+    prefetch(p + 1);  // (IDX[(p + 1) & 1]: written a pass ago, behind the last pass's barrier)
+    load_idx(p + 2);  // IDX[p & 1]: its last reader was prefetch(p), issued a pass ago
     SPP_TP(0);
     const bool svalid = col < bs;
+    auto acc_to = [&](float& dst, float v) { dst = sb ? dst + v : v; };  // passes of one step add up
     // ---- fc1: h1 = tanh(W1 [x; 1]), 4 unit tiles of this wave's 16 samples
     f32x4 h1r[4];
     {
@@ -386,7 +407,22 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
             d3r[T3][i] = d;
           }
         lpart = ml_wave_sum(lpart);
-        if (lane == 0) SCP[w][0] = lpart;
+        if (lane == 0) acc_to(SCP[w][0], lpart);
+      } else if constexpr (VALUE) {  // value head: v = z3 (linear), loss 0.5 (q - v)^2 (a2c.py:209-219)
+        float lpart = 0.f;
+        const float inv_n = 1.f / (float)bsg;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float d = 0.f;
+          if (q == 0 && i == 0 && svalid) {
+            const float e = fsub_rn(Y[col], acc[0][i]);
+            lpart = 0.5f * e * e;
+            d = -e * inv_n;
+          }
+          d3r[0][i] = d;
+        }
+        lpart = ml_wave_sum(lpart);
+        if (lane == 0) acc_to(SCP[w][0], lpart);
       } else {
         // log_prob of the stored action (torch Normal: -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi)), summed
         // over the outputs: this lane's registers, then the sample's 4 lane groups)
@@ -437,12 +473,12 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
             }
             d3r[T3][i] = d;
             lsg = ml_row16_sum(lsg);  // the log_scale gradient over this wave's 16 samples
-            if (n == 0 && u < OUT) BP[w][H2 + 16 * NO + u] = lsg;
+            if (n == 0 && u < OUT) acc_to(BP[w][H2 + 16 * NO + u], lsg);
           }
         const float sm_ = ml_wave_sum(q == 0 ? mterm : 0.f), sk = ml_wave_sum(q == 0 ? kl : 0.f);
         if (lane == 0) {
-          SCP[w][0] = sm_;
-          SCP[w][1] = sk;
+          acc_to(SCP[w][0], sm_);
+          acc_to(SCP[w][1], sk);
         }
       }
 #pragma unroll
@@ -451,7 +487,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         for (int i = 0; i < 4; ++i) {
           D3I[(16 * T3 + 4 * q + i) * RS + col] = d3r[T3][i];
           const float s = ml_row16_sum(d3r[T3][i]);  // b3's gradient over this wave's samples
-          if (n == 0) BP[w][H2 + 16 * T3 + 4 * q + i] = s;
+          if (n == 0) acc_to(BP[w][H2 + 16 * T3 + 4 * q + i], s);
         }
     }
     SPP_TP(2);
@@ -474,7 +510,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           d2r[T2][i] *= 1.f - h2r[T2][i] * h2r[T2][i];
           D2I[(16 * T2 + 4 * q + i) * RS + col] = d2r[T2][i];
           const float s = ml_row16_sum(d2r[T2][i]);  // b2's gradient over this wave's samples
-          if (n == 0) BP[w][16 * T2 + 4 * q + i] = s;
+          if (n == 0) acc_to(BP[w][16 * T2 + 4 * q + i], s);
         }
     }
     // ---- dz1 = (W2^T dz2) * (1 - h1^2)
@@ -503,12 +539,12 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         layer = 0; mt = tt / C::NIT1; nt = tt - mt * C::NIT1;
         ar = D1I; br = XT;
       } else if (tt < C::NT1 + C::NT2) {
-        const int p = tt - C::NT1;
-        layer = 1; mt = p >> 2; nt = p & 3;
+        const int u = tt - C::NT1;
+        layer = 1; mt = u >> 2; nt = u & 3;
         ar = D2I; br = H1I;
       } else {
-        const int p = tt - C::NT1 - C::NT2;
-        layer = 2; mt = p / NB2; nt = p - mt * NB2;
+        const int u = tt - C::NT1 - C::NT2;
+        layer = 2; mt = u / NB2; nt = u - mt * NB2;
         ar = D3I; br = H2I;
       }
       ar += (16 * mt + n) * RS + 16 * q;
@@ -522,7 +558,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if (layer == 0) c = cu < IN ? C::O_W1 + row * IN + cu : (cu == IN ? C::O_B1 + row : -1);
         else if (layer == 1) c = C::O_W2 + row * 64 + cu;
         else c = row < OUT ? C::O_W3 + row * H2 + cu : -1;
-        if (c >= 0) GR[c] = acc[i];
+        if (c >= 0) acc_to(GR[c], acc[i]);
       }
     };
     for (int tt = w; tt < C::NT; tt += 8) {  // (wave-uniform; a missing second tile repeats the first, unstored)
@@ -555,36 +591,44 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           x0 = nx0; y0 = ny0; x1 = nx1; y1 = ny1;
         }
       }
+      SPP_TP(9);
       tile_store(c0, l0, m0, n0);
       if (two) tile_store(c1, l1, m1, n1);
+      SPP_TP(10);
     }
     SPP_TP(4);
+    if (sb + 1 < nsub) {  // the step's next pass: its rows into LDS once every wave is done with this one's
+      __syncthreads();
+      stage(p + 1);
+      __syncthreads();
+    }
+   }  // passes
     // ---- bias (and log_scale) gradients: the waves' partials in a fixed order; scalars -> GR[O_SC ..]
     {
       auto wsum = [&](int j) { return ((BP[0][j] + BP[1][j]) + BP[2][j]) + BP[3][j]; };
       if (t < H2) GR[C::O_B2 + t] = wsum(t);
       else if (t < H2 + OUT) GR[C::O_B3 + t - H2] = wsum(t);
-      else if (HEAD && t >= 128 && t < 128 + OUT) {  // - ent_coef * d entropy / d log_scale (once: workgroup 0)
+      else if (GAUSS && t >= 128 && t < 128 + OUT) {  // - ent_coef * d entropy / d log_scale (once: workgroup 0)
         const int u = t - 128;
         const float s = wsum(H2 + 16 * NO + u);
         GR[u] = (g == 0) ? s - a.ent_coef : s;
       }
     }
     if (t < 4) GR[C::O_SC + t] = t == 0 ? ((SCP[0][0] + SCP[1][0]) + SCP[2][0]) + SCP[3][0]
-                                        : (HEAD && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f);
-    if constexpr (HEAD) {  // the dist partials of every thread (this step's rows)
+                                        : (GAUSS && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f);
+    if constexpr (GAUSS) {  // the dist partials of every thread (this step's rows)
       const float ds = ml_wave_sum(dist_step);
       if (lane == 0) SCP[w][2] = ds;
     }
     if (t >= 192 && t - 192 < C::O_SC - NP) GR[NP + t - 192] = 0.f;
     __syncthreads();
-    if constexpr (HEAD) {
+    if constexpr (GAUSS) {
       if (t == 0) GR[C::O_SC + 2] = ((SCP[0][2] + SCP[1][2]) + SCP[2][2]) + SCP[3][2];
       __syncthreads();
     }
     // ---- exchange (G > 1) and Adam on this workgroup's shard
     float entropy = 0.f;
-    if (HEAD && g == 0 && t == 0) {  // of the parameters this step's forward used (before the update)
+    if (GAUSS && g == 0 && t == 0) {  // of the parameters this step's forward used (before the update)
       double ent = 0.0;
       for (int j = 0; j < OUT; ++j) ent += 0.5 + 0.91893853320467274178 + (double)LS[j];
       entropy = (float)ent;
@@ -606,8 +650,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         for (int k = 0; k < C::RLC; ++k) {
           const int i = i0 + t + kMlTH * k;
           if (i < nit) {
-            const int p = i / c4n;
-            ld[k] = slab_ld4(all, p * C::SLAB + 4 * (f0 + i - p * c4n));
+            const int src = i / c4n;
+            ld[k] = slab_ld4(all, src * C::SLAB + 4 * (f0 + i - src * c4n));
           }
         }
 #pragma unroll
@@ -631,8 +675,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if constexpr (MW) {
           const float4* red = reinterpret_cast<const float4*>(IMG) + (f - f0);
           gg4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int p = 0; p < G; ++p) {
-            const float4 x4 = red[p * c4n];
+          for (int src = 0; src < G; ++src) {
+            const float4 x4 = red[src * c4n];
             gg4.x += x4.x; gg4.y += x4.y; gg4.z += x4.z; gg4.w += x4.w;
           }
         } else {
@@ -644,17 +688,17 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int c = 4 * f + i;
           if (c < NP) {  // torch.optim.Adam (k_adam's operation order)
-            float& p = pref(c);
+            float& pv = pref(c);
             const float gi = gv[i];
             mom[k][i] = fadd_rn(mom[k][i], fmul_rn(omb1, fsub_rn(gi, mom[k][i])));
             vel[k][i] = fadd_rn(fmul_rn(vel[k][i], b2c), fmul_rn(fmul_rn(omb2, gi), gi));
             const float denom = fadd_rn(fdiv_rn(sqrtf(vel[k][i]), bc2s), eps);
-            p = fadd_rn(p, fmul_rn(neg_step, fdiv_rn(mom[k][i], denom)));
-            nv[i] = p;
+            pv = fadd_rn(pv, fmul_rn(neg_step, fdiv_rn(mom[k][i], denom)));
+            nv[i] = pv;
           }
         }
         if (4 * f == C::O_SC) {  // the scalar partials (the shard holding them)
-          if constexpr (HEAD == 0) {
+          if constexpr (!GAUSS) {  // (HEAD 2: the partials are 0.5 e^2; OUT = 1)
             loss_acc += gv[0] * (1.f / (float)(bsg * OUT));
           } else {
             a.out[(int64_t)st * 4 + 0] = (float)(-(double)gv[0] / (double)bsg);
@@ -665,10 +709,10 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if constexpr (MW) slab_st4(pub, 4 * f, make_float4(nv[0], nv[1], nv[2], nv[3]));
       }
     }
-    if (HEAD && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
+    if (GAUSS && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
     // the next step's rows into LDS while the other workgroups publish (XT, Y, LPO, ADV: last read by this
     // step's head and dW tiles, before the gradient staging barrier)
-    stage(st + 1);
+    stage(p);
     SPP_TP(7);
     if constexpr (MW) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead);
@@ -707,7 +751,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       }
     }
   constexpr int fsc = C::O_SC / 4;  // the scalar slot: owned by thread (fsc - f0) % kMlTH of its shard
-  if (HEAD == 0 && fsc >= f0 && fsc < f1 && (fsc - f0) % kMlTH == t) *a.loss_sum += loss_acc;
+  if (!GAUSS && fsc >= f0 && fsc < f1 && (fsc - f0) % kMlTH == t) *a.loss_sum += loss_acc;
 }
 
 }  // namespace spp

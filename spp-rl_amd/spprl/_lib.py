@@ -62,6 +62,8 @@ _SIGS = {
     "sppMTDestroy": (c_int, [c_void_p]),
     "sppRandNormal": (c_int, [c_void_p, c_int64, c_uint64, c_uint64, c_void_p]),
     "sppRandIndex": (c_int, [c_void_p, c_int64, c_int64, c_uint64, c_uint64, c_void_p]),
+    "sppRandPermScratchBytes": (c_int64, [c_int64]),
+    "sppRandPerm": (c_int, [c_void_p, c_int64, c_uint64, c_uint64, c_void_p, c_int64, c_void_p]),
     "sppReplayCreate": (c_int, [P(c_void_p), c_int64, c_int, c_int, c_int, c_int]),
     "sppReplayDestroy": (c_int, [c_void_p]),
     "sppReplayAddObs": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
@@ -152,6 +154,8 @@ _SIGS = {
     "sppAcmSgdEpoch": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),  # h, x, y, rows, bs
     "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
     "sppOnpActorEpoch": (c_int, [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p]),
+    "sppOnpCriticSteps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sppOnpCriticStepsMaxBatch": (c_int, [c_void_p]),
     "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),
     "sppOnpActorEpochStatus": (c_int, [c_void_p, c_void_p]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),

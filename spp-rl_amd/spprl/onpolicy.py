@@ -19,6 +19,7 @@ import torch
 
 from . import _lib, nets, ppo
 from ._lib import call, ptr, stream_handle
+from .perm import device_randperm
 
 H = 64
 
@@ -47,6 +48,9 @@ class OnPolicyNets:
         self.normalize_adv = normalize_adv
         self.entropy_coef, self.custom_loss = float(entropy_coef), float(custom_loss)
         self.kl_div_updates_counter = 0  # ppo.py:91, += epochs + 1 of each update_actor (ppo.py:192)
+        # the device permutations of the minibatch epochs: seed from ``seed`` or torch's global generator
+        self._perm_seed = seed if seed is not None else int(torch.randint(0, 2**62, (1,)).item())
+        self._perm_ctr = 0
         self.max_batch = int(max_batch)
         cfg = _lib.OnPolicyConfig(ob, aout, actor_lr, critic_lr, ppo_epsilon, entropy_coef, self.max_batch)
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -110,12 +114,20 @@ class OnPolicyNets:
         return loss
 
     def update_critic(self, obs, next_obs, rew, done):
-        """A2C.update_critic (a2c.py:186-225); returns the advantages of calculate_advantage."""
+        """A2C.update_critic (a2c.py:186-225); returns the advantages of calculate_advantage.  Single-process
+        runs make each target's num_critic_updates_per_target full-batch steps in one persistent launch
+        (sppOnpCriticSteps); data-parallel ranks all-reduce every step's gradient (critic_step)."""
         obs, next_obs, rew, done = (self._dev(t) for t in (obs, next_obs, rew, done))
         total = torch.zeros(1, device=self.device)
+        one_launch = self._critic_kernel_ok(obs.shape[0])
         for _ in range(self.critic_num_target_updates):
             vn = self.value(next_obs)
-            q = rew + self.gamma * (1 - done) * vn
+            q = (rew + self.gamma * (1 - done) * vn).contiguous()
+            if one_launch:
+                call("sppOnpCriticSteps", self._h, ptr(obs), ptr(q), obs.shape[0], self.num_critic_updates_per_target,
+                     ptr(total), stream_handle())
+                self._keep_crit = (obs, q)
+                continue
             for _ in range(self.num_critic_updates_per_target):
                 total += self.critic_step(obs, q)
         self.loss["critic"] = float(total.item()) / (self.critic_num_target_updates *
@@ -169,9 +181,13 @@ class OnPolicyNets:
                 break
             self.last_epochs += 1
             # a CPU generator (tests) keeps its host permutation; by default the permutation is drawn on the
-            # device (a host randperm + pageable copy would stall the stream every epoch)
-            perm = (torch.randperm(N, generator=generator).to(self.device) if generator is not None
-                    else torch.randperm(N, device=self.device))
+            # device by sppRandPerm (a host randperm + copy, or torch.randperm on the device, would stall the
+            # stream every epoch)
+            if generator is not None:
+                perm = torch.randperm(N, generator=generator).to(self.device)
+            else:
+                self._perm_ctr += 1
+                perm = device_randperm(N, self._perm_seed, self._perm_ctr * N, self.device)
             outs = torch.empty(-(-N // mb), 4, device=self.device)  # one row per minibatch step
             if one_launch:  # the whole epoch in one persistent launch (the ragged last minibatch included)
                 call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
@@ -197,6 +213,14 @@ class OnPolicyNets:
             self.loss.update(dist=s[2] / d, policy=(s[0] - self.entropy_coef * s[3] + self.custom_loss * s[2]) / d)
         self.kl_div_updates_counter += i + 1
         return kl
+
+    def _critic_kernel_ok(self, n):
+        """The persistent critic steps run single-process batches the co-resident grid covers in <= 8 passes."""
+        if self.allreduce is not None:
+            return False
+        if getattr(self, "_critic_max_n", None) is None:
+            self._critic_max_n = int(_lib.load().sppOnpCriticStepsMaxBatch(self._h))
+        return n <= self._critic_max_n
 
     def _epoch_kernel_ok(self, mb):
         """The one-launch epoch (sppOnpActorEpoch) runs single-process epochs of these dims whose minibatch

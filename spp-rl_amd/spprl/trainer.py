@@ -39,6 +39,7 @@ import torch
 
 from . import config
 from ._lib import SppError, call, load, ptr, stream_handle
+from .perm import device_randperm
 from .dp import make_allgather, make_allreduce, make_allreduce_sum, make_host_allreduce_sum, stream_key
 
 # ---------------------------------------------------------------- stats
@@ -659,8 +660,8 @@ class OffPolicyLoop:
         n = len(self.replay_buffer)
         if n == 0:
             return
-        # epoch permutations drawn on the device (DataLoader(shuffle=True), acm.py:275): a host randperm and
-        # its pageable copy would hold the stream for every epoch of a large ring
+        # epoch permutations drawn on the device (DataLoader(shuffle=True), acm.py:275) by sppRandPerm (a
+        # host randperm and its copy, or torch.randperm on the device, would hold the stream every epoch)
         # (_perm_seed: a seed shared by data-parallel ranks that run the epochs replicated, spprl/ppo_acm.py)
         ps = getattr(self, "_perm_seed", None)
         if ps is None:
@@ -668,11 +669,10 @@ class OffPolicyLoop:
         else:
             self._perm_ctr = getattr(self, "_perm_ctr", 0) + 1
             seed = ps + 104729 * self._perm_ctr
-        g = torch.Generator(device=self.device).manual_seed(seed)
-        for _ in range(epochs):
+        for e in range(epochs):
             lr = self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step)
             self._set_acm_lr(lr)
-            perm = torch.randperm(n, generator=g, device=self.device)
+            perm = device_randperm(n, seed, e * n, self.device)
             self._acm_loss_acc.zero_()
             bs = self.acm_batch_size
             nb = -(-n // bs)

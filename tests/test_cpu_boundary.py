@@ -14,7 +14,7 @@ HDR = os.path.join(REPO, "include", "spprl.h")
 
 def declared():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:sppStatus|const char\*|int)\s+(spp\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:sppStatus|const char\*|int|int64_t)\s+(spp\w+)\s*\(", txt, re.M)))
 
 
 @pytest.fixture(scope="module")

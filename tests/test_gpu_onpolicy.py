@@ -84,6 +84,49 @@ def test_critic_full_batch_at_bench_size():
     assert e < 2e-5, e
 
 
+@pytest.mark.parametrize("N", [50, 300, 32768])
+def test_critic_steps_kernel_matches_per_step_path_and_oracle(N):
+    """sppOnpCriticSteps (A2C.update_critic's full-batch steps for one target in ONE launch: one workgroup at
+    N = 50, 5 at N = 300, 256 workgroups x 2 passes of 64 rows at the bench's N = 32,768) against (a) the
+    per-step path (sppOnpCriticGrads / Apply, five launches a step) and (b) the oracle's float64 steps with
+    the same Adam (oracle.onpolicy.critic_steps): the summed loss rtol 1e-4; parameters within 2 lr per Adam
+    step of the oracle (a sign flip of a near-zero gradient coordinate), mean far below that."""
+    from spprl import _lib
+    from spprl.onpolicy import OnPolicyNets
+
+    K, lr = 10, 3e-4
+    c0 = oo.init_flat(oo.critic_layout(OB), 31)
+    rng = np.random.RandomState(N + 3)
+    x = (rng.randn(N, OB) * 1.3).astype(np.float32)
+    q = (rng.randn(N) * 0.7).astype(np.float32)
+    xd, qd = torch.from_numpy(x).to(DEV), torch.from_numpy(q).to(DEV)
+    res = []
+    for one_launch in (True, False):
+        n = OnPolicyNets(OB, AOUT, critic_lr=lr, max_batch=max(N, 512), device=DEV)
+        n.load_net(1, c0)
+        if not one_launch:
+            n._critic_max_n = 0
+        assert n._critic_kernel_ok(N) == one_launch
+        total = torch.zeros(1, device=DEV)
+        if one_launch:
+            _lib.call("sppOnpCriticSteps", n._h, _lib.ptr(xd), _lib.ptr(qd), N, K, _lib.ptr(total),
+                      _lib.stream_handle())
+        else:
+            for _ in range(K):
+                total += n.critic_step(xd, qd)
+        torch.cuda.synchronize()
+        if one_launch:
+            n.check_actor_epochs()  # (the shared timeout flag of the persistent launches)
+        res.append((n.params[1].cpu().numpy().copy(), float(total.item())))
+    flat, losses = oo.critic_steps(c0, OB, x, q, lr, K, dtype=torch.float64)
+    for p, tot in res:
+        assert tot == pytest.approx(sum(losses), rel=1e-4)
+        d = np.abs(p - flat)
+        print("N %d: loss %.6f (ref %.6f) |d|/lr max %.4f mean %.6f" % (N, tot, sum(losses), d.max() / lr,
+                                                                       d.mean() / lr))
+        assert d.max() <= 2 * lr * K * 1.01 and d.mean() <= 0.01 * lr, (d.max(), d.mean())
+
+
 @pytest.mark.parametrize("N", [1, 500, 2048])
 def test_actor_grad_clip_entropy(nets, N):
     a, c = _setup(nets, 5)

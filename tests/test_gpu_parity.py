@@ -466,7 +466,7 @@ def test_update_acm_epochs_with_step_lr_match_oracle(bs, monkeypatch):
     """AcMTrainer.update_acm (acm.py:266-303, the pre-train epoch mode): shuffled epochs over every
     live row in batches of acm_batch_size with a ragged last batch, StepLR(step 1, gamma 0.5) stepped
     once per epoch, loss['acm'] = the last epoch's mean batch loss.  The oracle replays the same
-    permutations (recorded from the loop's torch.randperm) through AcMTrainer.batch_update with
+    permutations (recorded from the loop's device_randperm) through AcMTrainer.batch_update with
     the scheduled lr.  bs = 100 runs the one-workgroup sppAcmSgd launches, bs = 160 the
     multi-workgroup form.  Tolerance as for the persistent SGD test, over all 3 x 21 (13) Adam steps."""
     import spprl.trainer as tr
@@ -475,14 +475,14 @@ def test_update_acm_epochs_with_step_lr_match_oracle(bs, monkeypatch):
     ag = _filled_agent("Hopper-v2", 11, 3, n, seed=6)
     ag.acm_batch_size, ag.acm_scheduler_step, ag.acm_scheduler_gamma = bs, 1, 0.5
     perms = []
-    real = torch.randperm
+    real = tr.device_randperm
 
     def rec(*a, **k):
         p = real(*a, **k)
         perms.append(p.clone())
         return p
 
-    monkeypatch.setattr(tr.torch, "randperm", rec)
+    monkeypatch.setattr(tr, "device_randperm", rec)
     rb = ag.replay_buffer
     params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}
     o = OracleAcmTrainer(22, 3, lr=ag.acm_lr, ac_lim=ag.ac_lim.numpy(), params=params)

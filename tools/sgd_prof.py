@@ -18,7 +18,7 @@ from spprl import _lib  # noqa: E402
 
 NAMES = {0: "stage rows, prefetch", 1: "fc1", 2: "fc2, fc3, loss, dz2", 3: "dz1", 4: "gradient tiles, bias sums",
          5: "canonical staging", 6: "slab stores, barrier 1", 7: "shard reduce, Adam, publish",
-         8: "barrier 2, reload"}
+         8: "barrier 2, reload", 9: "  dW pair MFMAs", 10: "  dW pair stores"}
 
 
 def main():
@@ -52,7 +52,7 @@ def main():
     tot = v.sum()
     print("k_mlp_sgd<34, 32, 6, 0>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
           % (K, bs, el * 1e3, el * 1e6 / K, tot))
-    for k in range(9):
+    for k in range(11):
         print("  %2d %-20s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
 
 

@@ -151,7 +151,7 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
             ["-DSPP_PROF_DRAIN"] if "--drain" in sys.argv else []) + (
             ["-DSPP_WITH_HCHEETAH"] if "--hcheetah" in sys.argv else [])
         cmd = [HIPCC] + FLAGS + ["-shared", "-DSPP_PROF", "-DSPP_SINGLE_TU"] + extra + [
-            "-o", out, os.path.join(CSRC, "api.hip")]
+            "-o", out, os.path.join(CSRC, "api.hip"), os.path.join(CSRC, "ks_perm.hip")]
         subprocess.check_call(cmd)
         return out
     if not force and up_to_date():

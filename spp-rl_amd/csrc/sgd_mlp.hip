@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
                 NO = C::NO;
   __shared__ __attribute__((aligned(16))) float IMG[C::IMGR * RS];  // H1 | D1 | H2 | D2 | D3; G > 1: the slab chunks
   __shared__ __attribute__((aligned(16))) float XT[C::XTR * RS];    // [input][sample]; row IN = 1 (rows < bs)
-  __shared__ __attribute__((aligned(16))) float GR[C::NPS];         // the step's gradient, canonical order
+  __shared__ __attribute__((aligned(16))) float GR[C::NPS + 4];     // the step's gradient, canonical order (+ dump)
   __shared__ __attribute__((aligned(16))) float W1[64 * SW1];       // [unit][input]; column IN = b1
   __shared__ __attribute__((aligned(16))) float W2[H2 * SW2];
   __shared__ __attribute__((aligned(16))) float W3[16 * NO * SW3];  // rows >= OUT zero
@@ -550,15 +550,26 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       ar += (16 * mt + n) * RS + 16 * q;
       br += (16 * nt + n) * RS + 16 * q;
     };
+    // (elements outside the parameters -- dW1's padding columns, dW3's rows >= OUT -- go to the dump word
+    // GR[NPS]: every lane stores, no divergent branch)
     auto tile_store = [&](const f32x4& acc, int layer, int mt, int nt) {
+      const int row0 = 16 * mt + 4 * q, cu = 16 * nt + n;
+      int c0, dc;
+      if (layer == 0) {
+        c0 = cu < IN ? C::O_W1 + row0 * IN + cu : C::O_B1 + row0;
+        dc = cu < IN ? IN : 1;
+      } else if (layer == 1) {
+        c0 = C::O_W2 + row0 * 64 + cu;
+        dc = 64;
+      } else {
+        c0 = C::O_W3 + row0 * H2 + cu;
+        dc = H2;
+      }
+      const bool col_ok = layer != 0 || cu <= IN;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = 16 * mt + 4 * q + i, cu = 16 * nt + n;
-        int c = -1;
-        if (layer == 0) c = cu < IN ? C::O_W1 + row * IN + cu : (cu == IN ? C::O_B1 + row : -1);
-        else if (layer == 1) c = C::O_W2 + row * 64 + cu;
-        else c = row < OUT ? C::O_W3 + row * H2 + cu : -1;
-        if (c >= 0) acc_to(GR[c], acc[i]);
+        const bool ok = col_ok && (layer != 2 || row0 + i < OUT);
+        acc_to(GR[ok ? c0 + i * dc : C::NPS], acc[i]);
       }
     };
     for (int tt = w; tt < C::NT; tt += 8) {  // (wave-uniform; a missing second tile repeats the first, unstored)

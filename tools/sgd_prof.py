@@ -16,13 +16,48 @@ import torch  # noqa: E402
 import spprl  # noqa: E402
 from spprl import _lib  # noqa: E402
 
-NAMES = {0: "stage rows, prefetch", 1: "fc1", 2: "fc2, fc3, loss, dz2", 3: "dz1", 4: "gradient tiles, bias sums",
-         5: "canonical staging", 6: "slab stores, barrier 1", 7: "shard reduce, Adam, publish",
-         8: "barrier 2, reload", 9: "  dW pair MFMAs", 10: "  dW pair stores"}
+NAMES = {0: "prefetch issue", 1: "fc1", 2: "fc2, fc3, head, b3 sums", 3: "dz2, dz1, image barrier", 4: "dW loop exit",
+         5: "bias sums, scalars, barrier", 6: "slab stores, barrier 1", 7: "shard reduce, Adam, publish",
+         8: "barrier 2, reload (stage in 7)", 9: "  dW pair MFMAs", 10: "  dW pair stores"}
+
+
+def report(name, K, G, el, buf):
+    v = np.array(buf[:32], dtype=np.float64) / (4 * K * G)  # waves 0..3 of every workgroup recorded
+    tot = v.sum()
+    print("%s: %d steps in %.3f ms (%.2f us/step); cycles per step per wave: %.0f" % (name, K, el * 1e3, el * 1e6 / K, tot))
+    for k in range(11):
+        print("  %2d %-28s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
+
+
+def actor(dev):
+    """The PPO actor epoch (k_mlp_sgd<17, 64, 17, 1>): 32,768 rows in 512-row minibatches (8 workgroups)."""
+    from spprl.onpolicy import OnPolicyNets
+    N, mb = 32768, 512
+    n = OnPolicyNets(17, 17, ac_lim=1.0, max_batch=N, device=dev, seed=0)
+    x = torch.randn(N, 17, device=dev)
+    act = torch.rand(N, 17, device=dev) * 2 - 1
+    lp = torch.randn(N, device=dev) - 20
+    adv = torch.randn(N, device=dev)
+    perm = torch.randperm(N, device=dev)
+    outs = torch.empty(N // mb, 4, device=dev)
+    st = _lib.stream_handle()
+    args = [n._h] + [_lib.ptr(t) for t in (x, act, lp, adv, act, perm)] + [N, mb, _lib.ptr(outs), st]
+    _lib.call("sppOnpActorEpoch", *args)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 64)()
+    _lib.call("sppDebugReadProf", buf, 1)
+    t0 = time.perf_counter()
+    _lib.call("sppOnpActorEpoch", *args)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    _lib.call("sppDebugReadProf", buf, 1)
+    report("k_mlp_sgd<17, 64, 17, 1> (actor epoch, 512-row steps)", N // mb, mb // 64, el, buf)
 
 
 def main():
     dev = torch.device("cuda", 0)
+    if len(sys.argv) > 1 and sys.argv[1] == "actor":
+        return actor(dev)
     ob, ac, K = 17, 6, 400
     bs = int(sys.argv[1]) if len(sys.argv) > 1 else 1049  # > 64: the multi-workgroup form
     ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", max_batch=max(4096, bs), buffer_size=40_000, device=dev, seed=0)
@@ -47,13 +82,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     _lib.call("sppDebugReadProf", buf, 1)
-    G = -(-bs // 64)
-    v = np.array(buf[:32], dtype=np.float64) / (4 * K * G)  # waves 0..3 of every workgroup recorded
-    tot = v.sum()
-    print("k_mlp_sgd<34, 32, 6, 0>: %d steps of %d in %.3f ms (%.2f us/step); cycles per step per wave: %.0f"
-          % (K, bs, el * 1e3, el * 1e6 / K, tot))
-    for k in range(11):
-        print("  %2d %-20s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
+    report("k_mlp_sgd<34, 32, 6, 0> (%d-row steps)" % bs, K, -(-bs // 64), el, buf)
 
 
 if __name__ == "__main__":

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   __shared__ int64_t IDX[GAUSS ? 2 * R : 1];
   __shared__ float BP[4][C::NBP];   // per wave: bias (and log_scale) gradient partials over its 16 samples
   __shared__ float SCP[4][4];       // per wave: scalar partials
+  __shared__ float GT[GAUSS ? 4 : 1][3][32];  // HEAD 1, per wave: scale, variance, log(scale) of the step's log_scale
   __shared__ float adam_s[2][2];
   __shared__ int s_dead;
   float* const H1I = IMG;
@@ -425,7 +426,15 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if (lane == 0) acc_to(SCP[w][0], lpart);
       } else {
         // log_prob of the stored action (torch Normal: -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi)), summed
-        // over the outputs: this lane's registers, then the sample's 4 lane groups)
+        // over the outputs: this lane's registers, then the sample's 4 lane groups).  The per-output scale terms
+        // once per wave and step (the same values every use: scale = exp(log_scale), its square and log)
+        if (lane < OUT) {
+          const float sc = expf(LS[lane]);
+          GT[w][0][lane] = sc;
+          GT[w][1][lane] = fmul_rn(sc, sc);
+          GT[w][2][lane] = logf(sc);
+        }
+        SPP_XLANE_SYNC();
         float th[NO][4], dd[NO][4], lp = 0.f;
 #pragma unroll
         for (int T3 = 0; T3 < NO; ++T3)
@@ -435,11 +444,10 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
             th[T3][i] = 0.f;
             dd[T3][i] = 0.f;
             if (u < OUT) {
-              const float sc = expf(LS[u]);
               th[T3][i] = ml_tanh(acc[T3][i]);
               const float mu = fmul_rn(th[T3][i], LIM[u]);
               dd[T3][i] = fsub_rn(Y[col * OUT + u], mu);
-              lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(dd[T3][i], dd[T3][i]), 2.f * fmul_rn(sc, sc)), logf(sc)),
+              lp += fsub_rn(fsub_rn(fdiv_rn(-fmul_rn(dd[T3][i], dd[T3][i]), 2.f * GT[w][1][u]), GT[w][2][u]),
                             kLogSqrt2PiO);
             }
           }
@@ -465,8 +473,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
             const int u = 16 * T3 + 4 * q + i;
             float d = 0.f, lsg = 0.f;
             if (u < OUT) {
-              const float sc = expf(LS[u]);
-              const float var = fmul_rn(sc, sc);
+              const float var = GT[w][1][u];
               const float gmu = glp * dd[T3][i] / var;
               lsg = glp * (dd[T3][i] * dd[T3][i] / var - 1.f);
               d = gmu * LIM[u] * (1.f - th[T3][i] * th[T3][i]);

@@ -463,6 +463,10 @@ sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
 sppStatus sppOnpCriticSteps(sppOnPolicyHandle h, const float* x, const float* q, int N, int nsteps, float* loss_sum,
                             void* stream);
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle h);
+/* Leave n workgroup slots of the device to a persistent launch running concurrently on another stream (the
+ * PPO_AcM ACM epochs beside update(mem)): sppOnpCriticSteps / sppOnpActorEpoch size their grids from the
+ * co-resident capacity minus n, so both grids stay resident at once.  0 restores the whole device. */
+sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle h, int n);
 /* Actor.act (basic_model.py:32-51) continuous: a = mu + exp(log_scale) * eps (eps NULL:
  * deterministic mu), logp = Independent(Normal).log_prob(a). */
 sppStatus sppOnpAct(sppOnPolicyHandle h, const float* x, int N, const float* eps, float* act_out, float* logp_out,

@@ -2164,6 +2164,7 @@ struct sppOnPolicy {
   DevArray<int> sgd_sync;
   int sgd_max_wg = -1;
   int crit_max_wg = -1;  // co-resident persistent-critic workgroups (onp_critic_max_wg, cached)
+  int wg_reserve = 0;    // workgroup slots left to a persistent launch on another stream (sppOnpReserveWorkgroups)
 };
 
 static sppStatus onp_packs(sppOnPolicy* o) {
@@ -2448,7 +2449,7 @@ static int onp_epoch_max_wg(sppOnPolicy* o) {
 
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
   if (!o) return 0;
-  const int n = onp_epoch_max_wg(o);
+  const int n = onp_epoch_max_wg(o) - o->wg_reserve;
   return n > 0 ? kMlR * n : 0;
 }
 
@@ -2458,7 +2459,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
               "actor epoch: bad args");
   const int nsteps = cdiv(nrows, bs);
   SPP_REQUIRE(o->net[0].p && o->net[0].m && o->net[0].v && o->lim.ptr, SPP_E_STATE, "actor epoch: actor not bound");
-  const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o);
+  const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o) - o->wg_reserve;
   SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "actor epoch: no instantiation for ob=%d aout=%d", o->cfg.ob, o->cfg.aout);
   SPP_REQUIRE(nwg <= maxwg, SPP_E_SHAPE, "actor epoch: batch %d needs %d co-resident workgroups > %d", bs, nwg, maxwg);
   if (nsteps == 0) return SPP_OK;
@@ -2492,6 +2493,10 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
 
 // persistent critic steps (HEAD 2): co-resident workgroups, passes of 64 rows per workgroup and step
 constexpr int kCriticMaxPasses = 8;
+// slots the critic grid always leaves free (a concurrent ACM grid of up to 64 workgroups: PPO_AcM), so that
+// its row partition -- and with it the gradient's summation order -- is the same with or without one
+constexpr int kCriticSideSlots = 64;
+
 static int onp_critic_max_wg(sppOnPolicy* o) {
   if (o->crit_max_wg >= 0) return o->crit_max_wg;
   const int ob = o->cfg.ob;
@@ -2502,17 +2507,28 @@ static int onp_critic_max_wg(sppOnPolicy* o) {
   return n;
 }
 
+static int onp_critic_budget(sppOnPolicy* o) {
+  const int full = onp_critic_max_wg(o);
+  return std::max(0, std::min(full - std::max(o->wg_reserve, kCriticSideSlots), full > kCriticSideSlots ? full : 0));
+}
+
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle o) {
   if (!o) return 0;
-  return kMlR * kCriticMaxPasses * onp_critic_max_wg(o);
+  return kMlR * kCriticMaxPasses * onp_critic_budget(o);
+}
+
+sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle o, int n) {
+  SPP_REQUIRE(o && n >= 0, SPP_E_INVALID_ARG, "reserve workgroups: bad args");
+  o->wg_reserve = n;
+  return SPP_OK;
 }
 
 sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
                             void* stream) {
   SPP_REQUIRE(o && x && q && loss_sum && N > 0 && nsteps >= 0, SPP_E_INVALID_ARG, "critic steps: bad args");
   SPP_REQUIRE(o->net[1].p && o->net[1].m && o->net[1].v && o->lim.ptr, SPP_E_STATE, "critic steps: critic not bound");
-  const int maxwg = onp_critic_max_wg(o);
-  SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "critic steps: no instantiation for ob=%d", o->cfg.ob);
+  const int maxwg = onp_critic_budget(o);
+  SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "critic steps: no instantiation for ob=%d (or every slot reserved)", o->cfg.ob);
   // fewest passes per workgroup the co-resident grid allows, then the fewest workgroups for that many passes
   const int tiles = cdiv(N, kMlR), passes = cdiv(tiles, maxwg), nwg = cdiv(tiles, passes);
   SPP_REQUIRE(passes <= kCriticMaxPasses, SPP_E_SHAPE, "critic steps: batch %d > %d", N, kMlR * kCriticMaxPasses * maxwg);

@@ -156,6 +156,7 @@ _SIGS = {
     "sppOnpActorEpoch": (c_int, [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p]),
     "sppOnpCriticSteps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sppOnpCriticStepsMaxBatch": (c_int, [c_void_p]),
+    "sppOnpReserveWorkgroups": (c_int, [c_void_p, c_int]),
     "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),
     "sppOnpActorEpochStatus": (c_int, [c_void_p, c_void_p]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),

@@ -214,6 +214,12 @@ class OnPolicyNets:
         self.kl_div_updates_counter += i + 1
         return kl
 
+    def reserve_workgroups(self, n):
+        """Size the persistent critic / actor grids for n workgroup slots taken by a concurrent persistent
+        launch on another stream (sppOnpReserveWorkgroups); 0 restores the whole device."""
+        call("sppOnpReserveWorkgroups", self._h, int(n))
+        self._critic_max_n = self._epoch_max_bs = None
+
     def _critic_kernel_ok(self, n):
         """The persistent critic steps run single-process batches the co-resident grid covers in <= 8 passes."""
         if self.allreduce is not None:

@@ -191,21 +191,60 @@ class PPO_AcM:
         return self.stats_logger.running_return
 
     def perform_iteration(self, sync=True):
-        """on_policy.py:52-75.  Returns the mean return of the episodes completed (None if none)."""
+        """on_policy.py:52-75.  Returns the mean return of the episodes completed (None if none).
+
+        update(mem) (critic, GAE, actor) and update_acm touch disjoint networks and data: the ACM trains on
+        the ring, already flushed by collect_batch, and nothing in update(mem) reads the ACM.  A single-process
+        run therefore enqueues the ACM epochs on a side stream first and runs update(mem) beside them (the
+        persistent critic / actor grids leave the ACM grid's workgroup slots free); the obs statistics and the
+        next rollout wait for both, as in the reference's order.  The results are the serial order's."""
         self._ret_sums.zero_()
         mem = self.collect_batch()
-        self.update(mem)
-        if self.acm_update_freq and self.iteration % self.acm_update_freq == 0:
-            if self.acm_update_batches:
-                self.acm.update_acm_batches(self.acm_update_batches)
-            else:
-                self.acm.update_acm(self.acm_epochs)
+        acm_now = bool(self.acm_update_freq) and self.iteration % self.acm_update_freq == 0
+        side = self._acm_side_stream() if acm_now else None
+        if side is not None:
+            ready = torch.cuda.Event()
+            ready.record()
+            side.wait_event(ready)
+            self.nets.reserve_workgroups(self.acm.acm_sgd_workgroups())
+            with torch.cuda.stream(side):
+                self._update_acm()
+            done = torch.cuda.Event()
+            done.record(side)
+            try:
+                self.update(mem)
+            finally:
+                torch.cuda.current_stream().wait_event(done)
+                self.nets.reserve_workgroups(0)
+        else:
+            self.update(mem)
+            if acm_now:
+                self._update_acm()
         if self.denormalize_actor_out:
             self.acm.update_obs_stats()
         if not sync:
             return None
         s = self._ret_sums.cpu().numpy()
         return float(s[0] / s[1]) if s[1] > 0 else None
+
+    def _update_acm(self):
+        if self.acm_update_batches:
+            self.acm.update_acm_batches(self.acm_update_batches)
+        else:
+            self.acm.update_acm(self.acm_epochs)
+
+    def _acm_side_stream(self):
+        """The side stream of the concurrent ACM update, or None: single process, CUDA device, persistent ACM
+        SGD eligible (one launch per epoch), and the env var SPP_PPO_ACM_OVERLAP not 0."""
+        import os
+
+        if os.environ.get("SPP_PPO_ACM_OVERLAP", "1") == "0" or self.world > 1 or self.device.type != "cuda":
+            return None
+        if not self.acm._acm_sgd_ok(self.acm.acm_batch_size):
+            return None
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     # ---------------------------------------------------------------- A2C.collect_batch
     def _start(self):

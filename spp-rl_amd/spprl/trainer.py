@@ -598,6 +598,10 @@ class OffPolicyLoop:
             self._sgd_max_bs = int(load().sppAcmSgdMaxBatch(self._h))
         return bs <= self._sgd_max_bs
 
+    def acm_sgd_workgroups(self):
+        """Workgroups of one multi-workgroup sppAcmSgd step at acm_batch_size (64 rows each; 1 below that)."""
+        return max(1, -(-int(self.acm_batch_size) // 64))
+
     def _acm_sgd(self, idx, nsteps, bs, nrows=None):
         """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd); with nrows,
         one epoch over idx[:nrows] whose last batch is the ragged remainder (sppAcmSgdEpoch)."""

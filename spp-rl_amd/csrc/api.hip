@@ -2509,7 +2509,7 @@ static int onp_critic_max_wg(sppOnPolicy* o) {
 
 static int onp_critic_budget(sppOnPolicy* o) {
   const int full = onp_critic_max_wg(o);
-  return std::max(0, std::min(full - std::max(o->wg_reserve, kCriticSideSlots), full > kCriticSideSlots ? full : 0));
+  return std::max(0, full > kCriticSideSlots ? full - std::max(o->wg_reserve, kCriticSideSlots) : full - o->wg_reserve);
 }
 
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle o) {

@@ -278,6 +278,8 @@ def test_rand_perm_is_a_uniform_permutation(n):
             assert stats.chisquare(np.bincount(draws[:, pos], minlength=5)).pvalue > 1e-4
     if n >= 32768:
         assert abs(np.corrcoef(np.arange(n), x)[0, 1]) < 6 / np.sqrt(n)
+        # the stream's scratch has grown to this n: a small permutation through the larger buffer
+        np.testing.assert_array_equal(np.sort(device_randperm(7, 77, 0, DEV).cpu().numpy()), np.arange(7))
 
 
 def test_rand_streams_do_not_alias():

@@ -99,7 +99,7 @@ struct MlCfg {
   static constexpr int SLAB = (NPS + 63) / 64 * 64;     // slab stride (floats)
   static constexpr int K4 = (NP4 + kMlTH - 1) / kMlTH;  // float4 slots per thread (G = 1: all of them)
   static constexpr int NXP = (kMlR * IN + kMlTH - 1) / kMlTH, NYP = (kMlR * OUT + kMlTH - 1) / kMlTH;
-  static_assert(SLAB <= kMlSlabMax, "slab");
+  static_assert(SLAB <= kMlSlabMax && SLAB > NPS, "slab (and its dump word at NPS)");
   // G > 1: the shard's G slab chunks are staged in the image region, at most NP4 + G - 1 float4
   static constexpr int RED4 = IMGR * kMlRS / 4;
   static constexpr int MAXG = RED4 - NP4 + 1 < kMlMaxWG ? RED4 - NP4 + 1 : kMlMaxWG;
@@ -153,6 +153,9 @@ template <int IN, int H2, int OUT, int HEAD, bool MW>
 __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   using C = MlCfg<IN, H2, OUT, HEAD>;
   constexpr bool GAUSS = HEAD == 1, VALUE = HEAD == 2;
+  // G > 1, one pass per step: every gradient element goes to this workgroup's slab as soon as it is final
+  // (write-through stores issued under the remaining tiles' MFMAs), not through the canonical LDS staging
+  constexpr bool DIRECT = MW && !VALUE;
   static_assert(!VALUE || OUT == 1, "value head");
   constexpr int RS = kMlRS, R = kMlR, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
                 NO = C::NO;
@@ -314,6 +317,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   for (int st = 0; st < a.nsteps; ++st) {
     const int bsg = step_rows(st);
     const float inv_bs = 1.f / (float)bsg;
+    const auto mine = sgd_rsrc(a.slab + ((int64_t)(st & 1) * G + g) * C::SLAB);  // (G > 1) this step's slab
     float dist_step = 0.f;
    for (int sb = 0; sb < nsub; ++sb, ++p) {
     const int bs = pass_rows(p);
@@ -576,7 +580,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool ok = col_ok && (layer != 2 || row0 + i < OUT);
-        acc_to(GR[ok ? c0 + i * dc : C::NPS], acc[i]);
+        if constexpr (DIRECT) slab_st1(mine, ok ? c0 + i * dc : C::NPS, acc[i]);
+        else acc_to(GR[ok ? c0 + i * dc : C::NPS], acc[i]);
       }
     };
     for (int tt = w; tt < C::NT; tt += 8) {  // (wave-uniform; a missing second tile repeats the first, unstored)
@@ -624,24 +629,34 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     // ---- bias (and log_scale) gradients: the waves' partials in a fixed order; scalars -> GR[O_SC ..]
     {
       auto wsum = [&](int j) { return ((BP[0][j] + BP[1][j]) + BP[2][j]) + BP[3][j]; };
-      if (t < H2) GR[C::O_B2 + t] = wsum(t);
-      else if (t < H2 + OUT) GR[C::O_B3 + t - H2] = wsum(t);
+      auto put = [&](int c, float v) {
+        if constexpr (DIRECT) slab_st1(mine, c, v);
+        else GR[c] = v;
+      };
+      if (t < H2) put(C::O_B2 + t, wsum(t));
+      else if (t < H2 + OUT) put(C::O_B3 + t - H2, wsum(t));
       else if (GAUSS && t >= 128 && t < 128 + OUT) {  // - ent_coef * d entropy / d log_scale (once: workgroup 0)
         const int u = t - 128;
         const float s = wsum(H2 + 16 * NO + u);
-        GR[u] = (g == 0) ? s - a.ent_coef : s;
+        put(u, (g == 0) ? s - a.ent_coef : s);
       }
+      // scalars (HEAD 1's dist partial at O_SC + 2 is written below, after its reduction)
+      if (t < 4 && !(GAUSS && t == 2))
+        put(C::O_SC + t, t == 0 ? ((SCP[0][0] + SCP[1][0]) + SCP[2][0]) + SCP[3][0]
+                                : (GAUSS && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f));
+      if (t >= 192 && t - 192 < C::O_SC - NP) put(NP + t - 192, 0.f);
     }
-    if (t < 4) GR[C::O_SC + t] = t == 0 ? ((SCP[0][0] + SCP[1][0]) + SCP[2][0]) + SCP[3][0]
-                                        : (GAUSS && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f);
     if constexpr (GAUSS) {  // the dist partials of every thread (this step's rows)
       const float ds = ml_wave_sum(dist_step);
       if (lane == 0) SCP[w][2] = ds;
     }
-    if (t >= 192 && t - 192 < C::O_SC - NP) GR[NP + t - 192] = 0.f;
     __syncthreads();
     if constexpr (GAUSS) {
-      if (t == 0) GR[C::O_SC + 2] = ((SCP[0][2] + SCP[1][2]) + SCP[2][2]) + SCP[3][2];
+      if (t == 0) {
+        const float ds = ((SCP[0][2] + SCP[1][2]) + SCP[2][2]) + SCP[3][2];
+        if constexpr (DIRECT) slab_st1(mine, C::O_SC + 2, ds);
+        else GR[C::O_SC + 2] = ds;
+      }
       __syncthreads();
     }
     // ---- exchange (G > 1) and Adam on this workgroup's shard
@@ -654,11 +669,11 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     SPP_TP(5);
     const auto all = sgd_rsrc(a.slab + (int64_t)(st & 1) * G * C::SLAB);  // (G = 1: unused)
     if constexpr (MW) {
-      const auto mine = sgd_rsrc(a.slab + ((int64_t)(st & 1) * G + g) * C::SLAB);
-      for (int f = t; f < C::NP4; f += kMlTH) {
-        const float4 v4 = *reinterpret_cast<const float4*>(GR + 4 * f);
-        slab_st4(mine, 4 * f, v4);
-      }
+      if constexpr (!DIRECT)  // (HEAD 2: the passes' sums staged in GR)
+        for (int f = t; f < C::NP4; f += kMlTH) {
+          const float4 v4 = *reinterpret_cast<const float4*>(GR + 4 * f);
+          slab_st4(mine, 4 * f, v4);
+        }
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead);
       // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
       const int nit = c4n * G;

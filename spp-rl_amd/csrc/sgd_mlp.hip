@@ -374,6 +374,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           H2I[(16 * T2 + 4 * q + i) * RS + col] = h2r[T2][i];
         }
     }
+    SPP_TP(11);
     // ---- fc3 and the head: d3r = d loss / d z3 (rows >= OUT zero)
     f32x4 d3r[NO];
     {
@@ -392,6 +393,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           acc[T3] = ml_mfma16(w4.z, h2r[T][2], acc[T3]);
           acc[T3] = ml_mfma16(w4.w, h2r[T][3], acc[T3]);
         }
+      SPP_TP(12);
       if constexpr (HEAD == 0) {
         float lpart = 0.f;
         const float inv_n = 1.f / (float)(bsg * OUT);
@@ -492,6 +494,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           acc_to(SCP[w][1], sk);
         }
       }
+      SPP_TP(13);
 #pragma unroll
       for (int T3 = 0; T3 < NO; ++T3)
 #pragma unroll

@@ -149,6 +149,11 @@ __device__ __forceinline__ float ml_wave_sum(float v) {
   return (lane_v(0) + lane_v(16)) + (lane_v(32) + lane_v(48));
 }
 
+// LDS words addressed by 32-bit offsets held in registers (ds_write with a VGPR address, no generic pointer)
+typedef __attribute__((address_space(3))) float ml_lds_f;
+__device__ __forceinline__ uint32_t lds_off(float* p) { return (uint32_t)(uintptr_t)(ml_lds_f*)p; }
+__device__ __forceinline__ void lds_st(uint32_t off, float v) { *(ml_lds_f*)(uintptr_t)off = v; }
+
 template <int IN, int H2, int OUT, int HEAD, bool MW>
 __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   using C = MlCfg<IN, H2, OUT, HEAD>;
@@ -310,6 +315,16 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   load_idx(1);
   stage(0);
   __syncthreads();
+  // G > 1: the LDS image word of each canonical element this thread reloads after the publish (slot
+  // f = t + 256 k, element i; elements past the parameters -> a dump word), resolved once for the launch
+  uint32_t roff[MW ? C::NL : 1][4];
+#pragma unroll
+  for (int k = 0; k < (MW ? C::NL : 1); ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * (t + kMlTH * k) + i;
+      roff[k][i] = lds_off(c < NP ? &pref(c) : &GR[C::NPS + 1]);
+    }
   SPP_TP_INIT();
   float loss_acc = 0.f;  // HEAD 0 / 2: sum over steps of the batch loss (the scalar slot's owner)
   const float lo = 1.f - a.eps_clip, hi = 1.f + a.eps_clip;
@@ -754,19 +769,16 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead);
       float4 rv[C::NL];
 #pragma unroll
-      for (int k = 0; k < C::NL; ++k) {  // (this shard's values are already in the images)
-        const int f = t + kMlTH * k;
-        if (f < C::NP4 && (f < f0 || f >= f1)) rv[k] = slab_ld4(pub, 4 * f);
+      for (int k = 0; k < C::NL; ++k) {  // (this shard's own slots reload the values it published)
+        rv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t + kMlTH * k < C::NP4) rv[k] = slab_ld4(pub, 4 * (t + kMlTH * k));
       }
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {
-        const int f = t + kMlTH * k;
-        if (f < C::NP4 && (f < f0 || f >= f1)) {
-          const float vv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (4 * f + i < NP) pref(4 * f + i) = vv[i];
-        }
+        lds_st(roff[k][0], rv[k].x);
+        lds_st(roff[k][1], rv[k].y);
+        lds_st(roff[k][2], rv[k].z);
+        lds_st(roff[k][3], rv[k].w);
       }
     }
     __syncthreads();

@@ -261,6 +261,21 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   auto prefetch = [&](int p) {
     const int bs = pass_rows(p);
     const bool live = bs > 0;
+    if constexpr (!GAUSS) {  // HEAD 0 / 2: the pass's rows are contiguous, element i of the block at row 0 + i
+      const float* xb = a.x + (live ? row_of(p, 0) * IN : 0);
+      const float* yb = a.y + (live ? row_of(p, 0) * OUT : 0);
+#pragma unroll
+      for (int k = 0; k < C::NXP; ++k) {
+        const int i = t + kMlTH * k;
+        xp[k] = (live && i < bs * IN) ? xb[i] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < C::NYP; ++k) {
+        const int i = t + kMlTH * k;
+        yp[k] = (live && i < bs * OUT) ? yb[i] : 0.f;
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
       const int i = t + kMlTH * k, r = i / IN;

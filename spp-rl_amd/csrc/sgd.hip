@@ -32,7 +32,10 @@ __device__ __forceinline__ float4 slab_ld4(__amdgpu_buffer_rsrc_t r, int idx) {
 __device__ __forceinline__ float slab_ld1(__amdgpu_buffer_rsrc_t r, int idx) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, 4u * (uint32_t)idx, 0, kSc1));
 }
-__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead) {
+// idle(): work of the workgroup's threads while lane 0 waits for the other workgroups (thread 0 runs it after
+// its poll); it must not touch the handed-over data
+template <class Idle>
+__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, Idle&& idle) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores are written through
   __syncthreads();                                   // ... and every other wave's
   if (threadIdx.x == 0 && !*s_dead) {
@@ -50,8 +53,12 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
       }
     }
   }
+  idle();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below the poll
   __syncthreads();
+}
+__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead) {
+  sgd_arrive_wait_wt(ctr, target, err, s_dead, [] {});
 }
 
 }  // namespace spp

@@ -707,7 +707,10 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           const float4 v4 = *reinterpret_cast<const float4*>(GR + 4 * f);
           slab_st4(mine, 4 * f, v4);
         }
-      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead);
+      // the next step's Adam scalars (thread 255's double-precision powers) while lane 0 polls
+      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, [&] {
+        if (t == kMlTH - 1) adam_scalars(st + 1);
+      });
       // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
       const int nit = c4n * G;
       for (int i0 = 0; i0 < nit; i0 += C::RLC * kMlTH) {  // (G = 17, 64-wide AcM: one round)
@@ -730,7 +733,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     }
     SPP_TP(6);
     const float neg_step = adam_s[st & 1][0], bc2s = adam_s[st & 1][1];
-    if (t == kMlTH - 1) adam_scalars(st + 1);
+    if (!MW && t == kMlTH - 1) adam_scalars(st + 1);  // (G > 1: computed during the arrival wait)
     const float omb1 = 0.1f, b2c = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     const auto pub = sgd_rsrc(a.pbuf);
 #pragma unroll

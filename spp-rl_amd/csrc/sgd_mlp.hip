@@ -250,7 +250,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     adam_s[st & 1][1] = (float)sqrt(1.0 - pw2);
   };
   // ---- register prefetch of one pass's rows (HEAD 1: through the step's indices in IDX)
-  float xp[C::NXP], yp[C::NYP], lpp = 0.f, advp = 0.f, dsum = 0.f;
+  float xp[C::NXP], yp[C::NYP], nxp[GAUSS ? C::NYP : 1], lpp = 0.f, advp = 0.f;
   auto row_of = [&](int p, int r) -> int64_t {
     if constexpr (GAUSS) return IDX[(p & 1) * R + r];
     else {
@@ -286,10 +286,9 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       const int i = t + kMlTH * k, r = i / OUT;
       const bool ok = live && i < bs * OUT;
       yp[k] = ok ? a.y[row_of(p, r) * OUT + i % OUT] : 0.f;
-      if constexpr (GAUSS) {  // the dist loss is data only: its per-step sum is taken here
-        const float e = ok ? yp[k] - a.nxt[row_of(p, r) * OUT + i % OUT] : 0.f;
-        dsum = fmaf(e, e, dsum);
-      }
+      // the dist loss is data only: its per-step sum is taken when the rows are staged (not here, where it
+      // would wait for these loads instead of leaving them in flight under the step)
+      if constexpr (GAUSS) nxp[k] = ok ? a.nxt[row_of(p, r) * OUT + i % OUT] : 0.f;
     }
     if constexpr (GAUSS) {
       lpp = (live && t < bs) ? a.lp_old[row_of(p, t)] : 0.f;
@@ -320,8 +319,15 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         ADV[t] = advp;
       }
     }
-    dist_next = dsum;
-    dsum = 0.f;
+    if constexpr (GAUSS) {
+      float dsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < C::NYP; ++k) {
+        const float e = yp[k] - nxp[k];  // (rows past the batch: 0 - 0)
+        dsum = fmaf(e, e, dsum);
+      }
+      dist_next = dsum;
+    }
   };
   load_idx(0);
   if (t == kMlTH - 1) adam_scalars(0);

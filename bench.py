@@ -780,7 +780,11 @@ def main():
                    "schedule": sched, "replay_rows_per_gpu": cap, "parallelism": "dp%d" % world,
                    "env": "host (HostSynthEnv, PCIe-inclusive)" if args.host_env else "device (SynthVecEnv)",
                    "obs_stats": "%s rate: %d passes over %d timed steps (one per %d frames)" % (
-                       args.stats_rate, stats["passes"], args.steps, batch_size)},
+                       args.stats_rate, stats["passes"], args.steps, batch_size),
+                   "index_rng": ("philox (sppRandIndex, device); the reference's MT19937 stream "
+                                 "(np.random.randint, replay_buffer.py:234) is bit-exact through sppMTRandint on "
+                                 "the E = 1 reference schedule only") if sched == "fused" else
+                                "MT19937 (np.random.randint stream, replay_buffer.py:234), host"},
         "roofline": {"bound": "mfma", "kernel": "%s (critic targets + critic fwd/bwd)" % kname,
                      "achieved": round(crit_tf, 3), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(crit_tf / peak, 5), "traffic": None,

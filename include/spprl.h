@@ -255,6 +255,14 @@ sppStatus sppAgentUnpackImage(sppAgentHandle h, int net, int i, float* out_dev, 
 /* Fused replay sample + gather into the agent's staging area (device indices). */
 sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int64_t* idx_dev, int B,
                                   void* stream);
+/* The rest of sample_batch / make_update on the staged batch, in place:
+ *   normalize          obs and next_obs through the bound normaliser (ReplayBuffer._sample_batch with
+ *                      obs_norm, rltoolkit/buffer/replay_buffer.py:247-249; min-max or z-score per the
+ *                      agent's min_max_denormalize, memory.py:76-88)
+ *   act_from_next_obs  the critic's action operand := the (normalised) next obs
+ *                      (DDPG_AcM.make_unbiased_update, rltoolkit/acm/off_policy/ddpg_acm.py:59-73:
+ *                      update(action=next_obs)); needs acm_critic = 0 and aout == ob. */
+sppStatus sppAgentStagePost(sppAgentHandle h, int normalize, int act_from_next_obs, void* stream);
 /* Update on the staged batch (after sppAgentStageFromReplay), eps drawn on
  * device from (seed, counter). */
 sppStatus sppSacAcmUpdateStaged(sppAgentHandle h, uint64_t seed, uint64_t counter, float* losses_dev,
@@ -444,8 +452,9 @@ sppStatus sppOnpActorApply(sppOnPolicyHandle h, void* stream);
  * (normalised advantages) and next_obs [n][aout] (the dist loss, data only; NULL: 0).  out4 [nsteps][4]:
  * each step's actor loss, KL (mean lp_old - lp_new before the step), dist MSE, entropy.  Parameters stay in
  * LDS for the launch; bs > 64 spreads each step over ceil(bs / 64) co-resident workgroups whose gradients
- * are summed in a fixed order (deterministic).  Single-process only (data-parallel ranks all-reduce every
- * minibatch gradient: sppOnpActorGrads / Apply).  Instantiated for (ob, aout) = (17, 17), (11, 11). */
+ * are summed in a fixed order (deterministic).  Data-parallel PPO_AcM runs it on every rank over the all-gathered
+ * union batch (replicated, no per-step exchange; sppOnpActorGrads / Apply + an all-reduce remain for callers
+ * that shard the minibatch).  Instantiated for (ob, aout) = (17, 17), (11, 11). */
 sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
                            const float* adv, const float* next_obs, const int64_t* idx, int nrows, int bs,
                            float* out4, void* stream);
@@ -454,18 +463,28 @@ int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);
 /* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch / sppOnpCriticSteps launch timed out at an arrival
  * barrier, else 0. */
 sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
+/* Stream-ordered form (the product path: PPO_AcM.update_critic / update_actor, acm/on_policy.py:164-216,
+ * a2c.py:186-225): enqueues a copy of the handle's sticky timeout flag into *timed_out_pinned (pinned host
+ * memory, read once the stream has passed this point); 0 is written when no multi-workgroup launch ran. */
+sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle h, int* timed_out_pinned, void* stream);
+/* Test hook (no reference counterpart): polls before an arrival wait of any persistent SGD launch
+ * (sppAcmSgd*, sppOnpActorEpoch, sppOnpCriticSteps) times out; 0 restores the default (~0.2 s).  A tiny limit
+ * makes the first workgroup to arrive time out, which is how the tests force the timeout path. */
+sppStatus sppSetSgdSpinLimit(int polls);
 /* A2C.update_critic's inner loop (rltoolkit/algorithms/a2c/a2c.py:186-225): nsteps sequential full-batch
  * steps of 0.5 * mean((q - V(x))^2) + Adam at critic_lr on the same N rows (x [N][ob] normalised obs, q [N]
  * targets), in ONE launch: every workgroup runs ceil(rows / 64) passes of its share of the N rows, the
  * gradient is summed over the workgroups in a fixed order (deterministic), parameters stay in LDS.
- * loss_sum += sum over the steps of each step's loss.  Single-process only (data-parallel ranks all-reduce
- * each step: sppOnpCriticGrads / Apply).  N <= sppOnpCriticStepsMaxBatch; ob 17 and 11 instantiated. */
+ * loss_sum += sum over the steps of each step's loss.  Data-parallel PPO_AcM runs it on every rank over the
+ * all-gathered union batch (replicated; sppOnpCriticGrads / Apply + an all-reduce remain for callers that shard
+ * the batch).  N <= sppOnpCriticStepsMaxBatch (up to 64 passes of 64 rows per workgroup); ob 17 and 11. */
 sppStatus sppOnpCriticSteps(sppOnPolicyHandle h, const float* x, const float* q, int N, int nsteps, float* loss_sum,
                             void* stream);
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle h);
-/* Leave n workgroup slots of the device to a persistent launch running concurrently on another stream (the
- * PPO_AcM ACM epochs beside update(mem)): sppOnpCriticSteps / sppOnpActorEpoch size their grids from the
- * co-resident capacity minus n, so both grids stay resident at once.  0 restores the whole device. */
+/* Leave n CUs of the device to a persistent launch of n workgroups running concurrently on another stream
+ * (the PPO_AcM ACM epochs beside update(mem); every k_mlp_sgd workgroup fills a CU's LDS):
+ * sppOnpCriticSteps / sppOnpActorEpoch size their grids from the co-resident capacity minus n x their own
+ * per-CU occupancy, so both grids stay resident at once.  0 restores the whole device. */
 sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle h, int n);
 /* Actor.act (basic_model.py:32-51) continuous: a = mu + exp(log_scale) * eps (eps NULL:
  * deterministic mu), logp = Independent(Normal).log_prob(a). */

@@ -1868,6 +1868,20 @@ sppStatus sppAgentStageFromReplay(sppAgentHandle a, sppReplayHandle r, const int
   return SPP_OK;
 }
 
+sppStatus sppAgentStagePost(sppAgentHandle a, int normalize, int act_from_next_obs, void* stream) {
+  SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "stage_post: no staged batch");
+  if (!normalize && !act_from_next_obs) return SPP_OK;
+  SPP_REQUIRE(!act_from_next_obs || (!a->cfg.acm_critic && a->cfg.aout == a->cfg.ob && a->ACT), SPP_E_INVALID_ARG,
+              "stage_post: action = next_obs needs a critic on (obs, actor output) with aout == ob");
+  SPP_REQUIRE(!normalize || (a->cfg.min_max_denormalize ? (a->lo && a->hi) : (a->mean && a->std)), SPP_E_STATE,
+              "stage_post: normalizer not bound");
+  const int B = a->cur_B, Bp = (int)round_up(B, 32), ob = a->cfg.ob;
+  hipLaunchKernelGGL(k_stage_post, dim3(cdiv((int64_t)ob * B, 256)), dim3(256), 0, S(stream), a->S, a->S2, a->ACT, ob,
+                     B, Bp, a->lo, a->hi, a->mean, a->std, a->cfg.min_max_denormalize, normalize, act_from_next_obs);
+  SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
 sppStatus sppSacAcmUpdateStaged(sppAgentHandle a, uint64_t seed, uint64_t counter, float* losses, void* stream) {
   SPP_REQUIRE(a && a->cur_B > 0, SPP_E_STATE, "no staged batch");
   hipStream_t st = S(stream);
@@ -1955,6 +1969,9 @@ int sppAcmSgdMaxBatch(sppAgentHandle a) {
   return kMlR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
 }
 
+// polls before a k_mlp_sgd arrival wait times out (0: the kernel's default); test hook sppSetSgdSpinLimit
+static int g_sgd_spin = 0;
+
 // slabs [2][kMlMaxWG][kMlSlabMax] + the parameter buffer + {arrival counter, timeout flag}
 static sppStatus mlp_sgd_buffers(DevArray<float>& slab, DevArray<int>& sync, hipStream_t st) {
   if (!slab.ptr) {
@@ -1990,7 +2007,7 @@ static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, i
   MlpSgdArgs g{};
   g.x = x; g.y = y; g.nsteps = nsteps; g.bs = bs; g.bsl = bs; g.bs_last = bs_last;
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = a->cfg.acm_lr; g.step0 = a->steps[3];
-  g.lim = a->limits.ptr + a->cfg.aout; g.loss_sum = loss_sum;
+  g.lim = a->limits.ptr + a->cfg.aout; g.loss_sum = loss_sum; g.spin = g_sgd_spin;
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
   // 64 rows per workgroup (sgd_mlp.hip); the per-step arrival barriers need every workgroup resident at once
@@ -2164,7 +2181,7 @@ struct sppOnPolicy {
   DevArray<int> sgd_sync;
   int sgd_max_wg = -1;
   int crit_max_wg = -1;  // co-resident persistent-critic workgroups (onp_critic_max_wg, cached)
-  int wg_reserve = 0;    // workgroup slots left to a persistent launch on another stream (sppOnpReserveWorkgroups)
+  int wg_reserve = 0;    // CUs left to a persistent launch on another stream (sppOnpReserveWorkgroups)
 };
 
 static sppStatus onp_packs(sppOnPolicy* o) {
@@ -2447,9 +2464,16 @@ static int onp_epoch_max_wg(sppOnPolicy* o) {
   return n;
 }
 
+// slots of a kernel with `full` co-resident workgroups on the device that the reserved CUs take away: each
+// reserved CU held a whole workgroup of the concurrent launch (k_mlp_sgd's LDS, > 80 KB for every
+// instantiation, fits one per CU), so it removes this kernel's per-CU occupancy, not one slot
+static int onp_reserved_slots(sppOnPolicy* o, int full) {
+  return o->wg_reserve * std::max(1, cdiv(full, std::max(1, o->num_cu)));
+}
+
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
   if (!o) return 0;
-  const int n = onp_epoch_max_wg(o) - o->wg_reserve;
+  const int n = onp_epoch_max_wg(o) - onp_reserved_slots(o, onp_epoch_max_wg(o));
   return n > 0 ? kMlR * n : 0;
 }
 
@@ -2459,7 +2483,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
               "actor epoch: bad args");
   const int nsteps = cdiv(nrows, bs);
   SPP_REQUIRE(o->net[0].p && o->net[0].m && o->net[0].v && o->lim.ptr, SPP_E_STATE, "actor epoch: actor not bound");
-  const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o) - o->wg_reserve;
+  const int nwg = cdiv(bs, kMlR), maxwg = onp_epoch_max_wg(o) - onp_reserved_slots(o, onp_epoch_max_wg(o));
   SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "actor epoch: no instantiation for ob=%d aout=%d", o->cfg.ob, o->cfg.aout);
   SPP_REQUIRE(nwg <= maxwg, SPP_E_SHAPE, "actor epoch: batch %d needs %d co-resident workgroups > %d", bs, nwg, maxwg);
   if (nsteps == 0) return SPP_OK;
@@ -2470,6 +2494,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
   const NetBufs& n = o->net[0];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.actor_lr; g.step0 = o->steps[0];
   g.lim = o->lim.ptr; g.eps_clip = o->cfg.ppo_epsilon; g.ent_coef = o->cfg.entropy_coef; g.out = out4;
+  g.spin = g_sgd_spin;
   if (nwg > 1) {
     g.bsl = cdiv(bs, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2492,7 +2517,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
 }
 
 // persistent critic steps (HEAD 2): co-resident workgroups, passes of 64 rows per workgroup and step
-constexpr int kCriticMaxPasses = 8;
+constexpr int kCriticMaxPasses = 64;  // (the data-parallel PPO union batch: world x 32,768 rows)
 // slots the critic grid always leaves free (a concurrent ACM grid of up to 64 workgroups: PPO_AcM), so that
 // its row partition -- and with it the gradient's summation order -- is the same with or without one
 constexpr int kCriticSideSlots = 64;
@@ -2509,12 +2534,16 @@ static int onp_critic_max_wg(sppOnPolicy* o) {
 
 static int onp_critic_budget(sppOnPolicy* o) {
   const int full = onp_critic_max_wg(o);
-  return std::max(0, full > kCriticSideSlots ? full - std::max(o->wg_reserve, kCriticSideSlots) : full - o->wg_reserve);
+  const int res = onp_reserved_slots(o, full);
+  return std::max(0, full > kCriticSideSlots ? full - std::max(res, kCriticSideSlots) : full - res);
 }
 
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle o) {
   if (!o) return 0;
-  return kMlR * kCriticMaxPasses * onp_critic_budget(o);
+  const int b = onp_critic_budget(o);
+  // one workgroup takes one 64-row pass per step (its single-workgroup form has no passes): batches of more
+  // than one tile need >= 2 co-resident workgroups
+  return b >= 2 ? kMlR * kCriticMaxPasses * b : (b == 1 ? kMlR : 0);
 }
 
 sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle o, int n) {
@@ -2529,8 +2558,12 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
   SPP_REQUIRE(o->net[1].p && o->net[1].m && o->net[1].v && o->lim.ptr, SPP_E_STATE, "critic steps: critic not bound");
   const int maxwg = onp_critic_budget(o);
   SPP_REQUIRE(maxwg > 0, SPP_E_SHAPE, "critic steps: no instantiation for ob=%d (or every slot reserved)", o->cfg.ob);
-  // fewest passes per workgroup the co-resident grid allows, then the fewest workgroups for that many passes
-  const int tiles = cdiv(N, kMlR), passes = cdiv(tiles, maxwg), nwg = cdiv(tiles, passes);
+  // fewest passes per workgroup the co-resident grid allows, then the fewest workgroups for that many passes;
+  // more than one tile always runs the multi-workgroup form (G >= 2: the single-workgroup kernel makes one
+  // 64-row pass per step)
+  const int tiles = cdiv(N, kMlR);
+  SPP_REQUIRE(tiles == 1 || maxwg >= 2, SPP_E_SHAPE, "critic steps: batch %d needs >= 2 co-resident workgroups", N);
+  const int passes = tiles == 1 ? 1 : cdiv(tiles, maxwg), nwg = tiles == 1 ? 1 : std::max(2, cdiv(tiles, passes));
   SPP_REQUIRE(passes <= kCriticMaxPasses, SPP_E_SHAPE, "critic steps: batch %d > %d", N, kMlR * kCriticMaxPasses * maxwg);
   if (nsteps == 0) return SPP_OK;
   hipStream_t st = S(stream);
@@ -2538,7 +2571,7 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
   g.x = x; g.y = q; g.nsteps = nsteps; g.bs = N; g.bsl = N; g.bs_last = N;
   const NetBufs& n = o->net[1];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.critic_lr; g.step0 = o->steps[1];
-  g.lim = o->lim.ptr; g.loss_sum = loss_sum;
+  g.lim = o->lim.ptr; g.loss_sum = loss_sum; g.spin = g_sgd_spin;
   if (nwg > 1) {
     g.bsl = cdiv(N, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2557,6 +2590,21 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
 #undef SPP_CRITIC_LAUNCH
   o->steps[1] += nsteps;
   SPP_CHECK_HIP(hipGetLastError());
+  return SPP_OK;
+}
+
+sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle o, int* timed_out_pinned, void* stream) {
+  SPP_REQUIRE(o && timed_out_pinned, SPP_E_INVALID_ARG, "onp sync status async: null");
+  if (o->sgd_sync.ptr)
+    SPP_CHECK_HIP(hipMemcpyAsync(timed_out_pinned, o->sgd_sync.ptr + 1, sizeof(int), hipMemcpyDeviceToHost, S(stream)));
+  else
+    *timed_out_pinned = 0;
+  return SPP_OK;
+}
+
+sppStatus sppSetSgdSpinLimit(int polls) {
+  SPP_REQUIRE(polls >= 0, SPP_E_INVALID_ARG, "spin limit: negative");
+  g_sgd_spin = polls;
   return SPP_OK;
 }
 

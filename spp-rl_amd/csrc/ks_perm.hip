@@ -34,10 +34,13 @@ using namespace spp;
 
 extern "C" {
 
-// scratch layout: keys_in [n] u64 | keys_out [n] u64 | idx_in [n] i64 | the sort's temporary storage
+// scratch layout: keys_in [n] u64 | keys_out [n] u64 | idx_in [n] i64 | pad to 256 B | the sort's temporary
+// storage (256-byte aligned like a hipMalloc block, whatever n: 24 n is only 8-byte aligned for odd n)
+static size_t perm_tmp_offset(int64_t n) { return ((3 * (size_t)n * 8 + 255) / 256) * 256; }
+
 int64_t sppRandPermScratchBytes(int64_t n) {
   if (n <= 0) return 0;
-  return (int64_t)(3 * (size_t)n * 8 + ((perm_sort_bytes(n) + 255) / 256) * 256);
+  return (int64_t)(perm_tmp_offset(n) + ((perm_sort_bytes(n) + 255) / 256) * 256);
 }
 
 sppStatus sppRandPerm(int64_t* out, int64_t n, uint64_t seed, uint64_t offset, void* scratch, int64_t scratch_bytes,
@@ -49,8 +52,8 @@ sppStatus sppRandPerm(int64_t* out, int64_t n, uint64_t seed, uint64_t offset, v
   uint64_t* keys_in = reinterpret_cast<uint64_t*>(base);
   uint64_t* keys_out = keys_in + n;
   int64_t* idx_in = reinterpret_cast<int64_t*>(keys_out + n);
-  void* tmp = idx_in + n;
-  size_t tmp_bytes = (size_t)scratch_bytes - 3 * (size_t)n * 8;
+  void* tmp = base + perm_tmp_offset(n);
+  size_t tmp_bytes = (size_t)scratch_bytes - perm_tmp_offset(n);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_perm_keys, dim3((unsigned)blocks), dim3(256), 0, st, keys_in, idx_in, n, seed, offset);
   if (hipGetLastError() != hipSuccess) return SPP_E_HIP;

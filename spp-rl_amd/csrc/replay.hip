@@ -691,22 +691,42 @@ __global__ void k_synth_reset(float* obs, const uint8_t* mask, int E, int ob, ui
 // over [rows][ob], the same fp32 operation order as the fused device helpers:
 //   min-max : (x - mid) / (hi - mid + 1e-8)     |  mid + x * (hi - lo) / 2
 //   z-score : clamp((x - mean) / (std + 1e-8), -10, 10)  |  (std + 1e-8) * x + mean
+__device__ __forceinline__ float obs_norm1(float v, int j, const float* lo, const float* hi, const float* mean,
+                                           const float* std, int min_max, int inverse) {
+  if (min_max) {
+    const float l = lo[j], h = hi[j];
+    const float mid = fadd_rn(h, l) * 0.5f;
+    return inverse ? fadd_rn(mid, fmul_rn(v, fsub_rn(h, l) * 0.5f))
+                   : fdiv_rn(fsub_rn(v, mid), fadd_rn(fsub_rn(h, mid), 1e-8f));
+  }
+  return inverse ? fadd_rn(fmul_rn(fadd_rn(std[j], 1e-8f), v), mean[j])
+                 : fminf(fmaxf(fdiv_rn(fsub_rn(v, mean[j]), fadd_rn(std[j], 1e-8f)), -10.f), 10.f);
+}
+
 __global__ void k_obs_normalize(const float* __restrict__ x, int64_t n, int ob, const float* lo, const float* hi,
                                 const float* mean, const float* std, int min_max, int inverse, float* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int j = (int)(i % ob);
-  const float v = x[i];
-  float r;
-  if (min_max) {
-    const float l = lo[j], h = hi[j];
-    const float mid = fadd_rn(h, l) * 0.5f;
-    r = inverse ? fadd_rn(mid, fmul_rn(v, fsub_rn(h, l) * 0.5f)) : fdiv_rn(fsub_rn(v, mid), fadd_rn(fsub_rn(h, mid), 1e-8f));
-  } else {
-    r = inverse ? fadd_rn(fmul_rn(fadd_rn(std[j], 1e-8f), v), mean[j])
-                : fminf(fmaxf(fdiv_rn(fsub_rn(v, mean[j]), fadd_rn(std[j], 1e-8f)), -10.f), 10.f);
+  out[i] = obs_norm1(x[i], (int)(i % ob), lo, hi, mean, std, min_max, inverse);
+}
+
+// The staged batch's sample_batch tail (replay_buffer.py:247-249) and DDPG_AcM.make_unbiased_update
+// (acm/off_policy/ddpg_acm.py:59-73) on the feature-major staging arrays [ob][Bp]: with `norm`, the staged
+// obs and next obs are normalised in place (the buffer's obs_norm); with `act_next`, the critic's action
+// operand becomes the (normalised) next obs.  Columns b >= B (padding) stay zero.
+__global__ void k_stage_post(float* S, float* S2, float* ACT, int ob, int B, int Bp, const float* lo, const float* hi,
+                             const float* mean, const float* std, int min_max, int norm, int act_next) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)ob * B) return;
+  const int f = (int)(i / B), b = (int)(i - (int64_t)f * B);
+  const int64_t o = (int64_t)f * Bp + b;
+  float s2 = S2[o];
+  if (norm) {
+    S[o] = obs_norm1(S[o], f, lo, hi, mean, std, min_max, 0);
+    s2 = obs_norm1(s2, f, lo, hi, mean, std, min_max, 0);
+    S2[o] = s2;
   }
-  out[i] = r;
+  if (act_next) ACT[o] = s2;
 }
 
 }  // namespace spp

@@ -8,8 +8,8 @@
 namespace spp {
 
 // Arrival barrier of the multi-workgroup SGD.  The counter address is kept in a VGPR so the add and the
-// polls are vector-memory operations.  Bounded: a wait that times out sets *err and every later wait of
-// the launch returns at once.
+// polls are vector-memory operations.  Bounded: after `spin` polls (0: kSgdSpins, ~0.2 s) a wait times out,
+// sets *err and every later wait of the launch returns at once.
 // The per-step gradient hand-over between the workgroups is write-through: every slab word is stored
 // sc1 (aux 16) and every load of slab words is an sc1 load, so the arrival needs no agent-scope release
 // (its L2 write-back cost ~6.5 us per step with a freshly written 18 KB slab) and no acquire
@@ -34,8 +34,9 @@ __device__ __forceinline__ float slab_ld1(__amdgpu_buffer_rsrc_t r, int idx) {
 }
 // idle(): work of the workgroup's threads while lane 0 waits for the other workgroups (thread 0 runs it after
 // its poll); it must not touch the handed-over data
+constexpr int kSgdSpins = 1 << 23;
 template <class Idle>
-__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, Idle&& idle) {
+__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, int spin, Idle&& idle) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores are written through
   __syncthreads();                                   // ... and every other wave's
   if (threadIdx.x == 0 && !*s_dead) {
@@ -43,10 +44,11 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
     asm volatile("" : "+v"(off));
     int* c = ctr + off;
     __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int limit = spin > 0 ? spin : kSgdSpins;
     int spins = 0;
     while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 23)) {
+      if (++spins > limit) {
         *s_dead = 1;
         err[off] = 1;
         break;
@@ -57,8 +59,8 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below the poll
   __syncthreads();
 }
-__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead) {
-  sgd_arrive_wait_wt(ctr, target, err, s_dead, [] {});
+__device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, int spin) {
+  sgd_arrive_wait_wt(ctr, target, err, s_dead, spin, [] {});
 }
 
 }  // namespace spp

@@ -67,6 +67,7 @@ struct MlpSgdArgs {
   float* pbuf;           // G > 1: [param floats] the new parameters of each step
   int* ctr;              // arrival counter (zeroed per launch)
   int* err;              // set to 1 if an arrival wait timed out
+  int spin;              // polls before an arrival wait times out (sppSetSgdSpinLimit; 0: the default)
 };
 
 template <int IN, int H2, int OUT, int HEAD>
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
           slab_st4(mine, 4 * f, v4);
         }
       // the next step's Adam scalars (thread 255's double-precision powers) while lane 0 polls
-      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, [&] {
+      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, a.spin, [&] {
         if (t == kMlTH - 1) adam_scalars(st + 1);
       });
       // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
@@ -790,7 +791,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     stage(p);
     SPP_TP(7);
     if constexpr (MW) {
-      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead);
+      sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead, a.spin);
       float4 rv[C::NL];
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {  // (this shard's own slots reload the values it published)

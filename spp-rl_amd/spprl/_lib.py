@@ -98,6 +98,7 @@ _SIGS = {
     "sppSacAcmActorGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "sppSacAcmActorApply": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppAgentStageFromReplay": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "sppAgentStagePost": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "sppSacAcmUpdateStaged": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "sppAcmRegressStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "sppPolicyAct": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p,
@@ -159,6 +160,8 @@ _SIGS = {
     "sppOnpReserveWorkgroups": (c_int, [c_void_p, c_int]),
     "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),
     "sppOnpActorEpochStatus": (c_int, [c_void_p, c_void_p]),
+    "sppOnpSyncStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "sppSetSgdSpinLimit": (c_int, [c_int]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppAcmSgdMaxBatch": (c_int, [c_void_p]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),

@@ -46,6 +46,36 @@ ENV_SPECS = {
 }
 
 
+# Reference constructor kwargs the device path accepts and that change nothing it computes (the reason for
+# each).  Any other keyword an agent does not take explicitly raises TypeError, as the reference's own
+# constructor chain does (MetaLearner.__init__, rl.py:17-26, takes no **kwargs).
+NO_EFFECT_KWARGS = {
+    "use_gpu": "device placement is the `device` argument (rl.py:40)",
+    "tensorboard_comment": "event-file name suffix only (rl.py:68-70, 310)",
+    "log_dir": "basic text logs / final-model directory (rl.py:177-181, 221, 234, 316)",
+    "verbose": "console log level (rl.py:182, 332)",
+    "render": "rollout video to TensorBoard (rl.py:81, 183): out of scope (DESIGN §7)",
+    "acm_val_buffer_size": "validation buffer for the logged loss['acm_val'] only (acm.py:140-146, 301-303); "
+                           "never enters a gradient",
+    "pi_update_freq": "stored for hparams only: its use is commented out (sac.py:260, sac_acm.py:139)",
+}
+ON_POLICY_NO_EFFECT_KWARGS = dict(NO_EFFECT_KWARGS, **{
+    "tensorboard_dir": "PPO_AcM logs no TensorBoard panels on this path",
+    "debug_mode": "extra TensorBoard panels only (on_policy.py:128-131)",
+    "obs_norm_alpha": "redundant in the AcM path: A2C_AcM warns and never updates a running Memory "
+                      "normaliser (on_policy.py:138-144, 63-86)",
+})
+
+
+def check_kwargs(owner, kw, allowed=None):
+    """Raise TypeError for keywords neither taken explicitly nor listed in ``allowed`` (NO_EFFECT_KWARGS)."""
+    allowed = NO_EFFECT_KWARGS if allowed is None else allowed
+    bad = sorted(k for k in kw if k not in allowed)
+    if bad:
+        raise TypeError("%s got unexpected keyword argument(s): %s (accepted with no effect: %s)"
+                        % (owner, ", ".join(bad), ", ".join(sorted(allowed))))
+
+
 def default_max_batch(update_batch_size, kw):
     """Largest batch the agent's device scratch must hold when the caller gives no
     ``max_batch``: the reference batch, or with E > 1 envs the fused schedule's rho*E

@@ -28,7 +28,9 @@ class DDPG_AcM(OffPolicyLoop):
                  update_batch_size=config.UPDATE_BATCH_SIZE, buffer_size=config.BUFFER_SIZE, acm_lr=config.ACM_LR,
                  acm_critic=config.ACM_CRITIC, custom_loss=0.0, norm_closs=config.NORM_CLOSS,
                  min_max_denormalize=config.MIN_MAX_DENORMALIZE, denormalize_actor_out=config.DENORMALIZE_ACTOR_OUT,
-                 obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None, seed=None, **unused):
+                 obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None, seed=None,
+                 unbiased_update=False, **loop_kw):
+        self._check_kwargs(loop_kw)
         _lib.load()
         ob, ac, ac_high, _ = env_spec or config.ENV_SPECS[env_name]
         self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
@@ -38,11 +40,12 @@ class DDPG_AcM(OffPolicyLoop):
         self.act_noise = act_noise
         self.update_batch_size = update_batch_size
         self.acm_critic, self.custom_loss, self.norm_closs = bool(acm_critic), float(custom_loss), bool(norm_closs)
+        self.unbiased_update = bool(unbiased_update)  # make_unbiased_update (ddpg_acm.py:59-79)
         self.min_max_denormalize, self.denormalize_actor_out = bool(min_max_denormalize), bool(denormalize_actor_out)
         self.actor_output_dim = aout = ob
         lim = 1.0 if self.min_max_denormalize else float(config.MAX_ABS_OBS_VALUE)  # acm.py:102-108
         self.actor_ac_lim = torch.full((aout,), lim)
-        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, unused))
+        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, loop_kw))
         cin = ob + (ac if self.acm_critic else aout)
         self.layouts = {_lib.SPP_NET_ACTOR: nets.ddpg_actor_layout(ob, aout),
                         _lib.SPP_NET_ACTOR_TARG: nets.ddpg_actor_layout(ob, aout),
@@ -81,12 +84,12 @@ class DDPG_AcM(OffPolicyLoop):
         call("sppAgentSetLimits", self._h, a_lim.ctypes.data_as(ctypes.c_void_p), m_lim.ctypes.data_as(ctypes.c_void_p))
         self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
                                                 min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm,
-                                                n_envs=int(unused.get("n_envs", 1)))
+                                                n_envs=int(loop_kw.get("n_envs", 1)))
         rb = self.replay_buffer
         call("sppAgentBindNormalizer", self._h, ptr(rb.min_obs), ptr(rb.max_obs), ptr(rb.obs_mean), ptr(rb.obs_std))
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
         self.acm_kind = "basic"  # BasicAcM: per-step regression path
-        self._init_loop(update_batch_size=update_batch_size, **unused)
+        self._init_loop(update_batch_size=update_batch_size, **loop_kw)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -114,7 +117,7 @@ class DDPG_AcM(OffPolicyLoop):
     def update_from_replay_dp(self, idx, allreduce=None):
         """Device-sampled step split at its exchange points (allreduce averages a flat bucket)."""
         st = stream_handle()
-        call("sppAgentStageFromReplay", self._h, self.replay_buffer._h, ptr(idx), idx.numel(), st)
+        self._stage(idx)
         call("sppDdpgAcmCriticGrads", self._h, None, ptr(self._losses), st)
         if allreduce is not None:
             allreduce(self.bucket_critic)

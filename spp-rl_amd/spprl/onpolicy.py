@@ -130,8 +130,11 @@ class OnPolicyNets:
                 continue
             for _ in range(self.num_critic_updates_per_target):
                 total += self.critic_step(obs, q)
+        if one_launch:
+            self._sync_flag_copy()
         self.loss["critic"] = float(total.item()) / (self.critic_num_target_updates *
                                                      self.num_critic_updates_per_target)
+        self._sync_check()
         with torch.no_grad():
             q = rew + self.gamma * (1 - done) * self.value(next_obs)
             return q - self.value(obs)
@@ -192,6 +195,7 @@ class OnPolicyNets:
             if one_launch:  # the whole epoch in one persistent launch (the ragged last minibatch included)
                 call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
                      ptr(perm), N, mb, ptr(outs), stream_handle())
+                self._sync_flag_copy()
                 self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
             else:
                 # one permuted copy per epoch: every minibatch is then a contiguous slice
@@ -203,6 +207,7 @@ class OnPolicyNets:
                                     out=outs[k])
             sums += outs.sum(0)
             kl = float(outs[-1, 1].item())  # KL of the epoch's last minibatch (ppo.py:188)
+            self._sync_check()
         # the reference divides by i + 1 after the loop: the epochs run when none stopped early, one more than
         # that when the KL check broke the loop (on_policy.py:210-216, ppo.py:190-192)
         s = sums.cpu().numpy().astype(np.float64)
@@ -236,6 +241,28 @@ class OnPolicyNets:
         if getattr(self, "_epoch_max_bs", None) is None:
             self._epoch_max_bs = int(_lib.load().sppOnpActorEpochMaxBatch(self._h))
         return mb <= self._epoch_max_bs
+
+    def _sync_flag_copy(self):
+        """Enqueue a copy of the persistent launches' timeout flag (sppOnpSyncStatusAsync) into pinned memory on
+        the current stream; _sync_check reads it once the stream has passed that point."""
+        if getattr(self, "_sync_flag", None) is None:
+            self._sync_flag = torch.zeros(1, dtype=torch.int32).pin_memory()
+        call("sppOnpSyncStatusAsync", self._h, self._sync_flag.data_ptr(), stream_handle())
+        self._sync_ev = torch.cuda.Event()
+        self._sync_ev.record()
+
+    def _sync_check(self):
+        """Raise SppError if a multi-workgroup sppOnpCriticSteps / sppOnpActorEpoch launch timed out at an arrival
+        barrier (its parameters are then invalid).  Called right after the host synchronisation the update makes
+        anyway (the critic loss, each epoch's KL), which the flag copy precedes on the stream: no extra wait."""
+        ev = getattr(self, "_sync_ev", None)
+        if ev is None:
+            return
+        ev.synchronize()
+        self._sync_ev = None
+        if int(self._sync_flag[0]):
+            raise _lib.SppError("sppOnpCriticSteps / sppOnpActorEpoch: a multi-workgroup step timed out at its arrival "
+                                "barrier; the critic / actor parameters are invalid")
 
     def check_actor_epochs(self):
         """Raise if a multi-workgroup sppOnpActorEpoch launch timed out at an arrival barrier."""

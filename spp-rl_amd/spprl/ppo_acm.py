@@ -47,7 +47,14 @@ class PPO_AcM:
                  acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, acm_ring_size=None,
                  iterations=1001,
                  stats_freq=1, test_episodes=None, return_done=None, max_frames=None, n_envs=1, env=None,
-                 env_spec=None, device="cuda", seed=None, loop_seed=0, **unused):
+                 env_spec=None, device="cuda", seed=None, loop_seed=0, epsilon=None, obs_norm=False, **unused):
+        # unknown keywords raise (the reference's MetaLearner takes no **kwargs, rl.py:17-26); `epsilon` is the
+        # reference's name of the clip range (PPO.__init__, ppo.py:17), ppo_epsilon this class's older one
+        config.check_kwargs("PPO_AcM", unused, config.ON_POLICY_NO_EFFECT_KWARGS)
+        if obs_norm:
+            raise NotImplementedError("PPO_AcM with obs_norm=True (a normalised ACM ring) is not on the device path")
+        if epsilon is not None:
+            ppo_epsilon = epsilon
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
         self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
         self.device = torch.device(device)
@@ -67,13 +74,18 @@ class PPO_AcM:
         self.n_envs = E = env.n
         self.T = 1 if E == 1 else max(1, -(-self.batch_size // E))
         Nmax = max(self.T * E, self.batch_size + (max_ep or 1000) if E == 1 else 0)
+        from .dp import make_allreduce
+
+        import torch.distributed as dist
+
+        dp_world = dist.get_world_size() if make_allreduce() is not None else 1  # (the union: world x N rows)
         self.nets = OnPolicyNets(ob, ob, ac_lim=lim, actor_lr=actor_lr, critic_lr=critic_lr, ppo_epsilon=ppo_epsilon,
                                  entropy_coef=entropy_coef, gamma=gamma, gae_lambda=gae_lambda,
                                  critic_num_target_updates=critic_num_target_updates,
                                  num_critic_updates_per_target=num_critic_updates_per_target,
                                  max_ppo_epochs=max_ppo_epochs, ppo_batch_size=ppo_batch_size,
                                  kl_div_threshold=kl_div_threshold, normalize_adv=normalize_adv,
-                                 max_batch=max(Nmax, ppo_batch_size), device=self.device, seed=seed,
+                                 max_batch=max(dp_world * Nmax, ppo_batch_size), device=self.device, seed=seed,
                                  custom_loss=custom_loss)
         # the AcM and its replay ring (acm.py:127-141: size = pre-train samples * 1.1)
         ring = int(acm_ring_size or acm_pre_train_samples * 1.1)
@@ -90,16 +102,23 @@ class PPO_AcM:
         # order, at the end of each iteration: ReplayBufferAcM.add_buffer, replay_buffer.py:284-297), so the
         # ACM epochs (acm.py:266-303) run on identical rings with one permutation stream and need no
         # per-batch collective, and the ring's obs statistics are global without a collective either.
-        import torch.distributed as dist
-
-        self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
+        # Data parallel (self.dp: a process group with more than one rank, or SPP_DP_FORCE=1's one-rank rehearsal):
+        # the on-policy batch is REPLICATED too -- one all-gather of the ranks' rollouts per iteration, the union
+        # ordered rank-major along the env axis ([T][world * E]) -- and every rank runs update(mem) (critic
+        # targets, GAE, the persistent sppOnpCriticSteps / sppOnpActorEpoch launches) on the identical union with
+        # one permutation stream: no per-step gradient exchange, replicas bit-identical, and the result is one
+        # process's update on the union batch (acm/on_policy.py:72-75, a2c.py:186-225, ppo.py:152-192)
+        self.dp = self.nets.allreduce is not None
+        self.world = dist.get_world_size() if self.dp else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
+        self.nets.allreduce = self.nets.allreduce_sum = None  # (the nets see the union: no per-step exchange)
+        self.nets.world = 1
         if self.world > 1 and E == 1:
             # one env per rank collects whole episodes: the ranks' ring-write records ("start" per episode)
             # then differ in count and kind, which the rank-major all-gather of _flush_ring cannot carry
             raise ValueError("PPO_AcM data parallel needs n_envs > 1 per rank (vectorized lockstep envs); "
                              "got n_envs = 1 with world = %d" % self.world)
-        if self.nets.allreduce is not None:
+        if self.dp:  # the replicated ring needs no gradient or statistics exchange either
             self.acm.allreduce = self.acm.allreduce_sum = self.acm.host_sum = None
         self.acm._perm_seed = int(seed or 0) * 7919 + 17  # rank-independent epoch permutations
         self._ring_log = []  # this iteration's ring writes (applied by _flush_ring)
@@ -200,6 +219,8 @@ class PPO_AcM:
         next rollout wait for both, as in the reference's order.  The results are the serial order's."""
         self._ret_sums.zero_()
         mem = self.collect_batch()
+        if self.dp:
+            mem = self._union(mem)  # every rank's rollout, before the ACM's side stream starts
         acm_now = bool(self.acm_update_freq) and self.iteration % self.acm_update_freq == 0
         side = self._acm_side_stream() if acm_now else None
         if side is not None:
@@ -234,11 +255,13 @@ class PPO_AcM:
             self.acm.update_acm(self.acm_epochs)
 
     def _acm_side_stream(self):
-        """The side stream of the concurrent ACM update, or None: single process, CUDA device, persistent ACM
-        SGD eligible (one launch per epoch), and the env var SPP_PPO_ACM_OVERLAP not 0."""
+        """The side stream of the concurrent ACM update, or None: CUDA device, persistent ACM SGD eligible (one
+        launch per epoch), and the env var SPP_PPO_ACM_OVERLAP not 0.  Data parallel too: the iteration's
+        collectives (the ring flush, the rollout union) are all issued before the side stream starts, and the
+        ACM epochs themselves exchange nothing (replicated ring)."""
         import os
 
-        if os.environ.get("SPP_PPO_ACM_OVERLAP", "1") == "0" or self.world > 1 or self.device.type != "cuda":
+        if os.environ.get("SPP_PPO_ACM_OVERLAP", "1") == "0" or self.device.type != "cuda":
             return None
         if not self.acm._acm_sgd_ok(self.acm.acm_batch_size):
             return None
@@ -379,9 +402,40 @@ class PPO_AcM:
         self._ring_log.append(("step", out[6], out[3], done, out[5], env_act.clone(), mask, robs))
         return out
 
+    # ---------------------------------------------------------------- data parallel: the rollout union
+    def _union(self, mem):
+        """All-gather the ranks' rollouts [T][E] into the union [T][world * E] (rank-major along the env axis),
+        in one collective of one packed tensor: normalised obs | action | log-prob | reward | done | end | next
+        obs.  Every rank then holds the same batch."""
+        import torch.distributed as dist
+
+        if mem.get("union"):
+            return mem
+        T, E, ob, W = mem["T"], self.n_envs, self.ob_dim, self.world
+        F = 3 * ob + 4
+        pk = torch.empty(T, E, F, device=self.device)
+        pk[:, :, :ob] = mem["obs"]
+        pk[:, :, ob:2 * ob] = mem["act"]
+        pk[:, :, 2 * ob] = mem["lp"]
+        pk[:, :, 2 * ob + 1] = mem["rew"]
+        pk[:, :, 2 * ob + 2] = mem["done"].float()
+        pk[:, :, 2 * ob + 3] = mem["end"].float()
+        pk[:, :, 2 * ob + 4:] = mem["next_obs"]
+        allp = torch.empty(W, T, E, F, device=self.device)
+        dist.all_gather_into_tensor(allp.view(W * T, E, F), pk.view(T, E, F))
+        u = allp.permute(1, 0, 2, 3).reshape(T, W * E, F)  # [T][rank][env] -> [T][rank * E + env]
+        return {"obs": u[:, :, :ob], "act": u[:, :, ob:2 * ob], "lp": u[:, :, 2 * ob].contiguous(),
+                "rew": u[:, :, 2 * ob + 1].contiguous(), "done": u[:, :, 2 * ob + 2].to(torch.uint8),
+                "end": u[:, :, 2 * ob + 3].to(torch.uint8), "next_obs": u[:, :, 2 * ob + 4:], "T": T, "E": W * E,
+                "union": True}
+
     # ---------------------------------------------------------------- update (critic, GAE, actor)
     def update(self, mem):
-        T, E, ob = mem["T"], self.n_envs, self.ob_dim
+        """critic, GAE, actor on the iteration's batch: this rank's rollout, or (data parallel) the union of every
+        rank's (self._union; a caller may pass the union itself)."""
+        if self.dp:
+            mem = self._union(mem)
+        T, E, ob = mem["T"], mem.get("E", self.n_envs), self.ob_dim
         N = T * E
         obs = mem["obs"].reshape(N, ob)
         nobs = self.normalize(mem["next_obs"].reshape(N, ob))

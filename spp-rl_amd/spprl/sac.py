@@ -21,8 +21,14 @@ class SAC(SAC_AcM):
     VANILLA = True
 
     def __init__(self, env_name="HalfCheetah-v2", **kw):
-        for k in ("acm_critic", "custom_loss", "norm_closs", "min_max_denormalize", "denormalize_actor_out"):
-            kw.pop(k, None)
+        # SAC -> DDPG -> RL -> MetaLearner (sac.py:17-25, ddpg.py:19-33, rl.py:17-26) take no AcMTrainer /
+        # AcMOffPolicy / DDPG_AcM keyword: the reference raises TypeError on them, and so does this class
+        acm_only = sorted(k for k in kw if k.startswith("acm_") or k in (
+            "custom_loss", "norm_closs", "denormalize_actor_out", "unbiased_update", "acm_critic"))
+        if acm_only:
+            raise TypeError("SAC got unexpected keyword argument(s): %s (SPP / AcM options: use SAC_AcM)"
+                            % ", ".join(acm_only))
+        kw.pop("min_max_denormalize", None)  # MetaLearner's; without obs_norm it normalises nothing here
         super().__init__(env_name=env_name, acm_critic=False, custom_loss=0.0, min_max_denormalize=False,
                          denormalize_actor_out=False, **kw)
 

@@ -34,13 +34,14 @@ class SAC_AcM(OffPolicyLoop):
                  acm_lr=config.ACM_LR, acm_critic=config.ACM_CRITIC, custom_loss=0.0, norm_closs=config.NORM_CLOSS,
                  min_max_denormalize=config.MIN_MAX_DENORMALIZE, denormalize_actor_out=config.DENORMALIZE_ACTOR_OUT,
                  acm_ob_idx=None, obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None,
-                 seed=None, mlp_bf16=False, **unused):
+                 seed=None, mlp_bf16=False, unbiased_update=False, **loop_kw):
+        self._check_kwargs(loop_kw)
         _lib.load()
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
         vanilla = self.VANILLA
         if vanilla:  # SAC (sac.py): no ACM anywhere, the actor emits the env action
             acm_critic, custom_loss, acm_ob_idx = False, 0.0, None
-            unused.setdefault("acm_epochs", 0)
+            loop_kw.setdefault("acm_epochs", 0)
         self.env_spec = tuple(env_spec or config.ENV_SPECS[env_name])
         self.env_name, self.ob_dim, self.ac_dim = env_name, ob, ac
         # Q3: AcMOffPolicy never masks time-limit done (off_policy.py:43); RL does (rl.py:185)
@@ -51,6 +52,7 @@ class SAC_AcM(OffPolicyLoop):
         self.act_noise = config.ACT_NOISE  # Q1: likewise (ddpg.py:29,100)
         self.update_batch_size = update_batch_size
         self.acm_critic, self.custom_loss, self.norm_closs = bool(acm_critic), float(custom_loss), bool(norm_closs)
+        self.unbiased_update = bool(unbiased_update)  # DDPG_AcM.make_update (ddpg_acm.py:59-79), inherited
         self.min_max_denormalize, self.denormalize_actor_out = bool(min_max_denormalize), bool(denormalize_actor_out)
         self.acm_ob_idx = list(range(ob)) if acm_ob_idx is None else list(acm_ob_idx)
         if len(self.acm_ob_idx) != ob:
@@ -67,7 +69,7 @@ class SAC_AcM(OffPolicyLoop):
         self.ac_lim = torch.full((ac,), float(ac_high))
         self.target_entropy = -float(ac)  # Q4 (sac.py:104-106)
         self.alpha = alpha
-        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, unused))
+        self.max_batch = int(max_batch or config.default_max_batch(update_batch_size, loop_kw))
         aout = self.actor_output_dim
         cin = ob + (ac if self.acm_critic else aout)
         self.layouts = {_lib.SPP_NET_ACTOR: nets.sac_actor_layout(ob, aout),
@@ -121,7 +123,7 @@ class SAC_AcM(OffPolicyLoop):
             if obs_norm:
                 raise NotImplementedError("vanilla SAC with obs_norm=True is not on the device path")
             self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=False,
-                                              n_envs=int(unused.get("n_envs", 1)))
+                                              n_envs=int(loop_kw.get("n_envs", 1)))
             # identity denormalisation of the actor output: min-max over [-1, 1] is 0 + x * 1, exact
             self._ident = torch.stack([-torch.ones(ob), torch.ones(ob), torch.zeros(ob), torch.ones(ob)]).to(self.device)
             call("sppAgentBindNormalizer", self._h, ptr(self._ident[0]), ptr(self._ident[1]), ptr(self._ident[2]),
@@ -129,10 +131,10 @@ class SAC_AcM(OffPolicyLoop):
         else:
             self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
                                                     min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm,
-                                                    n_envs=int(unused.get("n_envs", 1)))
+                                                    n_envs=int(loop_kw.get("n_envs", 1)))
             self.bind_normalizer(self.replay_buffer)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
-        self._init_loop(update_batch_size=update_batch_size, **unused)
+        self._init_loop(update_batch_size=update_batch_size, **loop_kw)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -179,14 +181,14 @@ class SAC_AcM(OffPolicyLoop):
     def update_from_replay(self, idx, seed, counter):
         """Fused path: gather the sampled transitions on device and update with device eps."""
         idx = torch.as_tensor(idx, dtype=torch.int64).to(self.device).contiguous()
-        call("sppAgentStageFromReplay", self._h, self.replay_buffer._h, ptr(idx), idx.numel(), stream_handle())
+        self._stage(idx)
         call("sppSacAcmUpdateStaged", self._h, seed, counter, ptr(self._losses), stream_handle())
 
     def update_from_replay_dp(self, idx, seed, counter, allreduce=None):
         """The same grad step split at its exchange points: allreduce(bucket) averages a
         flat gradient bucket across data-parallel ranks (RCCL) between grads and apply."""
         st = stream_handle()
-        call("sppAgentStageFromReplay", self._h, self.replay_buffer._h, ptr(idx), idx.numel(), st)
+        self._stage(idx)
         call("sppSacAcmDrawEps", self._h, seed, counter, st)
         call("sppSacAcmCriticGrads", self._h, None, None, ptr(self._losses), st)
         if allreduce is not None:

@@ -309,8 +309,8 @@ class OffPolicyLoop:
                    acm_pre_train_epochs=config.ACM_PRE_TRAIN_N_EPOCHS, acm_scheduler_step=config.ACM_SCHEDULER_STEP,
                    acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=config.ACM_KEEP_PRE_TRAIN,
                    n_envs=1, env=None, schedule=None, loop_seed=0, allreduce=None, allreduce_sum=None, host_sum=None,
-                   tensorboard_dir=None,
-                   debug_mode=False, **unused):
+                   tensorboard_dir=None, debug_mode=False, update_batch_size=None, **rest):
+        config.check_kwargs(type(self).__name__, rest)  # (update_batch_size: already set by the agent)
         if max_frames is not None and max_frames > iterations * batch_size:
             raise AssertionError("max_frames should be smaller or equal than iterations * batch_size")  # rl.py:166
         self.iterations, self.batch_size, self.stats_freq = int(iterations), int(batch_size), int(stats_freq)
@@ -372,6 +372,14 @@ class OffPolicyLoop:
         self._obs = None
         self._prev_slots = None
         self._ep_len = np.zeros(E, np.int64)  # frames into the current episode, per env (time-limit done, Q3)
+
+    def _check_kwargs(self, kw):
+        """At the top of an agent constructor: every keyword it hands to _init_loop is a loop keyword or one of
+        config.NO_EFFECT_KWARGS, else TypeError (before any device allocation)."""
+        import inspect
+
+        taken = set(inspect.signature(OffPolicyLoop._init_loop).parameters) - {"self", "rest"}
+        config.check_kwargs(type(self).__name__, {k: v for k, v in kw.items() if k not in taken})
 
     # ---------------------------------------------------------- helpers
     def _next(self):
@@ -535,10 +543,15 @@ class OffPolicyLoop:
         return self.iteration > 0 and self.acm_epochs > 0 and self.stats_logger.frames % self.acm_update_freq == 0
 
     def make_update(self):
-        """Reference cadence (ddpg.py:231-237, ddpg_acm.py:75-85), one frame at a time."""
+        """Reference cadence (ddpg.py:231-237, ddpg_acm.py:75-85), one frame at a time.  unbiased_update
+        (make_unbiased_update, ddpg_acm.py:59-73): the sampled next obs is the critic's action."""
         if self.update_condition():
+            unbiased = getattr(self, "unbiased_update", False)
             for _ in range(self.grad_steps):
-                self.update(*self.replay_buffer.sample_batch(self.update_batch_size, self.device))
+                batch = self.replay_buffer.sample_batch(self.update_batch_size, self.device)
+                if unbiased:
+                    batch[2] = batch[1]
+                self.update(*batch)
         if self.acm_update_condition():
             if self.acm_update_batches:
                 self.update_acm_batches(self.acm_update_batches)
@@ -563,6 +576,18 @@ class OffPolicyLoop:
                 f1 = self.stats_logger.frames
                 if f1 // self.acm_update_freq > (f1 - self.n_envs) // self.acm_update_freq:
                     self.update_acm(self.acm_epochs)
+
+    def _stage(self, idx):
+        """sample_batch of the fused schedule on device: gather the transitions idx into the agent's staging
+        area (sppAgentStageFromReplay), then the normalisation of obs_norm buffers (replay_buffer.py:247-249)
+        and, with unbiased_update, action := next obs (ddpg_acm.py:59-73), in place (sppAgentStagePost)."""
+        st = stream_handle()
+        rb = self.replay_buffer
+        call("sppAgentStageFromReplay", self._h, rb._h, ptr(idx), idx.numel(), st)
+        norm = bool(rb.obs_norm) and not (rb.min_max_denormalize and not rb._have_minmax)  # normalize() no-ops
+        unbiased = bool(getattr(self, "unbiased_update", False)) and not self.acm_critic  # acm_critic: acm_action
+        if norm or unbiased:
+            call("sppAgentStagePost", self._h, int(norm), int(unbiased), st)
 
     def fused_batch_sizes(self):
         """(grad-step batch, ACM batch) of one fused vector step: rho*E and sigma*E."""

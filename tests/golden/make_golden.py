@@ -685,8 +685,75 @@ def gen_interop(seed=61):
     save("ref_interop.npz", **out)
 
 
+# ---------------------------------------------------------------- DDPG_AcM.make_update, unbiased_update=True
+def gen_ddpg_unbiased(seed=81):
+    """DDPG_AcM(unbiased_update=True).make_update (acm/off_policy/ddpg_acm.py:59-85) over two update
+    cadences: each samples grad_steps batches from the ring (np.random.randint after np.random.seed) and
+    updates with action = next_obs (normalised: obs_norm=True, z-score).  acm_critic=False, so the critic
+    takes (obs, action) and the unbiased branch changes what it learns; custom_loss with norm_closs."""
+    torch.manual_seed(0)
+    env, size, B, gsteps, ufreq = "HalfCheetah-v2", 400, 40, 2, 10
+    m = DDPG_AcM(env_name=env, unbiased_update=True, gamma=0.97, actor_lr=5e-4, critic_lr=5e-4, buffer_size=size,
+                 acm_pre_train_samples=10, acm_val_buffer_size=None, update_batch_size=B, grad_steps=gsteps,
+                 update_freq=ufreq, custom_loss=0.3, norm_closs=True, acm_critic=False, min_max_denormalize=False,
+                 denormalize_actor_out=True, obs_norm=True, use_gpu=False)
+    ob, aout, ac = m.ob_dim, m.actor_output_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic": m._critic, "actor_targ": m.actor_targ, "critic_targ": m.critic_targ}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    buf = m.replay_buffer
+    buf.obs_mean = torch.from_numpy((rng.randn(ob) * 0.3).astype(np.float32))
+    buf.obs_std = torch.from_numpy(rng.uniform(0.5, 1.5, ob).astype(np.float32))
+    ops, obs_log, act_log, acm_log, rew_log, done_log, end_log = [], [], [], [], [], [], []
+    for L in rng.randint(5, 40, 9):  # ragged episodes, no wrap (size 400)
+        o = (rng.randn(1, ob) * 1.4).astype(np.float32)
+        prev = buf.add_obs(torch.from_numpy(o))
+        obs_log.append(o[0])
+        ops.append((0, prev, -1))
+        for t in range(L):
+            acm = rng.uniform(-1, 1, ac).astype(np.float32)
+            buf.add_acm_action(acm)
+            a = torch.from_numpy(rng.uniform(-1.2, 1.2, (1, aout)).astype(np.float32))
+            o = (rng.randn(1, ob) * 1.4).astype(np.float32)
+            nxt = buf.add_obs(torch.from_numpy(o))
+            r = float(rng.randn())
+            end = t == L - 1
+            done = bool(end and rng.rand() < 0.5)
+            buf.add_timestep(prev, nxt, a, r, done, end)
+            ops.append((1, prev, nxt))
+            obs_log.append(o[0])
+            act_log.append(a.numpy()[0])
+            acm_log.append(acm)
+            rew_log.append(r)
+            done_log.append(done)
+            end_log.append(end)
+            prev = nxt
+    out = dict(dims=np.array([ob, aout, ac, B, gsteps, ufreq, size]), seed=np.array(seed),
+               norm=np.stack([buf.obs_mean.numpy(), buf.obs_std.numpy()]),
+               actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32), tau=np.array(m.tau), gamma=np.array(m.gamma),
+               ops=np.array(ops, np.int64), obs=np.array(obs_log, np.float32), act=np.array(act_log, np.float32),
+               acm=np.array(acm_log, np.float32), rew=np.array(rew_log, np.float32),
+               done=np.array(done_log, np.bool_), end=np.array(end_log, np.bool_))
+    m.iteration = 0  # no ACM update in these cadences (ddpg_acm.py:52-57)
+    losses, idxs, np_seeds = [], [], [101, 202]
+    for c, s in enumerate(np_seeds):
+        m.stats_logger.frames = ufreq * (c + 1)
+        assert m.update_condition()
+        np.random.seed(s)
+        idxs.append(np.stack([np.random.randint(0, len(buf), B) for _ in range(gsteps)]))
+        np.random.seed(s)
+        m.make_update()
+        losses.append([m.loss.get(k, 0.0) for k in ("critic", "actor", "ddpg", "dist")])
+    out.update(np_seeds=np.array(np_seeds), idx=np.stack(idxs), losses=np.array(losses))
+    for k, mod in nets.items():
+        out["post_" + k] = flat_params(mod)
+    save("ddpg_unbiased_hcheetah.npz", **out)
+
+
 GROUPS = {"interop": gen_interop, "randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
-          "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy, "ppo_epochs": gen_ppo_epochs}
+          "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy, "ppo_epochs": gen_ppo_epochs,
+          "ddpg_unbiased": gen_ddpg_unbiased}
 
 if __name__ == "__main__":
     which = sys.argv[1:] or list(GROUPS) + ["sac"]

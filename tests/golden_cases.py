@@ -105,3 +105,34 @@ def normalize_adv_ref(adv):
     """AdvantageDataset normalisation (advantage_dataset.py:8-12): torch.std is unbiased."""
     a = torch.as_tensor(adv)
     return ((a - a.mean()) / (a.std() + 1.2e-7)).numpy()
+
+
+def ddpg_unbiased_case():
+    """DDPG_AcM(unbiased_update=True).make_update fixture (tests/golden/ddpg_unbiased_hcheetah.npz):
+    (fixture, params, norm (z-score), ring ops replayer).  acm_critic=False: critic on (obs, actor output)."""
+    from oracle.nets import critic_layout, ddpg_actor_layout
+    fx = load("ddpg_unbiased_hcheetah")
+    ob, aout, ac = (int(v) for v in fx["dims"][:3])
+    seed = int(fx["seed"])
+    layouts = {"actor": ddpg_actor_layout(ob, aout), "critic": critic_layout(ob + aout),
+               "actor_targ": ddpg_actor_layout(ob, aout), "critic_targ": critic_layout(ob + aout)}
+    params = {k: fill_params(lay, seed * 100 + i) for i, (k, lay) in enumerate(layouts.items())}
+    mu, sd = fx["norm"]
+    norm = Norm(False, mean=torch.from_numpy(mu), std=torch.from_numpy(sd))
+
+    def replay(add_obs, add_acm_action, add_timestep):
+        """Feed the fixture's ring writes (add_obs / add_acm_action / add_timestep) to a buffer."""
+        oi = si = 0
+        for kind, a, b in fx["ops"]:
+            if kind == 0:
+                assert add_obs(fx["obs"][oi]) == a
+                oi += 1
+                continue
+            add_acm_action(fx["acm"][si])
+            assert add_obs(fx["obs"][oi]) == b
+            oi += 1
+            add_timestep(int(a), int(b), fx["act"][si], float(fx["rew"][si]), bool(fx["done"][si]),
+                         bool(fx["end"][si]))
+            si += 1
+
+    return fx, params, layouts, norm, replay

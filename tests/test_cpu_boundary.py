@@ -95,3 +95,24 @@ def test_bench_refuses_world_size_other_than_gpus():
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 2, out.stderr[-2000:]
     assert "WORLD_SIZE=2" in out.stderr
+
+
+def test_unknown_reference_kwargs_raise_and_no_effect_ones_are_listed():
+    """Agent constructors reject keywords they neither take nor list in config.NO_EFFECT_KWARGS, as the
+    reference's constructor chain does (MetaLearner, rl.py:17-26, takes no **kwargs); the check runs
+    before the library is touched, so it needs no GPU."""
+    import spprl
+    from spprl import config
+
+    for cls in (spprl.SAC_AcM, spprl.DDPG_AcM):
+        with pytest.raises(TypeError, match="foo"):
+            cls(unbiased_update=True, foo=1)
+    with pytest.raises(TypeError, match="acm_epochs"):
+        spprl.SAC(acm_epochs=3)
+    with pytest.raises(TypeError, match="unbiased_update"):
+        spprl.SAC(unbiased_update=True)
+    with pytest.raises(TypeError, match="bar"):
+        spprl.PPO_AcM(bar=2)
+    assert {"use_gpu", "log_dir", "verbose", "render", "acm_val_buffer_size"} <= set(config.NO_EFFECT_KWARGS)
+    assert "obs_norm_alpha" in config.ON_POLICY_NO_EFFECT_KWARGS
+    config.check_kwargs("x", {"use_gpu": True, "tensorboard_comment": "c"})

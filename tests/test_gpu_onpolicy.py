@@ -350,3 +350,53 @@ def test_actor_epoch_kernel_matches_per_step_path_and_oracle(N, mb):
         d = np.abs(p - flat)
         print("N %d mb %d: |d|/lr max %.4f mean %.6f" % (N, mb, d.max() / lr, d.mean() / lr))
         assert d.max() <= 2 * lr * nsteps * 1.01 and d.mean() <= 0.01 * lr, (d.max(), d.mean())
+
+
+def test_persistent_launch_timeouts_raise_in_the_product_path():
+    """A multi-workgroup persistent launch whose arrival wait times out leaves invalid parameters: the product
+    path (OnPolicyNets.update_critic / update_actor as PPO_AcM.update runs them, and the AcM epochs of
+    update_acm) must raise SppError, not continue.  The timeout is forced with the spin-limit test hook
+    (sppSetSgdSpinLimit(1): the first workgroup to arrive at a barrier gives up)."""
+    import spprl
+    from spprl import _lib
+    from spprl.onpolicy import OnPolicyNets
+
+    N = 4096
+    rng = np.random.RandomState(7)
+    obs = torch.from_numpy((rng.randn(N, OB)).astype(np.float32)).to(DEV)
+    nobs = torch.from_numpy((rng.randn(N, OB)).astype(np.float32)).to(DEV)
+    rew = torch.from_numpy(rng.randn(N).astype(np.float32)).to(DEV)
+    done = torch.zeros(N, device=DEV)
+    act = torch.from_numpy(rng.uniform(-1, 1, (N, AOUT)).astype(np.float32)).to(DEV)
+    lp = torch.from_numpy(rng.randn(N).astype(np.float32)).to(DEV)
+    adv = torch.from_numpy(rng.randn(N).astype(np.float32)).to(DEV)
+    # healthy: the same calls raise nothing
+    n0 = OnPolicyNets(OB, AOUT, max_batch=N, ppo_batch_size=512, max_ppo_epochs=2, critic_num_target_updates=1,
+                      num_critic_updates_per_target=3, device=DEV, seed=1)
+    assert n0._critic_kernel_ok(N) and n0._epoch_kernel_ok(512)
+    n0.update_critic(obs, nobs, rew, done)
+    n0.update_actor(adv, obs, act, lp, nobs)
+    try:
+        _lib.call("sppSetSgdSpinLimit", 1)
+        n1 = OnPolicyNets(OB, AOUT, max_batch=N, critic_num_target_updates=1, num_critic_updates_per_target=3,
+                          device=DEV, seed=1)
+        with pytest.raises(_lib.SppError, match="timed out"):
+            n1.update_critic(obs, nobs, rew, done)
+        n2 = OnPolicyNets(OB, AOUT, max_batch=N, ppo_batch_size=512, max_ppo_epochs=2, device=DEV, seed=1)
+        with pytest.raises(_lib.SppError, match="timed out"):
+            n2.update_actor(adv, obs, act, lp, nobs)
+        # the AcM epochs (multi-workgroup sppAcmSgdEpoch, acm_batch_size > 64): raised at the next update_acm
+        ag = spprl.SAC_AcM(env_name="HalfCheetah-v2", buffer_size=5000, max_batch=1024, acm_batch_size=1024,
+                           device=DEV, seed=0)
+        rb = ag.replay_buffer
+        slots = rb.add_obs_batch(torch.randn(3001, 17, device=DEV))
+        z = torch.zeros(3000, dtype=torch.uint8, device=DEV)
+        rb.add_timestep_batch(slots[:-1], slots[1:], torch.randn(3000, 17, device=DEV), torch.randn(3000, device=DEV),
+                              z, z, torch.rand(3000, 6, device=DEV))
+        assert ag._acm_sgd_ok(1024)
+        ag.update_acm(1)
+        with pytest.raises(_lib.SppError, match="timed out"):
+            ag.check_acm_sgd()
+    finally:
+        _lib.call("sppSetSgdSpinLimit", 0)
+    torch.cuda.synchronize()

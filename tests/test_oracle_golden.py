@@ -4,10 +4,10 @@ import numpy as np
 import pytest
 import torch
 
-from golden_cases import SAC_CASES, ddpg_case, load, sac_case
+from golden_cases import SAC_CASES, ddpg_case, ddpg_unbiased_case, load, sac_case
 from oracle import nets
 from oracle.acm import OracleAcmTrainer
-from oracle.ddpg_acm import OracleDdpgAcm
+from oracle.ddpg_acm import OracleDdpgAcm, make_unbiased_update
 from oracle.ppo import clip_loss, gae_affine, gae_loop, q_val
 from oracle.replay import OracleReplay
 from oracle.rng import OracleMT
@@ -121,6 +121,32 @@ def test_ddpg_acm_update_matches_reference():
                                    rtol=1e-6, atol=1e-7)
     for k in ("actor", "critic", "actor_targ", "critic_targ"):
         np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_ddpg_acm_unbiased_make_update_matches_reference():
+    """make_unbiased_update (ddpg_acm.py:59-73) over two cadences of the reference's ring: sampled indices,
+    losses and post-step parameters (action = normalised next obs, acm_critic=False)."""
+    fx, params, layouts, norm, replay = ddpg_unbiased_case()
+    ob, aout, ac, B, gsteps, ufreq, size = (int(v) for v in fx["dims"])
+    rb = OracleReplay(size, ob, aout, ac)
+    replay(rb.add_obs, rb.add_acm_action, rb.add_timestep)
+    params = dict(params, acm={n: np.zeros(s, np.float32) for n, s in nets.basic_acm_layout(2 * ob, ac)})
+    o = OracleDdpgAcm(ob, aout, ac, acm_critic=False, custom_loss=0.3, norm_closs=True, norm=norm,
+                      actor_lim=fx["actor_ac_lim"], gamma=float(fx["gamma"]), tau=float(fx["tau"]), params=params)
+    for c, s in enumerate(fx["np_seeds"]):
+        losses, idx = make_unbiased_update(o, rb, B, gsteps, OracleMT(int(s)), norm)
+        np.testing.assert_array_equal(idx, fx["idx"][c])
+        np.testing.assert_allclose([losses[k] for k in ("critic", "actor", "ddpg", "dist")], fx["losses"][c],
+                                   rtol=1e-5, atol=1e-7)
+    for k in ("actor", "critic", "actor_targ", "critic_targ"):
+        np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    # the branch matters: the biased update (action = the stored actor output) lands elsewhere
+    o2 = OracleDdpgAcm(ob, aout, ac, acm_critic=False, custom_loss=0.3, norm_closs=True, norm=norm,
+                       actor_lim=fx["actor_ac_lim"], gamma=float(fx["gamma"]), tau=float(fx["tau"]), params=params)
+    (b_obs, b_nobs, b_act, b_rew, b_done, b_acm), _ = rb.sample_batch(B, OracleMT(int(fx["np_seeds"][0])))
+    o2.update(norm.normalize(torch.from_numpy(b_obs)).numpy(), norm.normalize(torch.from_numpy(b_nobs)).numpy(),
+              b_act, b_rew, b_done, b_acm)
+    assert np.abs(o2.flat("critic") - fx["post_critic"]).max() > 1e-4
 
 
 def test_acm_batch_update_matches_reference():

@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--dp-comm", choices=["native", "torch"], default="native",
                     help="N > 1 exchange: libspprl's own RCCL communicator on the compute stream (gradient buckets, "
                          "obs-statistics collectives) or torch.distributed's (its own stream + event waits)")
+    ap.add_argument("--rehearse-world", type=int, default=None,
+                    help="ppo_hcheetah on one GPU: the per-rank work of a W-rank job (ACM cadence scaled for W ranks, "
+                         "update on a W-rank union's shape); value = W x this rank's env-steps/s (projection)")
     ap.add_argument("--host-env", action="store_true",
                     help="step the envs on the host CPU (HostSynthEnv: vectorised numpy SynthEnv behind pinned "
                          "staging + side-stream copies, the update overlapping the host step): the PCIe-inclusive "
@@ -431,17 +434,20 @@ def bench_ppo(args, world, rank, dev):
     ref_batch, ref_ring, ref_acm_bs, acm_epochs, acm_freq = 2000, 110_000, 64, 5, 3
     # N > 1: the ACM ring is replicated (every rank holds every rank's rows, spprl/ppo_acm.py), so the ACM
     # cadence is scaled by the frames of all ranks
-    scale = world * N / ref_batch
+    rw = args.rehearse_world or 0  # (one-GPU rehearsal of a rw-rank job's per-rank work)
+    wj = max(world, rw)  # ranks of the job whose cadence is run
+    scale = wj * N / ref_batch
     acm_bs = int(round(ref_acm_bs * scale))
     seed = shard_seed(1000, rank)
     ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=N,
                        ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
                        custom_loss=0.1, norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True,
                        acm_epochs=acm_epochs, acm_batch_size=acm_bs, acm_update_freq=acm_freq, acm_lr=3e-4,
-                       acm_ring_size=int(round(ref_ring * scale)), n_envs=E, device=dev, seed=0, loop_seed=seed)
+                       acm_ring_size=int(round(ref_ring * scale)), n_envs=E, device=dev, seed=0, loop_seed=seed,
+                       rehearse_world=rw or None)
     rb = ag.replay_buffer
     ob, ac = ag.ob_dim, ag.ac_dim
-    sigma = acm_epochs * rb.size / (acm_freq * N * world)
+    sigma = acm_epochs * rb.size / (acm_freq * N * wj)
     torch.manual_seed(1000)  # the same pre-filled ring on every rank (replicated)
     fill = rb.size - 2 * E  # the ACM ring after pre-training (random env actions)
     prev = rb.add_obs_batch(torch.randn(1, ob, device=dev))
@@ -479,12 +485,12 @@ def bench_ppo(args, world, rank, dev):
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
-    value = world * N * args.steps / elapsed
+    value = wj * N * args.steps / elapsed
     mac = flops.onpolicy_macs(ob, ob, ac)
     # algorithmic work of the timed iterations: 100 full-batch critic steps on N samples, the PPO
     # epochs actually run (KL stop) over N samples, acm_epochs epochs over the ring per ACM update, the rollout
     # (the ACM epochs run replicated on every rank: their algorithmic share per rank is 1/world of them)
-    acm_samples = epochs["acm_updates"] * acm_epochs * rb.size / world
+    acm_samples = epochs["acm_updates"] * acm_epochs * rb.size / wj
     flop = 2.0 * (args.steps * (mac["critic_step"] * N * 100 + (mac["A"] + mac["M"]) * N)
                   + mac["actor_step"] * N * epochs["ppo"] + mac["acm_step"] * acm_samples)
     per_env_step = flop / (args.steps * N)
@@ -513,6 +519,21 @@ def bench_ppo(args, world, rank, dev):
                                 "~64 sequential 512-sample actor steps per epoch bound the iteration by latency"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
+    if ag.dp:
+        res["config"]["update_batch"] = ("union of %d ranks' rollouts, %d rows, replicated on every rank (one "
+                                         "all-gather per iteration; no per-step gradient exchange)" % (wj, wj * N))
+    if rw:
+        res["config"]["rehearsal"] = ("one GPU running the per-rank work of a %d-rank job: ACM ring / batch scaled "
+                                      "for %d ranks, update(mem) on the local rollout tiled to the %d-rank union "
+                                      "shape; value = %d x this GPU's env-steps/s (a projection, not a "
+                                      "multi-GPU measurement)" % (rw, rw, rw, rw))
+    if world > 1:  # the replicas must stay bit-identical (identical union batch, ring and permutation streams)
+        chk = torch.stack([t.double().sum() for t in (ag.nets.params[0], ag.nets.params[1], ag.acm.params[5])] +
+                          [t.double().abs().sum() for t in (ag.nets.params[0], ag.nets.params[1],
+                                                            ag.acm.params[5])])
+        allc = [torch.empty_like(chk) for _ in range(world)]
+        dist.all_gather(allc, chk)
+        res["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
     # the dominant kernel: the ACM epoch (k_mlp_sgd<2 ob, 32, ac, 0>, sequential 64 x s-row Adam steps over the
     # ring), timed by HIP events around each launch on the stream it runs on
     ev = ag.acm.sgd_events
@@ -534,7 +555,9 @@ def bench_ppo(args, world, rank, dev):
             "avg_launch_ms": round(k_ms, 4), "launches": len(ms_l),
             "us_per_sgd_step": round(k_ms * 1e3 / -(-rows // acm_bs), 2),
             "whole_iteration": {"achieved": res["roofline"]["achieved"], "frac": res["roofline"]["frac"],
-                                "note": res["roofline"]["note"]}}
+                                "note": res["roofline"]["note"]},
+            "scope": "achieved / frac / traffic are the dominant kernel's (one ACM-epoch launch), as in every bench "
+                     "line since round 4; the iteration's algorithmic rate is whole_iteration"}
         if rank == 0 and world == 1 and not args.no_rocprof:
             kt_ms, kt_src = rocprof_kernel_ms(args, args.envs, None, kname, steps=6, warmup=3, timed_launches=10)
             rl = res["roofline"]

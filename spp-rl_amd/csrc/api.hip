@@ -1260,12 +1260,18 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
   } else if (set == 0) {
     // critic phase: fc1 (delta1 x [s|a]), fc2 (delta2 x h1) per critic; fc3 (dq x h2) is fused into the
     // critic-phase kernel, which writes one [256 | 1] partial per wave: a reduce-only job
-    int fused_idx[2];
+    // (bf16 sets with SPP_BF16_FUSE3 = 0: the critic phase stores h2 (bf16) and dq; fc3 is a k_dw job)
+    const bool fuse3 = !a->cfg.mlp_bf16 || SPP_BF16_FUSE3;
+    int fused_idx[2] = {-1, -1};
     for (int i = 0; i < 2; ++i) {
       float* G = a->net[SPP_NET_CRITIC1 + i].g;
       float *gW1 = G, *gb1 = gW1 + 256 * cin, *gW2 = gb1 + 256, *gb2 = gW2 + 65536, *gw3 = gb2 + 256, *gb3 = gw3 + 256;
       J(a->D1[i], 256, a->S, ob, a->cfg.acm_critic ? a->AENV : a->ACT, ca, gW1, gb1);
       J(a->D2[i], 256, a->H1[i], 256, nullptr, 0, gW2, gb2);
+      if (!fuse3) {
+        J(a->DQ[i], 1, a->H2[i], 256, nullptr, 0, gw3, gb3);
+        continue;
+      }
       J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
       jobs.back().fused = 1;
       jobs.back().nsplit = phase_grid(a, Bp) * kWavesPerWG;
@@ -1284,8 +1290,8 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
     D.nj[1] = (int)jobs.size() - D.nj[0];
     nph = 2;
     sppStatus s = finalize_dw(D, jobs, nph, Bp, B, a->num_cu);
-    for (int i = 0; i < 2; ++i) a->w3p[i] = jobs[fused_idx[i]].slab;
-    a->w3p_stride = jobs[fused_idx[0]].slab_stride;
+    for (int i = 0; i < 2; ++i) a->w3p[i] = fuse3 ? jobs[fused_idx[i]].slab : nullptr;
+    a->w3p_stride = fuse3 ? jobs[fused_idx[0]].slab_stride : 0;
     return s;
   } else {
     float* G = a->net[SPP_NET_ACM].g;

@@ -5,6 +5,14 @@
 
 #include <string>
 
+// bf16 SAC kernel sets: fuse the critics' fc3 weight gradient into the critic phase (1) or hand h2 / dq to a
+// k_dw job (0).  Compile-time A/B (tools/build_variant.py -DSPP_BF16_FUSE3=...); fp32 sets always fuse.
+// Measured round 5 (Ant bf16, 100 steps, profiles/r05/ab_fuse3_*.json): fused critic phase 1.8145 ms,
+// unfused 1.6787 ms (+0.027 ms of k_dw), step 6.79 -> 6.71 ms: the bf16 default is the k_dw job.
+#ifndef SPP_BF16_FUSE3
+#define SPP_BF16_FUSE3 0
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

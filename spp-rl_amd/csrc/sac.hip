@@ -23,6 +23,9 @@ struct Cfg {
   static constexpr int OB = OB_, AOUT = AOUT_, AC = AC_;
   static constexpr bool ACMC = ACMC_;
   static constexpr bool BF = BF_;  // bf16 MFMA MLP layers (fp32 accumulation, epilogues and targets)
+  // the critics' fc3 weight gradient fused into k_sac_critic_phase (else h2 / dq go to HBM for a k_dw job);
+  // bf16 sets: SPP_BF16_FUSE3 (api.hip's build_dw makes the same choice through sac_fuse3())
+  static constexpr bool F3 = !BF_ || SPP_BF16_FUSE3;
   static constexpr int NB_OB = blocks_of(OB);
   static constexpr int NB_AOUT = blocks_of(AOUT);
   static constexpr int NB_H2 = blocks_of(2 * AOUT);      // heads output blocks (natural rows mu | logsig)
@@ -497,11 +500,15 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, C::ACMC ? p.AENV : p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
       SPP_TP(10);
-      const float q = critic_forward<C, true, 11, true>(Q, xin, L, p.H1[i], nullptr, m1lo, m1hi, m2lo, m2hi);
+      const float q = critic_forward<C, true, 11, C::F3>(Q, xin, L, p.H1[i], C::F3 ? nullptr : p.H2[i], m1lo, m1hi,
+                                                        m2lo, m2hi);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;  // d mse / dq
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
       if (i == 0) lq0 = lqi; else lq1 = lqi;
+      if constexpr (!C::F3) {
+        if (L.h == 0) p.DQ[i][b] = dq;  // (h2 is stored by critic_forward: the k_dw job dW3 = dq . h2^T)
+      } else {
       // fc3's weight gradient, fused (sac_acm.py:117-131; dW3 = dq . h2^T, db3 = sum dq): h2 is in the image;
       // lane l sums units l + 64k over the tile's 32 samples (rotated column order: conflict-free rows)
       // into registers that carry over the wave's tiles; the per-wave partials are reduced in a fixed order
@@ -525,6 +532,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       if (i == 0) b3a += dsum;
       else b3b += dsum;
       SPP_XLANE_SYNC();  // the image rows are rewritten by the delta2 staging below
+      }
       // delta2 = dq * w3 * relu'(h2): staged through the LDS image, stored feature-major
       const rsrc_t d2r = rsrc(p.D2[i]);
       const float* w3 = tbl + Q.tw3;
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
     SPP_TP(15);
   }
   // this wave's fc3 partials [256 weights | bias] per critic (every wave writes, tiles or not)
-  {
+  if constexpr (C::F3) {
     const int64_t wg = (int64_t)blockIdx.x * kWavesPerWG + w;
     float* o0 = p.W3P[0] + wg * p.w3p_stride;
     float* o1 = p.W3P[1] + wg * p.w3p_stride;

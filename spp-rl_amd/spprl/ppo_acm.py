@@ -47,7 +47,8 @@ class PPO_AcM:
                  acm_scheduler_gamma=config.ACM_SCHEDULER_GAMMA, acm_keep_pretrain=True, acm_ring_size=None,
                  iterations=1001,
                  stats_freq=1, test_episodes=None, return_done=None, max_frames=None, n_envs=1, env=None,
-                 env_spec=None, device="cuda", seed=None, loop_seed=0, epsilon=None, obs_norm=False, **unused):
+                 env_spec=None, device="cuda", seed=None, loop_seed=0, epsilon=None, obs_norm=False,
+                 rehearse_world=None, **unused):
         # unknown keywords raise (the reference's MetaLearner takes no **kwargs, rl.py:17-26); `epsilon` is the
         # reference's name of the clip range (PPO.__init__, ppo.py:17), ppo_epsilon this class's older one
         config.check_kwargs("PPO_AcM", unused, config.ON_POLICY_NO_EFFECT_KWARGS)
@@ -79,6 +80,10 @@ class PPO_AcM:
         import torch.distributed as dist
 
         dp_world = dist.get_world_size() if make_allreduce() is not None else 1  # (the union: world x N rows)
+        # rehearse_world = W (measurement only, one process): update(mem) runs on this rank's rollout tiled W
+        # times -- the shape, and so the per-rank work, of a W-rank job's union batch -- with no collective
+        self.rehearse_world = int(rehearse_world or 0)
+        dp_world = max(dp_world, self.rehearse_world)
         self.nets = OnPolicyNets(ob, ob, ac_lim=lim, actor_lr=actor_lr, critic_lr=critic_lr, ppo_epsilon=ppo_epsilon,
                                  entropy_coef=entropy_coef, gamma=gamma, gae_lambda=gae_lambda,
                                  critic_num_target_updates=critic_num_target_updates,
@@ -108,8 +113,8 @@ class PPO_AcM:
         # targets, GAE, the persistent sppOnpCriticSteps / sppOnpActorEpoch launches) on the identical union with
         # one permutation stream: no per-step gradient exchange, replicas bit-identical, and the result is one
         # process's update on the union batch (acm/on_policy.py:72-75, a2c.py:186-225, ppo.py:152-192)
-        self.dp = self.nets.allreduce is not None
-        self.world = dist.get_world_size() if self.dp else 1
+        self.dp = self.nets.allreduce is not None or self.rehearse_world > 1
+        self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
         self.nets.allreduce = self.nets.allreduce_sum = None  # (the nets see the union: no per-step exchange)
         self.nets.world = 1
@@ -412,6 +417,12 @@ class PPO_AcM:
         if mem.get("union"):
             return mem
         T, E, ob, W = mem["T"], self.n_envs, self.ob_dim, self.world
+        if self.rehearse_world > 1:  # (measurement: a W-rank union's shape from this rank's rollout)
+            R = self.rehearse_world
+            tile = lambda x: x.repeat(1, R, *([1] * (x.dim() - 2)))  # noqa: E731
+            out = {k: tile(mem[k]) for k in ("obs", "act", "lp", "rew", "done", "end", "next_obs")}
+            out.update(T=T, E=R * E, union=True)
+            return out
         F = 3 * ob + 4
         pk = torch.empty(T, E, F, device=self.device)
         pk[:, :, :ob] = mem["obs"]

@@ -46,6 +46,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "spp-rl_amd"))
 sys.path.insert(0, REPO)
 
+# HIP hardware queues per process (read once, when the runtime initialises: before torch touches the GPU).  The
+# PPO_AcM iteration runs its ACM epochs on a second stream beside the update; with a process group's RCCL
+# streams there are more streams than HIP's default 4 queues, and the runtime then maps the update's stream and
+# the ACM's onto one queue, serialising them (DP-forced PPO 452 K vs 496 K env-steps/s at 4 queues, equal to the
+# plain line at 8: profiles/r05/ab_acm_wv.txt).  8 <= the pool's limit of 32.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -547,7 +555,7 @@ def bench_ppo(args, world, rank, dev):
         kname = "k_mlp_sgd<%d, 32, %d, 0" % (2 * ob, ac)
         res["roofline"] = {
             "bound": "mfma", "kernel": "%s, true> (one ACM epoch: %d sequential Adam steps of %d rows, workgroups "
-                                      "%d)" % (kname, -(-rows // acm_bs), acm_bs, -(-acm_bs // 64)),
+                                      "%d)" % (kname, -(-rows // acm_bs), acm_bs, ag.acm.acm_sgd_workgroups()),
             "achieved": round(kflop / (k_ms * 1e-3) / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(kflop / (k_ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 5), "traffic": None,
             "flop_per_launch": kflop, "algorithmic": "2 x 3 x %d MAC (AcM forward + both backward GEMMs) per row x %d "

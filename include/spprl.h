@@ -338,6 +338,9 @@ sppStatus sppAcmSgdStatusAsync(sppAgentHandle h, int* timed_out_pinned, void* st
 /* Largest bs sppAcmSgd accepts on this device for this agent: every workgroup of a step must be resident
  * at once (the arrival barrier), so min(32768, 64 x occupancy x CUs).  Larger batches: SPP_E_SHAPE. */
 int sppAcmSgdMaxBatch(sppAgentHandle h);
+/* Co-resident workgroups (one per CU) one sppAcmSgd / sppAcmSgdEpoch step of bs rows runs on: 1 for bs <= 64
+ * (4 waves), else max(2, ceil(bs / 128)) (8 waves, two per SIMD); 0 for handles without the AcM kernel. */
+int sppAcmSgdWorkgroups(sppAgentHandle h, int bs);
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
 
 /* Per-kernel device timing (HIP events on the launch stream), for measurement:

@@ -1951,28 +1951,41 @@ sppStatus sppAcmRegressApply(sppAgentHandle a, void* stream) {
 
 // co-resident workgroups of the multi-workgroup AcM k_mlp_sgd on this device (0: no instantiation)
 extern "C++" {
-template <int IN, int H2, int OUT, int HEAD>
+template <int IN, int H2, int OUT, int HEAD, int WV = 4>
 static int mlp_sgd_max_wg(int num_cu) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_mlp_sgd<IN, H2, OUT, HEAD, true>, kMlTH,
-                                                   0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_mlp_sgd<IN, H2, OUT, HEAD, true, WV>,
+                                                   64 * WV, 0) != hipSuccess)
     per_cu = 0;
-  return std::min(MlCfg<IN, H2, OUT, HEAD>::MAXG, per_cu * num_cu);
+  return std::min(MlCfg<IN, H2, OUT, HEAD, WV>::MAXG, per_cu * num_cu);
 }
 }
+// waves per workgroup of the multi-workgroup AcM regression kernel (HEAD 0, bs > 64).  8 = two waves per SIMD,
+// up to 128 rows per workgroup, at least 2 workgroups (its LDS has no room for the single-workgroup form's
+// canonical gradient staging).  Measured round 5 (1049-row PPO ACM steps, profiles/r05/ab_acm_wv.txt): 8 waves
+// on 9 workgroups 17.3 us per step against 13.4 us for 4 waves on 17: the MFMA work per CU doubles while the
+// second wave per SIMD hides less than that, so the default stays 4 (A/B: -DSPP_ACM_WV=8).  bs <= 64 always runs
+// the single-workgroup 4-wave form.
+#ifndef SPP_ACM_WV
+#define SPP_ACM_WV 4
+#endif
+constexpr int kAcmWV = SPP_ACM_WV, kAcmR = 16 * kAcmWV;
+static int acm_sgd_nwg(int bs) { return bs <= kMlR ? 1 : std::max(2, cdiv(bs, kAcmR)); }
 static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
   if (a->sgd_max_wg >= 0) return a->sgd_max_wg;
   int n = 0;
-  if (ob == 11 && ac == 3) n = mlp_sgd_max_wg<22, 32, 3, 0>(a->num_cu);
-  else if (ob == 17 && ac == 6) n = mlp_sgd_max_wg<34, 32, 6, 0>(a->num_cu);
-  else if (ob == 3 && ac == 1) n = mlp_sgd_max_wg<6, 32, 1, 0>(a->num_cu);
+  if (ob == 11 && ac == 3) n = mlp_sgd_max_wg<22, 32, 3, 0, kAcmWV>(a->num_cu);
+  else if (ob == 17 && ac == 6) n = mlp_sgd_max_wg<34, 32, 6, 0, kAcmWV>(a->num_cu);
+  else if (ob == 3 && ac == 1) n = mlp_sgd_max_wg<6, 32, 1, 0, kAcmWV>(a->num_cu);
   a->sgd_max_wg = n;
   return n;
 }
 
+int sppAcmSgdWorkgroups(sppAgentHandle a, int bs) { return (a && !a->ddpg && bs > 0) ? acm_sgd_nwg(bs) : 0; }
+
 int sppAcmSgdMaxBatch(sppAgentHandle a) {
   if (!a || a->ddpg) return 0;
-  return kMlR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
+  return kAcmR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
 }
 
 // polls before a k_mlp_sgd arrival wait times out (0: the kernel's default); test hook sppSetSgdSpinLimit
@@ -2004,7 +2017,7 @@ static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, i
   SPP_REQUIRE(a && x && y && loss_sum && nsteps >= 0 && bs > 0 && bs_last > 0 && bs_last <= bs, SPP_E_INVALID_ARG,
               "acm_sgd: bad args");
   SPP_REQUIRE(!a->ddpg, SPP_E_INVALID_ARG, "acm_sgd: the persistent kernel is for the AcM (SAC_AcM / PPO_AcM handles)");
-  SPP_REQUIRE(bs <= kMlR * kMlMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kMlR * kMlMaxWG);
+  SPP_REQUIRE(bs <= kAcmR * kMlMaxWG, SPP_E_SHAPE, "acm_sgd: batch %d > %d", bs, kAcmR * kMlMaxWG);
   sppStatus s = check_ready(a);
   if (s) return s;
   if (nsteps == 0) return SPP_OK;
@@ -2016,8 +2029,8 @@ static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, i
   g.lim = a->limits.ptr + a->cfg.aout; g.loss_sum = loss_sum; g.spin = g_sgd_spin;
   const int ob = a->cfg.ob, ac = a->cfg.ac;
   hipStream_t st = S(stream);
-  // 64 rows per workgroup (sgd_mlp.hip); the per-step arrival barriers need every workgroup resident at once
-  const int nwg = cdiv(bs, kMlR);
+  // <= kAcmR rows per workgroup (sgd_mlp.hip); the per-step arrival barriers need every workgroup resident at once
+  const int nwg = acm_sgd_nwg(bs);
   SPP_REQUIRE(nwg <= acm_sgd_max_wg(a, ob, ac), SPP_E_SHAPE, "acm_sgd: batch %d needs %d co-resident workgroups > %d",
               bs, nwg, acm_sgd_max_wg(a, ob, ac));
   if (nwg > 1) {
@@ -2031,7 +2044,7 @@ static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, i
   }
   const bool mw = nwg > 1;
 #define SPP_SGD_LAUNCH(IN_, AC_)                                                                      \
-  if (mw) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true>), dim3(nwg), dim3(kMlTH), 0, st, g);   \
+  if (mw) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true, kAcmWV>), dim3(nwg), dim3(64 * kAcmWV), 0, st, g);   \
   else hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, false>), dim3(1), dim3(kMlTH), 0, st, g)
   if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3);
   else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6);

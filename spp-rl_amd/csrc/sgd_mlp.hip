@@ -37,9 +37,9 @@
 
 namespace spp {
 
-constexpr int kMlR = 64;          // rows per workgroup and step (4 waves x 16)
-constexpr int kMlTH = 256;        // 4 waves
-constexpr int kMlRS = 68;         // row stride of the [unit][64 sample] images
+constexpr int kMlR = 64;          // rows per workgroup and step of the 4-wave form (4 waves x 16; WV waves: 16 WV)
+constexpr int kMlTH = 256;        // threads of the 4-wave form (WV waves: 64 WV)
+constexpr int kMlRS = 68;         // row stride of the 4-wave form's [unit][64 sample] images (WV waves: 16 WV + 4)
 constexpr int kMlMaxWG = 512;     // workgroups per step (bs <= 32,768)
 constexpr int kMlSlabMax = 8192;  // slab floats per workgroup (>= MlCfg::SLAB)
 
@@ -70,8 +70,12 @@ struct MlpSgdArgs {
   int spin;              // polls before an arrival wait times out (sppSetSgdSpinLimit; 0: the default)
 };
 
-template <int IN, int H2, int OUT, int HEAD>
+template <int IN, int H2, int OUT, int HEAD, int WV = 4>
 struct MlCfg {
+  static_assert(WV == 4 || WV == 8, "4 or 8 waves per workgroup");
+  static constexpr int R = 16 * WV;                 // rows per workgroup and step (16 per wave)
+  static constexpr int TH = 64 * WV;                // threads
+  static constexpr int RS = R + 4;                  // image row stride (result-layout stores: 64 distinct banks)
   static_assert(H2 == 32 || H2 == 64, "H2");
   static_assert(OUT >= 1 && OUT <= 32, "OUT");
   static constexpr int KQ1 = (IN + 1 + 3) / 4;     // fc1 k-steps (the inputs and the constant-1 row)
@@ -98,14 +102,14 @@ struct MlCfg {
   static constexpr int NPS = O_SC + 4;                  // slab floats
   static constexpr int NP4 = NPS / 4;
   static constexpr int SLAB = (NPS + 63) / 64 * 64;     // slab stride (floats)
-  static constexpr int K4 = (NP4 + kMlTH - 1) / kMlTH;  // float4 slots per thread (G = 1: all of them)
-  static constexpr int NXP = (kMlR * IN + kMlTH - 1) / kMlTH, NYP = (kMlR * OUT + kMlTH - 1) / kMlTH;
+  static constexpr int K4 = (NP4 + TH - 1) / TH;  // float4 slots per thread (G = 1: all of them)
+  static constexpr int NXP = (R * IN + TH - 1) / TH, NYP = (R * OUT + TH - 1) / TH;
   static_assert(SLAB <= kMlSlabMax && SLAB > NPS, "slab (and its dump word at NPS)");
   // G > 1: the shard's G slab chunks are staged in the image region, at most NP4 + G - 1 float4
-  static constexpr int RED4 = IMGR * kMlRS / 4;
+  static constexpr int RED4 = IMGR * RS / 4;
   static constexpr int MAXG = RED4 - NP4 + 1 < kMlMaxWG ? RED4 - NP4 + 1 : kMlMaxWG;
   static constexpr int RLC = HEAD == 1 ? 4 : 8;  // slab float4 loads in flight per thread (register budget)
-  static constexpr int NL = (NP4 + kMlTH - 1) / kMlTH;   // reloaded float4 per thread
+  static constexpr int NL = (NP4 + TH - 1) / TH;   // reloaded float4 per thread
 };
 
 __device__ __forceinline__ f32x4 ml_mfma16(float a, float b, f32x4 c) {
@@ -155,19 +159,25 @@ typedef __attribute__((address_space(3))) float ml_lds_f;
 __device__ __forceinline__ uint32_t lds_off(float* p) { return (uint32_t)(uintptr_t)(ml_lds_f*)p; }
 __device__ __forceinline__ void lds_st(uint32_t off, float v) { *(ml_lds_f*)(uintptr_t)off = v; }
 
-template <int IN, int H2, int OUT, int HEAD, bool MW>
-__global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
-  using C = MlCfg<IN, H2, OUT, HEAD>;
+// WV = 8: two waves per SIMD (128 rows per workgroup, half the workgroups of a step): every latency of one
+// wave's chain (LDS reads, dependent MFMAs, tanh) overlaps the other wave's work; <= 256 registers per wave.
+template <int IN, int H2, int OUT, int HEAD, bool MW, int WV = 4>
+__global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
+  using C = MlCfg<IN, H2, OUT, HEAD, WV>;
+  constexpr int TH = C::TH;
   constexpr bool GAUSS = HEAD == 1, VALUE = HEAD == 2;
   // G > 1, one pass per step: every gradient element goes to this workgroup's slab as soon as it is final
   // (write-through stores issued under the remaining tiles' MFMAs), not through the canonical LDS staging
   constexpr bool DIRECT = MW && !VALUE;
   static_assert(!VALUE || OUT == 1, "value head");
-  constexpr int RS = kMlRS, R = kMlR, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
+  constexpr int RS = C::RS, R = C::R, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
                 NO = C::NO;
   __shared__ __attribute__((aligned(16))) float IMG[C::IMGR * RS];  // H1 | D1 | H2 | D2 | D3; G > 1: the slab chunks
   __shared__ __attribute__((aligned(16))) float XT[C::XTR * RS];    // [input][sample]; row IN = 1 (rows < bs)
-  __shared__ __attribute__((aligned(16))) float GR[C::NPS + 4];     // the step's gradient, canonical order (+ dump)
+  // the step's gradient, canonical order (+ dump words at NPS, NPS + 1); the direct-store form (DIRECT) keeps
+  // only the dump word (its gradient goes straight to the slab)
+  constexpr int GRN = DIRECT ? 4 : C::NPS + 4, GRD = DIRECT ? 1 : C::NPS + 1;
+  __shared__ __attribute__((aligned(16))) float GR[GRN];
   __shared__ __attribute__((aligned(16))) float W1[64 * SW1];       // [unit][input]; column IN = b1
   __shared__ __attribute__((aligned(16))) float W2[H2 * SW2];
   __shared__ __attribute__((aligned(16))) float W3[16 * NO * SW3];  // rows >= OUT zero
@@ -175,9 +185,9 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   __shared__ float Y[R * OUT];
   __shared__ float LPO[GAUSS ? R : 1], ADV[GAUSS ? R : 1];
   __shared__ int64_t IDX[GAUSS ? 2 * R : 1];
-  __shared__ float BP[4][C::NBP];   // per wave: bias (and log_scale) gradient partials over its 16 samples
-  __shared__ float SCP[4][4];       // per wave: scalar partials
-  __shared__ float GT[GAUSS ? 4 : 1][3][32];  // HEAD 1, per wave: scale, variance, log(scale) of the step's log_scale
+  __shared__ float BP[WV][C::NBP];   // per wave: bias (and log_scale) gradient partials over its 16 samples
+  __shared__ float SCP[WV][4];       // per wave: scalar partials
+  __shared__ float GT[GAUSS ? WV : 1][3][32];  // HEAD 1, per wave: scale, variance, log(scale) of the step's log_scale
   __shared__ float adam_s[2][2];
   __shared__ int s_dead;
   float* const H1I = IMG;
@@ -212,33 +222,33 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     return B3[c - C::O_B3];
   };
   // ---- images (zero padding)
-  for (int i = t; i < 64 * SW1; i += kMlTH) W1[i] = 0.f;
-  for (int i = t; i < H2 * SW2; i += kMlTH) W2[i] = 0.f;
-  for (int i = t; i < 16 * NO * SW3; i += kMlTH) W3[i] = 0.f;
-  for (int i = t; i < C::XTR * RS; i += kMlTH) XT[i] = 0.f;  // rows > IN stay zero
+  for (int i = t; i < 64 * SW1; i += TH) W1[i] = 0.f;
+  for (int i = t; i < H2 * SW2; i += TH) W2[i] = 0.f;
+  for (int i = t; i < 16 * NO * SW3; i += TH) W3[i] = 0.f;
+  for (int i = t; i < C::XTR * RS; i += TH) XT[i] = 0.f;  // rows > IN stay zero
   if (t < 16 * NO) B3[t] = 0.f;
   if (t < 32) {
     LS[t] = 0.f;
     LIM[t] = t < OUT ? a.lim[t] : 0.f;
   }
   __syncthreads();
-  for (int c = t; c < NP; c += kMlTH) pref(c) = a.params[c];
+  for (int c = t; c < NP; c += TH) pref(c) = a.params[c];
   // ---- Adam moments of the owned float4 slots: slot f = f0 + t + 256 k (this workgroup's shard)
   const int C4 = (C::NP4 + G - 1) / G, f0 = g * C4, f1 = min(f0 + C4, C::NP4);
   const int c4n = max(f1 - f0, 0);  // this shard's float4 slots
   // (MW: G >= 2, so a shard holds at most ceil(NP4 / 2) slots)
-  constexpr int K4 = MW ? ((C::NP4 + 1) / 2 + kMlTH - 1) / kMlTH : C::K4;
+  constexpr int K4 = MW ? ((C::NP4 + 1) / 2 + TH - 1) / TH : C::K4;
   float mom[K4][4], vel[K4][4];
 #pragma unroll
   for (int k = 0; k < K4; ++k)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = f0 + t + kMlTH * k, c = 4 * f + i;
+      const int f = f0 + t + TH * k, c = 4 * f + i;
       const bool own = f < f1 && c < NP;
       mom[k][i] = own ? a.m[c] : 0.f;
       vel[k][i] = own ? a.v[c] : 0.f;
     }
-  double pw1 = 0.0, pw2 = 0.0;  // beta1^t, beta2^t of the next step (thread kMlTH - 1: pow once, then products)
+  double pw1 = 0.0, pw2 = 0.0;  // beta1^t, beta2^t of the next step (thread TH - 1: pow once, then products)
   auto adam_scalars = [&](int st) {
     if (st == 0) {
       pw1 = pow(0.9, (double)(a.step0 + 1));
@@ -267,24 +277,24 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       const float* yb = a.y + (live ? row_of(p, 0) * OUT : 0);
 #pragma unroll
       for (int k = 0; k < C::NXP; ++k) {
-        const int i = t + kMlTH * k;
+        const int i = t + TH * k;
         xp[k] = (live && i < bs * IN) ? xb[i] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < C::NYP; ++k) {
-        const int i = t + kMlTH * k;
+        const int i = t + TH * k;
         yp[k] = (live && i < bs * OUT) ? yb[i] : 0.f;
       }
       return;
     }
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
-      const int i = t + kMlTH * k, r = i / IN;
+      const int i = t + TH * k, r = i / IN;
       xp[k] = (live && i < bs * IN) ? a.x[row_of(p, r) * IN + i % IN] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < C::NYP; ++k) {
-      const int i = t + kMlTH * k, r = i / OUT;
+      const int i = t + TH * k, r = i / OUT;
       const bool ok = live && i < bs * OUT;
       yp[k] = ok ? a.y[row_of(p, r) * OUT + i % OUT] : 0.f;
       // the dist loss is data only: its per-step sum is taken when the rows are staged (not here, where it
@@ -305,13 +315,13 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   auto stage = [&](int p) {
 #pragma unroll
     for (int k = 0; k < C::NXP; ++k) {
-      const int i = t + kMlTH * k;
+      const int i = t + TH * k;
       if (i < R * IN) XT[(i % IN) * RS + i / IN] = xp[k];
     }
     if (t < R) XT[IN * RS + t] = t < pass_rows(p) ? 1.f : 0.f;
 #pragma unroll
     for (int k = 0; k < C::NYP; ++k) {
-      const int i = t + kMlTH * k;
+      const int i = t + TH * k;
       if (i < R * OUT) Y[i] = yp[k];
     }
     if constexpr (GAUSS) {
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     }
   };
   load_idx(0);
-  if (t == kMlTH - 1) adam_scalars(0);
+  if (t == TH - 1) adam_scalars(0);
   __syncthreads();
   prefetch(0);
   load_idx(1);
@@ -344,8 +354,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   for (int k = 0; k < (MW ? C::NL : 1); ++k)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = 4 * (t + kMlTH * k) + i;
-      roff[k][i] = lds_off(c < NP ? &pref(c) : &GR[C::NPS + 1]);
+      const int c = 4 * (t + TH * k) + i;
+      roff[k][i] = lds_off(c < NP ? &pref(c) : &GR[GRD]);
     }
   SPP_TP_INIT();
   float loss_acc = 0.f;  // HEAD 0 / 2: sum over steps of the batch loss (the scalar slot's owner)
@@ -583,8 +593,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     }
     __syncthreads();  // the images hold all 64 samples
     SPP_TP(3);
-    // ---- weight gradients: 16x16 tiles over the 64 samples (k-step ks of lane group q = sample 16q + ks),
-    // tiles w, w + 4, ... of this wave two at a time; each finished tile goes to GR in canonical order
+    // ---- weight gradients: 16x16 tiles over the R samples (k-step ks of lane group q = sample (R/4) q + ks),
+    // tiles w, w + WV, ... of this wave two at a time; each finished tile goes to GR in canonical order
     auto tile_rows = [&](int tt, const float*& ar, const float*& br, int& layer, int& mt, int& nt) {
       if (tt < C::NT1) {
         layer = 0; mt = tt / C::NIT1; nt = tt - mt * C::NIT1;
@@ -598,8 +608,8 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         layer = 2; mt = u / NB2; nt = u - mt * NB2;
         ar = D3I; br = H2I;
       }
-      ar += (16 * mt + n) * RS + 16 * q;
-      br += (16 * nt + n) * RS + 16 * q;
+      ar += (16 * mt + n) * RS + (R / 4) * q;
+      br += (16 * nt + n) * RS + (R / 4) * q;
     };
     // (elements outside the parameters -- dW1's padding columns, dW3's rows >= OUT -- go to the dump word
     // GR[NPS]: every lane stores, no divergent branch)
@@ -624,19 +634,20 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         else acc_to(GR[ok ? c0 + i * dc : C::NPS], acc[i]);
       }
     };
-    for (int tt = w; tt < C::NT; tt += 8) {  // (wave-uniform; a missing second tile repeats the first, unstored)
-      const bool two = tt + 4 < C::NT;
+    for (int tt = w; tt < C::NT; tt += 2 * WV) {  // (wave-uniform; a missing second tile repeats the first)
+      const bool two = tt + WV < C::NT;
       const float *a0, *b0, *a1, *b1;
       int l0, m0, n0, l1, m1, n1;
       tile_rows(tt, a0, b0, l0, m0, n0);
-      tile_rows(two ? tt + 4 : tt, a1, b1, l1, m1, n1);
+      tile_rows(two ? tt + WV : tt, a1, b1, l1, m1, n1);
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
       float4 x0 = reinterpret_cast<const float4*>(a0)[0], y0 = reinterpret_cast<const float4*>(b0)[0];
       float4 x1 = reinterpret_cast<const float4*>(a1)[0], y1 = reinterpret_cast<const float4*>(b1)[0];
+      constexpr int NCQ = R / 16;  // float4 groups of a lane group's R / 4 samples
 #pragma unroll
-      for (int cq = 0; cq < 4; ++cq) {
+      for (int cq = 0; cq < NCQ; ++cq) {
         float4 nx0, ny0, nx1, ny1;
-        if (cq < 3) {  // the next 4 samples' operands in flight under this group's MFMAs
+        if (cq < NCQ - 1) {  // the next 4 samples' operands in flight under this group's MFMAs
           nx0 = reinterpret_cast<const float4*>(a0)[cq + 1];
           ny0 = reinterpret_cast<const float4*>(b0)[cq + 1];
           nx1 = reinterpret_cast<const float4*>(a1)[cq + 1];
@@ -650,7 +661,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         c1 = ml_mfma16(x1.z, y1.z, c1);
         c0 = ml_mfma16(x0.w, y0.w, c0);
         c1 = ml_mfma16(x1.w, y1.w, c1);
-        if (cq < 3) {
+        if (cq < NCQ - 1) {
           x0 = nx0; y0 = ny0; x1 = nx1; y1 = ny1;
         }
       }
@@ -668,7 +679,18 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
    }  // passes
     // ---- bias (and log_scale) gradients: the waves' partials in a fixed order; scalars -> GR[O_SC ..]
     {
-      auto wsum = [&](int j) { return ((BP[0][j] + BP[1][j]) + BP[2][j]) + BP[3][j]; };
+      auto wsum = [&](int j) {  // waves in order
+        float v = BP[0][j];
+#pragma unroll
+        for (int k = 1; k < WV; ++k) v += BP[k][j];
+        return v;
+      };
+      auto scsum = [&](int j) {
+        float v = SCP[0][j];
+#pragma unroll
+        for (int k = 1; k < WV; ++k) v += SCP[k][j];
+        return v;
+      };
       auto put = [&](int c, float v) {
         if constexpr (DIRECT) slab_st1(mine, c, v);
         else GR[c] = v;
@@ -682,8 +704,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
       }
       // scalars (HEAD 1's dist partial at O_SC + 2 is written below, after its reduction)
       if (t < 4 && !(GAUSS && t == 2))
-        put(C::O_SC + t, t == 0 ? ((SCP[0][0] + SCP[1][0]) + SCP[2][0]) + SCP[3][0]
-                                : (GAUSS && t == 1 ? ((SCP[0][1] + SCP[1][1]) + SCP[2][1]) + SCP[3][1] : 0.f));
+        put(C::O_SC + t, t == 0 ? scsum(0) : (GAUSS && t == 1 ? scsum(1) : 0.f));
       if (t >= 192 && t - 192 < C::O_SC - NP) put(NP + t - 192, 0.f);
     }
     if constexpr (GAUSS) {  // the dist partials of every thread (this step's rows)
@@ -693,7 +714,9 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     __syncthreads();
     if constexpr (GAUSS) {
       if (t == 0) {
-        const float ds = ((SCP[0][2] + SCP[1][2]) + SCP[2][2]) + SCP[3][2];
+        float ds = SCP[0][2];
+#pragma unroll
+        for (int k = 1; k < WV; ++k) ds += SCP[k][2];
         if constexpr (DIRECT) slab_st1(mine, C::O_SC + 2, ds);
         else GR[C::O_SC + 2] = ds;
       }
@@ -710,21 +733,21 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     const auto all = sgd_rsrc(a.slab + (int64_t)(st & 1) * G * C::SLAB);  // (G = 1: unused)
     if constexpr (MW) {
       if constexpr (!DIRECT)  // (HEAD 2: the passes' sums staged in GR)
-        for (int f = t; f < C::NP4; f += kMlTH) {
+        for (int f = t; f < C::NP4; f += TH) {
           const float4 v4 = *reinterpret_cast<const float4*>(GR + 4 * f);
           slab_st4(mine, 4 * f, v4);
         }
       // the next step's Adam scalars (thread 255's double-precision powers) while lane 0 polls
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, a.spin, [&] {
-        if (t == kMlTH - 1) adam_scalars(st + 1);
+        if (t == TH - 1) adam_scalars(st + 1);
       });
       // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
       const int nit = c4n * G;
-      for (int i0 = 0; i0 < nit; i0 += C::RLC * kMlTH) {  // (G = 17, 64-wide AcM: one round)
+      for (int i0 = 0; i0 < nit; i0 += C::RLC * TH) {  // (G = 17, 64-wide AcM: one round)
         float4 ld[C::RLC];
 #pragma unroll
         for (int k = 0; k < C::RLC; ++k) {
-          const int i = i0 + t + kMlTH * k;
+          const int i = i0 + t + TH * k;
           if (i < nit) {
             const int src = i / c4n;
             ld[k] = slab_ld4(all, src * C::SLAB + 4 * (f0 + i - src * c4n));
@@ -732,7 +755,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < C::RLC; ++k) {
-          const int i = i0 + t + kMlTH * k;
+          const int i = i0 + t + TH * k;
           if (i < nit) reinterpret_cast<float4*>(IMG)[i] = ld[k];
         }
       }
@@ -740,12 +763,12 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
     }
     SPP_TP(6);
     const float neg_step = adam_s[st & 1][0], bc2s = adam_s[st & 1][1];
-    if (!MW && t == kMlTH - 1) adam_scalars(st + 1);  // (G > 1: computed during the arrival wait)
+    if (!MW && t == TH - 1) adam_scalars(st + 1);  // (G > 1: computed during the arrival wait)
     const float omb1 = 0.1f, b2c = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     const auto pub = sgd_rsrc(a.pbuf);
 #pragma unroll
     for (int k = 0; k < K4; ++k) {
-      const int f = f0 + t + kMlTH * k;
+      const int f = f0 + t + TH * k;
       if (f < f1) {
         float4 gg4;
         if constexpr (MW) {
@@ -796,7 +819,7 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {  // (this shard's own slots reload the values it published)
         rv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (t + kMlTH * k < C::NP4) rv[k] = slab_ld4(pub, 4 * (t + kMlTH * k));
+        if (t + TH * k < C::NP4) rv[k] = slab_ld4(pub, 4 * (t + TH * k));
       }
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {
@@ -812,19 +835,19 @@ __global__ __launch_bounds__(kMlTH, 1) void k_mlp_sgd(MlpSgdArgs a) {
   SPP_TP_FLUSH();
   // ---- write back: parameters (workgroup 0, from its images), moments (each shard's owner)
   if (g == 0)
-    for (int c = t; c < NP; c += kMlTH) a.params[c] = pref(c);
+    for (int c = t; c < NP; c += TH) a.params[c] = pref(c);
 #pragma unroll
   for (int k = 0; k < K4; ++k)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = f0 + t + kMlTH * k, c = 4 * f + i;
+      const int f = f0 + t + TH * k, c = 4 * f + i;
       if (f < f1 && c < NP) {
         a.m[c] = mom[k][i];
         a.v[c] = vel[k][i];
       }
     }
-  constexpr int fsc = C::O_SC / 4;  // the scalar slot: owned by thread (fsc - f0) % kMlTH of its shard
-  if (!GAUSS && fsc >= f0 && fsc < f1 && (fsc - f0) % kMlTH == t) *a.loss_sum += loss_acc;
+  constexpr int fsc = C::O_SC / 4;  // the scalar slot: owned by thread (fsc - f0) % TH of its shard
+  if (!GAUSS && fsc >= f0 && fsc < f1 && (fsc - f0) % TH == t) *a.loss_sum += loss_acc;
 }
 
 }  // namespace spp

@@ -164,6 +164,7 @@ _SIGS = {
     "sppSetSgdSpinLimit": (c_int, [c_int]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppAcmSgdMaxBatch": (c_int, [c_void_p]),
+    "sppAcmSgdWorkgroups": (c_int, [c_void_p, c_int]),
     "sppDebugReadProf": (c_int, [c_void_p, c_int]),
     "sppDebugDense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
 }

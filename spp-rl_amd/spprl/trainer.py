@@ -624,8 +624,8 @@ class OffPolicyLoop:
         return bs <= self._sgd_max_bs
 
     def acm_sgd_workgroups(self):
-        """Workgroups of one multi-workgroup sppAcmSgd step at acm_batch_size (64 rows each; 1 below that)."""
-        return max(1, -(-int(self.acm_batch_size) // 64))
+        """Workgroups (one per CU) of one sppAcmSgd step at acm_batch_size (sppAcmSgdWorkgroups)."""
+        return max(1, int(load().sppAcmSgdWorkgroups(self._h, int(self.acm_batch_size))))
 
     def _acm_sgd(self, idx, nsteps, bs, nrows=None):
         """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd); with nrows,
@@ -675,7 +675,7 @@ class OffPolicyLoop:
         self._acm_loss_acc.zero_()
         if self._acm_sgd_ok(self.acm_batch_size):
             self._acm_sgd(self._rand_idx(n_batches * self.acm_batch_size, n), n_batches, self.acm_batch_size)
-            if self.acm_batch_size > 64:
+            if self.acm_sgd_workgroups() > 1:
                 self._acm_sgd_check()
         else:
             for _ in range(n_batches):
@@ -713,7 +713,7 @@ class OffPolicyLoop:
                     self._acm_loss_acc += self._acm_loss
             self._acm_loss_acc /= max(nb, 1)
             self._acm_sched_epochs += 1
-        if self.acm_batch_size > 64 and self._acm_sgd_ok(self.acm_batch_size):  # a multi-workgroup launch ran
+        if self.acm_sgd_workgroups() > 1 and self._acm_sgd_ok(self.acm_batch_size):  # a multi-workgroup launch ran
             self._acm_sgd_check()
         self._set_acm_lr(self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step))
 

@@ -203,6 +203,13 @@ def cpu_baseline_report(name, seconds, procs):
     if ref_per_core:
         out["reference_per_core_measured_in_survey"] = ref_per_core
         out["port_vs_reference_per_core"] = round(one["value"] / ref_per_core, 3)
+        out["calibration"] = (
+            "port_vs_reference_per_core divides this host's port rate by the reference's rate measured on the build "
+            "container's CPU (SURVEY Appendix B): two different CPUs.  Same host, same moment "
+            "(tools/cpu_calibrate.py, profiles/r05/cpu_calibrate.txt): the reference's SAC_AcM.update (B = 100, one "
+            "thread) takes 1.03-1.08x the port's over two runs (12.96 vs 12.55 ms, 8.77 vs 8.11 ms) since the port "
+            "steps the reference's own optimizer class, torch.optim.Adam; with round 4's restated Adam the port's "
+            "update was 1.31-1.38x faster, and the rest of round 4's 2.27x is the faster host CPU")
     return out
 
 

@@ -405,11 +405,11 @@ def hbm_kernels(ag, cfg, B, E):
     rec("obs_stats", ms, n * (4 * ob + 8), "one read of the live rows: len x (4 ob + 8 obs_idx)")
     idx = torch.randint(0, n, (B,), device=ag.device)
     acmc = cfg["algo"] != "vanilla"
-    per_s = 24 + 8 * ob + 4 * ac + 5 + (0 if acmc else 4 * aout)
+    per_s = 16 + 8 * ob + 4 * ac + 5 + (0 if acmc else 4 * aout)
     per_w = 4 * (2 * ob + ac + 2 + (0 if acmc else aout))
     ms = cuda_time(lambda: _lib.call("sppAgentStageFromReplay", ag._h, rb._h, _lib.ptr(idx), B, _lib.stream_handle()))
-    rec("replay_stage", ms, B * (per_s + per_w), "per sample: 8 idx + 16 (obs_idx, next_idx) + gathered row values "
-        "+ the same values written feature-major")
+    rec("replay_stage", ms, B * (per_s + per_w), "per sample: 8 idx + 8 (the record's 32-bit obs / next-obs slots) + "
+        "gathered values (2 obs rows, ACM action, reward, done) + the same values written feature-major")
     obs = torch.randn(E, ob, device=ag.device)
 
     def add():

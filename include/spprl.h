@@ -131,16 +131,16 @@ int sppReplayObsStatsDP1SampleRows(sppReplayHandle h, int world, int64_t n_globa
 sppStatus sppReplayObsStatsDP1(sppReplayHandle h, int phase, int world, int rank, const float* pivot /*[ob]*/,
                                uint32_t* samp, double* exch, uint32_t* hist, int64_t n_global, float* mean,
                                float* std, float* max_obs, float* min_obs, int first_update, void* stream);
-/* Raw device pointers of the ring (for the fused sample+update path). */
+/* Raw device pointers of the ring.  A timestep is ONE 64-B-aligned record of rec_words 32-bit words:
+ *   0 obs slot, 1 next-obs slot (uint32; capacity < 2^31), 2 reward (fp32), 3 done (bit 0) | end (bit 8),
+ *   rec_acm .. rec_acm + ac - 1 the ACM action, rec_act .. rec_act + aout - 1 the stored actor output (fp32);
+ * a sampled transition then reads one record and two obs rows.  obs_idx repeats word 0 as a contiguous
+ * int64 array (the obs statistics walk every live row through it). */
 typedef struct {
-  float* obs;          /* [capacity][ob]    */
-  int64_t* obs_idx;    /* [capacity]        */
-  int64_t* next_idx;   /* [capacity]        */
-  float* act;          /* [capacity][aout]  */
-  float* acm;          /* [capacity][ac]    */
-  float* rew;          /* [capacity]        */
-  uint8_t* done;       /* [capacity]        */
-  uint8_t* end;        /* [capacity]        */
+  float* obs;          /* [capacity][ob]        */
+  int64_t* obs_idx;    /* [capacity]            */
+  uint32_t* rec;       /* [capacity][rec_words] */
+  int rec_words, rec_acm, rec_act;
 } sppReplayView;
 /* Raw device arrays of the ring; counts as a possible write (the next ObsStats re-brackets). */
 sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* out);

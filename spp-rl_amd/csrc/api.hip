@@ -180,6 +180,8 @@ sppStatus sppRandIndex(int64_t* out, int64_t n, int64_t high, uint64_t seed, uin
 // ------------------------------------------------------------------ replay
 sppStatus sppReplayCreate(sppReplayHandle* out, int64_t cap, int ob, int aout, int ac, int device) {
   SPP_REQUIRE(out && cap > 0 && ob > 0 && aout > 0 && ac > 0, SPP_E_INVALID_ARG, "replay create: bad args");
+  SPP_REQUIRE(cap < (int64_t)1 << 31, SPP_E_INVALID_ARG, "replay create: capacity %lld >= 2^31 (32-bit slots)",
+              (long long)cap);
   SPP_CHECK_HIP(hipSetDevice(device));
   auto* h = new sppReplay;
   h->device = device;
@@ -192,18 +194,14 @@ sppStatus sppReplayCreate(sppReplayHandle* out, int64_t cap, int ob, int aout, i
   d.ob = ob;
   d.aout = aout;
   d.ac = ac;
+  d.rw = rec_words(aout, ac);
   hipError_t e = hipSuccess;
   e = e ? e : hipMalloc(&d.obs, sizeof(float) * cap * ob);
   e = e ? e : hipMalloc(&d.obs_idx, sizeof(int64_t) * cap);
-  e = e ? e : hipMalloc(&d.next_idx, sizeof(int64_t) * cap);
-  e = e ? e : hipMalloc(&d.act, sizeof(float) * cap * aout);
-  e = e ? e : hipMalloc(&d.acm, sizeof(float) * cap * ac);
-  e = e ? e : hipMalloc(&d.rew, sizeof(float) * cap);
-  e = e ? e : hipMalloc(&d.done, cap);
-  e = e ? e : hipMalloc(&d.end, cap);
+  e = e ? e : hipMalloc(&d.rec, sizeof(uint32_t) * cap * d.rw);  // (hipMalloc: 256-B aligned, records 64 B)
   e = e ? e : hipMemset(d.obs, 0, sizeof(float) * cap * ob);
   e = e ? e : hipMemset(d.obs_idx, 0, sizeof(int64_t) * cap);
-  e = e ? e : hipMemset(d.next_idx, 0, sizeof(int64_t) * cap);
+  e = e ? e : hipMemset(d.rec, 0, sizeof(uint32_t) * cap * d.rw);
   if (e != hipSuccess) {
     set_error("replay alloc (%lld x %d): %s", (long long)cap, ob, hipGetErrorString(e));
     delete h;
@@ -219,8 +217,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
   hipSetDevice(h->device);
   hipDeviceSynchronize();
   ReplayDev& d = h->d;
-  hipFree(d.obs); hipFree(d.obs_idx); hipFree(d.next_idx); hipFree(d.act); hipFree(d.acm);
-  hipFree(d.rew); hipFree(d.done); hipFree(d.end);
+  hipFree(d.obs); hipFree(d.obs_idx); hipFree(d.rec);
   for (int i = 0; i < sppReplay::kRing; ++i) {
     if (h->pinned[i]) hipHostFree(h->pinned[i]);
     if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
@@ -327,12 +324,10 @@ sppStatus sppReplayGetView(sppReplayHandle h, sppReplayView* v) {
   ++h->gen;  // the caller may write the ring through the view
   v->obs = h->d.obs;
   v->obs_idx = h->d.obs_idx;
-  v->next_idx = h->d.next_idx;
-  v->act = h->d.act;
-  v->acm = h->d.acm;
-  v->rew = h->d.rew;
-  v->done = h->d.done;
-  v->end = h->d.end;
+  v->rec = h->d.rec;
+  v->rec_words = h->d.rw;
+  v->rec_acm = kRecAcm;
+  v->rec_act = rec_act(h->d);
   return SPP_OK;
 }
 
@@ -370,10 +365,10 @@ sppStatus sppReplayLastRollout(sppReplayHandle h, int64_t* first, int64_t* lengt
   if (h->ts_idx == 0 && len == h->d.cap) {
     // python index ts_idx - 1 = -1 is the array's last element; when it is an end, the reference's
     // walk wraps to that same element at once (i = -2 -> current_len - 1) and stops: a 1-step rollout
-    uint8_t e = 0;
-    SPP_CHECK_HIP(hipMemcpyAsync(&e, h->d.end + (len - 1), 1, hipMemcpyDeviceToHost, st));
+    uint32_t w3 = 0;  // the last record's done | end word
+    SPP_CHECK_HIP(hipMemcpyAsync(&w3, h->d.rec + (len - 1) * h->d.rw + 3, 4, hipMemcpyDeviceToHost, st));
     SPP_CHECK_HIP(hipStreamSynchronize(st));
-    if (e) {
+    if ((w3 >> 8) & 1u) {
       *first = len - 1;
       *length = 1;
       return SPP_OK;
@@ -382,7 +377,8 @@ sppStatus sppReplayLastRollout(sppReplayHandle h, int64_t* first, int64_t* lengt
   const int64_t p = h->ts_idx > 0 ? std::min(h->ts_idx - 1, len - 1) : len - 1;
   int64_t* d = nullptr;
   SPP_CHECK_HIP(hipMallocAsync((void**)&d, 2 * sizeof(int64_t), st));
-  hipLaunchKernelGGL(k_replay_last_rollout, dim3(1), dim3(1024), 0, st, (const uint8_t*)h->d.end, len, p, d);
+  hipLaunchKernelGGL(k_replay_last_rollout, dim3(1), dim3(1024), 0, st, (const uint32_t*)h->d.rec, h->d.rw, len, p,
+                     d);
   int64_t hb[2] = {-1, -1};
   SPP_CHECK_HIP(hipMemcpyAsync(hb, d, sizeof(hb), hipMemcpyDeviceToHost, st));
   SPP_CHECK_HIP(hipFreeAsync(d, st));

@@ -13,10 +13,10 @@ __global__ void k_replay_add_obs(float* obs, int64_t cap, int ob, const float* s
   obs[((base + e) % cap) * ob + f] = src[i];
 }
 
-// add_acm_action (:332-333) + add_timestep (:65-75) + ReplayBuffer.addition (:133-137).
-// One thread per element: [E][aout] action values, then [E][ac] ACM actions, then the E scalar
-// records, so consecutive lanes write consecutive floats of consecutive timestep rows (the
-// rows of one vector step are consecutive slots except at the Q6 wrap).
+// add_acm_action (:332-333) + add_timestep (:65-75) + ReplayBuffer.addition (:133-137) into the timestep
+// records (replay.h).  One thread per element: [E][aout] action values, then [E][ac] ACM actions, then the E
+// record heads (one 16-B store each, plus the obs_idx array), so consecutive lanes write consecutive words of
+// consecutive records (the rows of one vector step are consecutive slots except at the Q6 wrap).
 __global__ void k_replay_add_step(ReplayDev r, const int64_t* __restrict__ meta /*[3][E]: prev, next, ts*/, int E,
                                   const float* act, const float* acm, const float* rew, const uint8_t* done,
                                   const uint8_t* end) {
@@ -24,18 +24,17 @@ __global__ void k_replay_add_step(ReplayDev r, const int64_t* __restrict__ meta 
   const int64_t na = (int64_t)E * r.aout, nm = (int64_t)E * r.ac;
   if (i < na) {
     const int64_t e = i / r.aout, f = i - e * r.aout;
-    r.act[meta[2 * E + e] * r.aout + f] = act ? act[i] : 0.f;
+    r.rec[meta[2 * E + e] * r.rw + rec_act(r) + f] = __float_as_uint(act ? act[i] : 0.f);
   } else if (i < na + nm) {
     const int64_t j = i - na, e = j / r.ac, f = j - e * r.ac;
-    r.acm[meta[2 * E + e] * r.ac + f] = acm ? acm[j] : 0.f;
+    r.rec[meta[2 * E + e] * r.rw + kRecAcm + f] = __float_as_uint(acm ? acm[j] : 0.f);
   } else if (i < na + nm + E) {
     const int e = (int)(i - na - nm);
     const int64_t t = meta[2 * E + e];
     r.obs_idx[t] = meta[e];
-    r.next_idx[t] = meta[E + e];
-    r.rew[t] = rew[e];
-    r.done[t] = done[e];
-    r.end[t] = end[e];
+    *reinterpret_cast<uint4*>(r.rec + t * r.rw) =
+        make_uint4((uint32_t)meta[e], (uint32_t)meta[E + e], __float_as_uint(rew[e]),
+                   (uint32_t)(done[e] != 0) | ((uint32_t)(end[e] != 0) << 8));
   }
 }
 
@@ -46,17 +45,19 @@ __global__ void k_replay_gather_rm(ReplayDev r, const int64_t* __restrict__ idx,
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int64_t t = idx[b];
-  const int64_t o = r.obs_idx[t], n = r.next_idx[t];
+  const uint32_t* rc = r.rec + t * r.rw;
+  const uint4 hd = *reinterpret_cast<const uint4*>(rc);
+  const int64_t o = hd.x, n = hd.y;
   for (int f = 0; f < r.ob; ++f) {
     if (obs) obs[(int64_t)b * r.ob + f] = r.obs[o * r.ob + f];
     if (nobs) nobs[(int64_t)b * r.ob + f] = r.obs[n * r.ob + f];
   }
   if (act)
-    for (int f = 0; f < r.aout; ++f) act[(int64_t)b * r.aout + f] = r.act[t * r.aout + f];
+    for (int f = 0; f < r.aout; ++f) act[(int64_t)b * r.aout + f] = __uint_as_float(rc[rec_act(r) + f]);
   if (acm)
-    for (int f = 0; f < r.ac; ++f) acm[(int64_t)b * r.ac + f] = r.acm[t * r.ac + f];
-  if (rew) rew[b] = r.rew[t];
-  if (done) done[b] = (int8_t)r.done[t];
+    for (int f = 0; f < r.ac; ++f) acm[(int64_t)b * r.ac + f] = __uint_as_float(rc[kRecAcm + f]);
+  if (rew) rew[b] = __uint_as_float(hd.z);
+  if (done) done[b] = (int8_t)(hd.w & 1u);
 }
 
 // Fused sample -> feature-major staging of the update batch (zero padded to Bp).
@@ -67,13 +68,15 @@ __global__ void k_replay_gather_rm(ReplayDev r, const int64_t* __restrict__ idx,
 // so both the random-row gather and the transposed store are coalesced.
 constexpr int kStageTile = 64;
 
-__device__ __forceinline__ void stage_rows(const float* __restrict__ src, const int64_t* rows, int w, int valid,
-                                           float* lds, float* dst, int64_t Bp, int64_t b0) {
+// element (row, f) of the source at src[row * stride + f] (obs rows: stride = w; record fields: stride = rw,
+// src = the field's first word)
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, int64_t stride, const int64_t* rows, int w,
+                                           int valid, float* lds, float* dst, int64_t Bp, int64_t b0) {
   // rows [b0, b0 + kStageTile) of the padded batch; only b < Bp exist in dst
   const int n = kStageTile * w;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int s = i / w, f = i - s * w;
-    lds[s * w + f] = s < valid ? src[rows[s] * w + f] : 0.f;
+    lds[s * w + f] = s < valid ? src[rows[s] * stride + f] : 0.f;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -93,19 +96,21 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm(ReplayDev r, const int6
   if (threadIdx.x < kStageTile) {
     const int s = threadIdx.x;
     const int64_t t = s < valid ? idx[b0 + s] : 0;
+    const uint4 hd = s < valid ? *reinterpret_cast<const uint4*>(r.rec + t * r.rw) : make_uint4(0, 0, 0, 0);
     rt[s] = t;
-    ro[s] = s < valid ? r.obs_idx[t] : 0;
-    rn[s] = s < valid ? r.next_idx[t] : 0;
+    ro[s] = hd.x;
+    rn[s] = hd.y;
     if (b0 + s < Bp) {
-      R[b0 + s] = s < valid ? r.rew[t] : 0.f;
-      DN[b0 + s] = s < valid ? (float)r.done[t] : 0.f;
+      R[b0 + s] = __uint_as_float(hd.z);
+      DN[b0 + s] = (float)(hd.w & 1u);
     }
   }
   __syncthreads();
-  stage_rows(r.obs, ro, r.ob, valid, stg, S, Bp, b0);
-  stage_rows(r.obs, rn, r.ob, valid, stg, S2, Bp, b0);
-  if (ACT) stage_rows(r.act, rt, r.aout, valid, stg, ACT, Bp, b0);
-  stage_rows(r.acm, rt, r.ac, valid, stg, AENV, Bp, b0);
+  const float* recf = reinterpret_cast<const float*>(r.rec);
+  stage_rows(r.obs, r.ob, ro, r.ob, valid, stg, S, Bp, b0);
+  stage_rows(r.obs, r.ob, rn, r.ob, valid, stg, S2, Bp, b0);
+  if (ACT) stage_rows(recf + rec_act(r), r.rw, rt, r.aout, valid, stg, ACT, Bp, b0);
+  stage_rows(recf + kRecAcm, r.rw, rt, r.ac, valid, stg, AENV, Bp, b0);
 }
 
 // Second form (the default): kStage2Tile = 32 samples per workgroup, the four row gathers (obs,
@@ -144,8 +149,8 @@ __device__ __forceinline__ int stage2_items(const Stage2Geo& G, int wv) {
   return ks * G.nc;
 }
 
-__device__ __forceinline__ void stage2_gather(const float* __restrict__ src, const int64_t* rows, int valid,
-                                              const Stage2Geo& G, int wv, float* l) {
+__device__ __forceinline__ void stage2_gather(const float* __restrict__ src, int64_t stride, const int64_t* rows,
+                                              int valid, const Stage2Geo& G, int wv, float* l) {
   const int n = stage2_items(G, wv), ls = stage2_stride(G.w);
   for (int i0 = 0; i0 < n; i0 += kStage2Ld) {
     float v[kStage2Ld];
@@ -157,7 +162,7 @@ __device__ __forceinline__ void stage2_gather(const float* __restrict__ src, con
       const int s = (wv + 4 * k) * G.G + G.g, f = G.f0 + 64 * j;
       const bool ok = i < n && G.on && s < kStage2Tile && f < G.w;
       at[u] = ok ? s * ls + f : -1;
-      v[u] = (ok && s < valid) ? src[rows[s] * G.w + f] : 0.f;
+      v[u] = (ok && s < valid) ? src[rows[s] * stride + f] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < kStage2Ld; ++u)
@@ -182,12 +187,13 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm2(ReplayDev r, const int
   if (tid < kStage2Tile) {
     const int s = tid;
     const int64_t t = s < valid ? idx[b0 + s] : 0;
+    const uint4 hd = s < valid ? *reinterpret_cast<const uint4*>(r.rec + t * r.rw) : make_uint4(0, 0, 0, 0);
     rt[s] = t;
-    ro[s] = s < valid ? r.obs_idx[t] : 0;
-    rn[s] = s < valid ? r.next_idx[t] : 0;
+    ro[s] = hd.x;
+    rn[s] = hd.y;
     if (b0 + s < Bp) {
-      R[b0 + s] = s < valid ? r.rew[t] : 0.f;
-      DN[b0 + s] = s < valid ? (float)r.done[t] : 0.f;
+      R[b0 + s] = __uint_as_float(hd.z);
+      DN[b0 + s] = (float)(hd.w & 1u);
     }
   }
   __syncthreads();
@@ -196,10 +202,11 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm2(ReplayDev r, const int
   float* la = ln + kStage2Tile * stage2_stride(r.ob);
   float* lm = la + (ACT ? kStage2Tile * stage2_stride(r.aout) : 0);
   const Stage2Geo go(r.ob, lane), gm(r.ac, lane);
-  stage2_gather(r.obs, ro, valid, go, wv, lo);
-  stage2_gather(r.obs, rn, valid, go, wv, ln);
-  if (ACT) stage2_gather(r.act, rt, valid, Stage2Geo(r.aout, lane), wv, la);
-  stage2_gather(r.acm, rt, valid, gm, wv, lm);
+  const float* recf = reinterpret_cast<const float*>(r.rec);
+  stage2_gather(r.obs, r.ob, ro, valid, go, wv, lo);
+  stage2_gather(r.obs, r.ob, rn, valid, go, wv, ln);
+  if (ACT) stage2_gather(recf + rec_act(r), r.rw, rt, valid, Stage2Geo(r.aout, lane), wv, la);
+  stage2_gather(recf + kRecAcm, r.rw, rt, valid, gm, wv, lm);
   __syncthreads();
   stage2_store(lo, r.ob, S, Bp, b0);
   stage2_store(ln, r.ob, S2, Bp, b0);
@@ -210,8 +217,8 @@ __global__ __launch_bounds__(256) void k_replay_stage_fm2(ReplayDev r, const int
 // last_end (replay_buffer.py:170-177) and the walk of last_rollout (:335-383): out[0] = the first
 // index at distance 0, 1, ... back from p (cyclic over [0, len)) with end set; out[1] = the first
 // one at distance 1 .. len back from out[0] (itself when it is the only end).  -1: none.
-__global__ __launch_bounds__(1024) void k_replay_last_rollout(const uint8_t* __restrict__ end, int64_t len, int64_t p,
-                                                              int64_t* out) {
+__global__ __launch_bounds__(1024) void k_replay_last_rollout(const uint32_t* __restrict__ rec, int rw, int64_t len,
+                                                              int64_t p, int64_t* out) {
   __shared__ int best;
   __shared__ int64_t at;
   const int tid = threadIdx.x;
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(1024) void k_replay_last_rollout(const uint8_t* __r
       if (k < k1) {
         int64_t i = (from - k) % len;
         if (i < 0) i += len;
-        if (end[i]) atomicMin(&best, (int)(k - base));
+        if ((rec[i * rw + 3] >> 8) & 1u) atomicMin(&best, (int)(k - base));  // the record's end flag
       }
       __syncthreads();
       const int b = best;
@@ -256,9 +263,10 @@ __global__ __launch_bounds__(256) void k_replay_gather_acm(ReplayDev r, const in
   const int valid = (int)min((int64_t)kStageTile, (int64_t)B - b0);
   if (threadIdx.x < valid) {
     const int64_t t = idx[b0 + threadIdx.x];
+    const uint2 hd = *reinterpret_cast<const uint2*>(r.rec + t * r.rw);
     rt[threadIdx.x] = t;
-    ro[threadIdx.x] = r.obs_idx[t];
-    rn[threadIdx.x] = r.next_idx[t];
+    ro[threadIdx.x] = hd.x;
+    rn[threadIdx.x] = hd.y;
   }
   __syncthreads();
   const int ob = r.ob, w = 2 * ob;
@@ -268,7 +276,7 @@ __global__ __launch_bounds__(256) void k_replay_gather_acm(ReplayDev r, const in
   }
   for (int i = threadIdx.x; i < valid * r.ac; i += blockDim.x) {
     const int s = i / r.ac, f = i - s * r.ac;
-    y[(b0 + s) * r.ac + f] = r.acm[rt[s] * r.ac + f];
+    y[(b0 + s) * r.ac + f] = __uint_as_float(r.rec[rt[s] * r.rw + kRecAcm + f]);
   }
 }
 

@@ -48,8 +48,8 @@ class Batch(ctypes.Structure):
 
 
 class ReplayView(ctypes.Structure):
-    _fields_ = [("obs", c_void_p), ("obs_idx", c_void_p), ("next_idx", c_void_p), ("act", c_void_p),
-                ("acm", c_void_p), ("rew", c_void_p), ("done", c_void_p), ("end", c_void_p)]
+    _fields_ = [("obs", c_void_p), ("obs_idx", c_void_p), ("rec", c_void_p), ("rec_words", c_int),
+                ("rec_acm", c_int), ("rec_act", c_int)]
 
 
 P = ctypes.POINTER

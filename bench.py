@@ -836,9 +836,10 @@ def main():
         "step_tflops": round(flop_step * args.steps / elapsed / 1e12, 3),
         "losses": {k: round(v, 5) for k, v in losses.items()},
     }
+    chk = torch.stack([p.double().sum() for p in ag.params.values()] +
+                      [p.double().abs().sum() for p in ag.params.values()])
+    result["param_checksum"] = hashlib.sha1(chk.cpu().numpy().tobytes()).hexdigest()[:16]
     if world > 1:  # data-parallel replicas must stay bit-identical (same averaged grads, same Adam)
-        chk = torch.stack([p.double().sum() for p in ag.params.values()] +
-                          [p.double().abs().sum() for p in ag.params.values()])
         allc = [torch.empty_like(chk) for _ in range(world)]
         dist.all_gather(allc, chk)
         result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))

@@ -479,7 +479,14 @@ __device__ __forceinline__ void dense16_impl(const float4* __restrict__ Wf, int 
 }
 
 // 256-input layer from the LDS image, bf16 MFMA: all NBO output blocks accumulate at once;
-// input block ib's fragments (2 per output block) are double-buffered one block ahead.
+// input block ib+1's fragments (2 per output block, 128 VGPRs for both buffers) are loaded
+// while block ib's MFMAs issue, and block ib+1's LDS image reads follow block ib's MFMAs.
+// A finer ring (4-fragment chunks, 4 / 6 / 8 deep: 12 / 20 / 28 fragments in flight instead
+// of 16) measured slower: Ant bf16 critic phase 1.668 ms -> 1.752 / 1.721 / 1.731 ms
+// (profiles/r05/ab_bf16_ring.txt); a third whole block spills.
+// Output-block chains (all 8 input blocks converted to bf16 registers once, one 16-MFMA chain per
+// output block with the previous block's epilogue under it, as dense16_impl) measured slower too:
+// 1.686 -> 1.770 ms, bit-identical results.
 template <int NBO, bool BIAS, typename Epi>
 __device__ __forceinline__ void dense16_lds_impl(const float4* __restrict__ Wf, const float* img, const float* biasL,
                                                  Epi&& epi) {
@@ -495,11 +502,11 @@ __device__ __forceinline__ void dense16_lds_impl(const float4* __restrict__ Wf, 
   });
   float4 fr[2][2 * NBO];
   static_for<0, 2 * NBO>([&](auto J) { fr[0][J] = wfrag(wr, l16, (int)J * 1024); });
+  f32x16 x;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = l[ru(r) * 32];
   static_for<0, 8>([&](auto IB) {
     constexpr int ib = IB;
-    f32x16 x;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) x[r] = l[(32 * ib + ru(r)) * 32];
     const bf16x8 b0 = to_bf16x8<0>(x), b1 = to_bf16x8<1>(x);
     if constexpr (ib + 1 < 8) {
       static_for<0, 2 * NBO>([&](auto J) {
@@ -512,6 +519,10 @@ __device__ __forceinline__ void dense16_lds_impl(const float4* __restrict__ Wf, 
       acc[ob] = mfma16(frag16(fr[ib & 1][2 * ob]), b0, acc[ob]);
       acc[ob] = mfma16(frag16(fr[ib & 1][2 * ob + 1]), b1, acc[ob]);
     });
+    if constexpr (ib + 1 < 8) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[r] = l[(32 * (ib + 1) + ru(r)) * 32];
+    }
   });
   static_for<0, NBO>([&](auto O) { epi(IC<(int)O>{}, acc[O]); });
 }

@@ -114,8 +114,9 @@ class DDPG_AcM(OffPolicyLoop):
         call("sppDdpgAcmUpdate", self._h, ctypes.byref(b), ptr(self._losses), stream_handle())
         self._keep = tens
 
-    def update_from_replay_dp(self, idx, allreduce=None):
-        """Device-sampled step split at its exchange points (allreduce averages a flat bucket)."""
+    def update_from_replay_dp(self, idx, allreduce=None, beside=None):
+        """Device-sampled step split at its exchange points (allreduce averages a flat bucket); beside()
+        enqueues independent work under the actor bucket's exchange."""
         st = stream_handle()
         self._stage(idx)
         call("sppDdpgAcmCriticGrads", self._h, None, ptr(self._losses), st)
@@ -123,12 +124,11 @@ class DDPG_AcM(OffPolicyLoop):
             allreduce(self.bucket_critic)
         call("sppDdpgAcmCriticApply", self._h, st)
         call("sppDdpgAcmActorGrads", self._h, ptr(self._losses), st)
-        if allreduce is not None:
-            allreduce(self.bucket_actor)
+        self._exchange(allreduce, self.bucket_actor, beside)
         call("sppDdpgAcmActorApply", self._h, st)
 
-    def _fused_update(self, idx, counter, allreduce=None):
-        self.update_from_replay_dp(idx, allreduce)
+    def _fused_update(self, idx, counter, allreduce=None, beside=None):
+        self.update_from_replay_dp(idx, allreduce, beside)
 
     @property
     def loss(self):

@@ -184,9 +184,10 @@ class SAC_AcM(OffPolicyLoop):
         self._stage(idx)
         call("sppSacAcmUpdateStaged", self._h, seed, counter, ptr(self._losses), stream_handle())
 
-    def update_from_replay_dp(self, idx, seed, counter, allreduce=None):
+    def update_from_replay_dp(self, idx, seed, counter, allreduce=None, beside=None):
         """The same grad step split at its exchange points: allreduce(bucket) averages a
-        flat gradient bucket across data-parallel ranks (RCCL) between grads and apply."""
+        flat gradient bucket across data-parallel ranks (RCCL) between grads and apply.  beside()
+        enqueues independent work (the ACM step's gradients) under the actor bucket's exchange."""
         st = stream_handle()
         self._stage(idx)
         call("sppSacAcmDrawEps", self._h, seed, counter, st)
@@ -195,12 +196,11 @@ class SAC_AcM(OffPolicyLoop):
             allreduce(self.bucket_critic)
         call("sppSacAcmCriticApply", self._h, st)
         call("sppSacAcmActorGrads", self._h, None, ptr(self._losses), st)
-        if allreduce is not None:
-            allreduce(self.bucket_actor)
+        self._exchange(allreduce, self.bucket_actor, beside)
         call("sppSacAcmActorApply", self._h, ptr(self._losses), st)
 
-    def _fused_update(self, idx, counter, allreduce=None):
-        self.update_from_replay_dp(idx, self._key_update, counter, allreduce)
+    def _fused_update(self, idx, counter, allreduce=None, beside=None):
+        self.update_from_replay_dp(idx, self._key_update, counter, allreduce, beside)
 
     def acm_update_from_replay(self, idx, x, y, loss, allreduce=None):
         """update_acm_batches body (acm.py:356-372) for one device-sampled batch."""

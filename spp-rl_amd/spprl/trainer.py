@@ -32,6 +32,7 @@ buffers and H2D/D2H copies on a side stream).  Everything device-side runs in
 libspprl.so; this module only sequences calls.
 """
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -299,7 +300,7 @@ class HostSynthEnv(HostVecEnv):
 
 class OffPolicyLoop:
     """Trainer mixin of SAC_AcM / DDPG_AcM.  The host class provides ``act``,
-    ``update``, ``replay_buffer``, ``bucket_acm``, ``_h`` and ``_fused_update(idx, ctr, allreduce)``."""
+    ``update``, ``replay_buffer``, ``bucket_acm``, ``_h`` and ``_fused_update(idx, ctr, allreduce, beside)``."""
 
     def _init_loop(self, iterations=config.ITERATIONS, batch_size=config.BATCH_SIZE, stats_freq=config.STATS_FREQ,
                    test_episodes=None, return_done=None, max_frames=None, random_frames=config.RANDOM_FRAMES,
@@ -563,11 +564,24 @@ class OffPolicyLoop:
         rb = self.replay_buffer
         n = len(rb)
         B, BA = self.fused_batch_sizes()
+        acm_batch = self.iteration > 0 and self.acm_epochs > 0 and bool(self.acm_update_batches)
         if n > self.update_batch_size:
             idx = torch.empty(B, dtype=torch.int64, device=self.device)
-            call("sppRandIndex", ptr(idx), B, n, self._key_index, self._next(), stream_handle())
-            self._fused_update(idx, self._ctr, self.allreduce)
+            ctr = self._next()
+            call("sppRandIndex", ptr(idx), B, n, self._key_index, ctr, stream_handle())
+            beside = None
+            if acm_batch and self._exchange_overlap():
+                # the ACM step's gather and gradients (they read only the ACM and the replay, which the actor
+                # update leaves alone) run while the actor bucket is exchanged; its indices are the same draw
+                # (the next counter) as in the serial order below
+                ia = self._rand_idx(BA, n)
+                beside = lambda: self._acm_grads_from_idx(ia)  # noqa: E731
+            self._fused_update(idx, ctr, self.allreduce, beside)  # (eps counter: the index draw's, as serial)
             self._keep_idx = idx
+            if beside is not None:
+                self._acm_exchange_apply()
+                self._acm_loss_acc.copy_(self._acm_loss)
+                return
         if self.iteration > 0 and self.acm_epochs > 0:
             if self.acm_update_batches:
                 self._acm_step_from_idx(self._rand_idx(BA, n))
@@ -602,16 +616,50 @@ class OffPolicyLoop:
     # ---------------------------------------------------------- ACM regression
     def _acm_step_from_idx(self, idx):
         """acm_cat + batch_update (acm.py:246-264) on gathered replay rows."""
+        self._acm_grads_from_idx(idx)
+        self._acm_exchange_apply()
+
+    def _acm_grads_from_idx(self, idx):
         B = idx.numel()
         st = stream_handle()
         x = torch.empty(B, 2 * self.ob_dim, device=self.device)
         y = torch.empty(B, self.ac_dim, device=self.device)
         call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), B, ptr(x), ptr(y), st)
         call("sppAcmRegressGrads", self._h, ptr(x), ptr(y), B, ptr(self._acm_loss), st)
+        self._keep_acm_xy = (idx, x, y)
+
+    def _acm_exchange_apply(self):
         if self.allreduce is not None:
             self.allreduce(self.bucket_acm)
-        call("sppAcmRegressApply", self._h, st)
-        self._keep_acm_xy = (idx, x, y)
+        call("sppAcmRegressApply", self._h, stream_handle())
+
+    # ---------------------------------------------------------- exchange overlap (SURVEY §8e)
+    def _exchange_overlap(self):
+        """Data-parallel bucket exchanges overlap independent compute (SPP_DP_OVERLAP=0: serial order)."""
+        return (self.allreduce is not None and torch.device(self.device).type == "cuda"
+                and os.environ.get("SPP_DP_OVERLAP", "1") != "0")
+
+    def _exchange(self, allreduce, bucket, beside=None):
+        """allreduce(bucket), averaged in place.  With ``beside`` the exchange is enqueued on the agent's
+        exchange stream (after everything already on the current stream) while ``beside()`` enqueues work that
+        neither reads nor writes the bucket on the current stream; the current stream then waits for the
+        exchange.  The same operations on the same data as the serial order, so the results are identical."""
+        if beside is None:
+            if allreduce is not None:
+                allreduce(bucket)
+            return
+        if allreduce is None:
+            beside()
+            return
+        main = torch.cuda.current_stream(self.device)
+        side = getattr(self, "_xstream", None)
+        if side is None:
+            side = self._xstream = torch.cuda.Stream(device=self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            allreduce(bucket)
+        beside()
+        main.wait_stream(side)
 
     def _acm_sgd_ok(self, bs):
         """The persistent one-launch SGD kernel (sppAcmSgd) covers the AcM of these dims, one rank, and

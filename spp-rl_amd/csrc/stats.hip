@@ -52,14 +52,17 @@ __host__ __device__ inline int st_list_cap(int ob) {
 // for the keys it owns.  Query q starts from the known bits qpre[q] / qmask[q] (the masks are
 // whole-bit prefixes; queries may share a prefix, and then share a histogram).  On return
 // qpre[q] is the key of rank qrank[q] (in the set restricted to the starting prefix).
-// Needs blockDim.x >= 64 * NQ; qpre / qmask / qrank / hist in LDS.
+// Needs blockDim.x >= 64 * NQ; qpre / qmask / qrank / hist in LDS.  At most MAXP digit passes are
+// made; returns true if a query still has unknown digits then (the state is resumable: a later call
+// over the keys that match the queries' prefixes continues it).
 // Histograms hold kStCopies copies of every bin (lane & 7 picks the copy): the keys of a digit
 // pass usually fall into a handful of bins, and same-address LDS atomics of one instruction
 // serialise, so the copies cut that serialisation 8-fold.  hist: [NQ][256][kStCopies].
 constexpr int kStCopies = 8;
-template <int NQ, class Visit>
-__device__ void st_radix_select(uint32_t* qpre, uint32_t* qmask, uint32_t* qrank, Visit visit, uint32_t* hist) {
+template <int NQ, int MAXP = 4, class Visit>
+__device__ bool st_radix_select(uint32_t* qpre, uint32_t* qmask, uint32_t* qrank, Visit visit, uint32_t* hist) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  [[maybe_unused]] int passes = 0;
   for (int shift = 24; shift >= 0; shift -= 8) {
     const uint32_t dm = 0xffu << shift;
     uint32_t pre[NQ], msk[NQ];
@@ -77,6 +80,10 @@ __device__ void st_radix_select(uint32_t* qpre, uint32_t* qmask, uint32_t* qrank
         if (rep[q] == q && pre[p] == pre[q] && msk[p] == msk[q]) rep[q] = rep[p];
     }
     if (!any) continue;  // uniform: every thread read the same state
+    if constexpr (MAXP < 4) {
+      if (passes == MAXP) return true;
+      ++passes;
+    }
     for (int i = tid; i < NQ * 256 * kStCopies; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     uint32_t* hl = hist + (lane & (kStCopies - 1));
@@ -123,6 +130,7 @@ __device__ void st_radix_select(uint32_t* qpre, uint32_t* qmask, uint32_t* qrank
     }
     __syncthreads();
   }
+  return false;
 }
 
 // ---------------------------------------------------------------- sample bracket
@@ -590,23 +598,47 @@ __global__ __launch_bounds__(kStSelThreads) void k_st_select(StSelArgs a) {
                          for (uint32_t i = tid; i < ncd; i += T) fn(cand[i]);
                        },
                        hist);
-  } else if (nq > 0 && md == 2) {  // too many candidates for LDS: visit the global lists
+  } else if (nq > 0 && md == 2) {
+    // too many candidates for LDS: digit passes over the global lists until the keys that still match a
+    // query's prefix fit in LDS (usually one pass), then those are gathered and the select ends in LDS
     const uint32_t* wgl = a.wgl;
     const uint32_t* ovf = a.ovf + (int64_t)ct * kStOvfCap;
-    st_radix_select<2>(qpre, qmask, qrank,
-                       [&](auto&& fn) {
-                         const uint32_t* L = wgl + ((int64_t)b * ob * 2 + ct) * cap;
-                         for (uint32_t i = 0; i < nb; i += 4) {
-                           uint32_t k4[4];
+    auto visit_global = [&](auto&& fn) {
+      const uint32_t* L = wgl + ((int64_t)b * ob * 2 + ct) * cap;
+      for (uint32_t i = 0; i < nb; i += 4) {
+        uint32_t k4[4];
 #pragma unroll
-                           for (int u = 0; u < 4; ++u) k4[u] = i + u < nb ? L[i + u] : 0u;
+        for (int u = 0; u < 4; ++u) k4[u] = i + u < nb ? L[i + u] : 0u;
 #pragma unroll
-                           for (int u = 0; u < 4; ++u)
-                             if (i + u < nb) fn(k4[u]);
-                         }
-                         for (uint32_t i = tid; i < novf; i += T) fn(ovf[i]);
-                       },
-                       hist);
+        for (int u = 0; u < 4; ++u)
+          if (i + u < nb) fn(k4[u]);
+      }
+      for (uint32_t i = tid; i < novf; i += T) fn(ovf[i]);
+    };
+    __shared__ uint32_t s_nc;
+    while (st_radix_select<2, 1>(qpre, qmask, qrank, visit_global, hist)) {
+      if (tid == 0) s_nc = 0;
+      __syncthreads();
+      const int nqa = nq;
+      const uint32_t p0 = qpre[0], k0m = qmask[0], p1 = qpre[1], k1m = qmask[1];
+      visit_global([&](uint32_t k) {
+        if ((k & k0m) == p0 || (nqa > 1 && (k & k1m) == p1)) {
+          const uint32_t slot = atomicAdd(&s_nc, 1u);
+          if (slot < (uint32_t)kStSelKeys) cand[slot] = k;
+        }
+      });
+      __syncthreads();
+      const uint32_t nc = s_nc;
+      if (nc <= (uint32_t)kStSelKeys) {
+        st_radix_select<2>(qpre, qmask, qrank,
+                           [&](auto&& fn) {
+                             for (uint32_t i = tid; i < nc; i += T) fn(cand[i]);
+                           },
+                           hist);
+        break;
+      }
+      __syncthreads();  // every thread has read s_nc before the next round resets it
+    }
   } else if (nq > 0) {
     const ReplayDev r = a.r;
     st_radix_select<2>(qpre, qmask, qrank,

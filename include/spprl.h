@@ -471,8 +471,9 @@ sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
  * memory, read once the stream has passed this point); 0 is written when no multi-workgroup launch ran. */
 sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle h, int* timed_out_pinned, void* stream);
 /* Test hook (no reference counterpart): polls before an arrival wait of any persistent SGD launch
- * (sppAcmSgd*, sppOnpActorEpoch, sppOnpCriticSteps) times out; 0 restores the default (~0.2 s).  A tiny limit
- * makes the first workgroup to arrive time out, which is how the tests force the timeout path. */
+ * (sppAcmSgd*, sppOnpActorEpoch, sppOnpCriticSteps) times out; 0 restores the default (~0.2 s).  A negative
+ * value makes every wait give up at once (a co-residency miss, deterministically): how the tests force the
+ * timeout path. */
 sppStatus sppSetSgdSpinLimit(int polls);
 /* A2C.update_critic's inner loop (rltoolkit/algorithms/a2c/a2c.py:186-225): nsteps sequential full-batch
  * steps of 0.5 * mean((q - V(x))^2) + Adam at critic_lr on the same N rows (x [N][ob] normalised obs, q [N]

@@ -2618,8 +2618,7 @@ sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle o, int* timed_out_pinned, void
 }
 
 sppStatus sppSetSgdSpinLimit(int polls) {
-  SPP_REQUIRE(polls >= 0, SPP_E_INVALID_ARG, "spin limit: negative");
-  g_sgd_spin = polls;
+  g_sgd_spin = polls;  // < 0: every wait gives up at once (sgd_arrive_wait_wt)
   return SPP_OK;
 }
 

@@ -8,8 +8,8 @@
 namespace spp {
 
 // Arrival barrier of the multi-workgroup SGD.  The counter address is kept in a VGPR so the add and the
-// polls are vector-memory operations.  Bounded: after `spin` polls (0: kSgdSpins, ~0.2 s) a wait times out,
-// sets *err and every later wait of the launch returns at once.
+// polls are vector-memory operations.  Bounded: after `spin` polls (0: kSgdSpins, ~0.2 s; < 0: none, the test
+// hook's forced timeout) a wait times out, sets *err and every later wait of the launch returns at once.
 // The per-step gradient hand-over between the workgroups is write-through: every slab word is stored
 // sc1 (aux 16) and every load of slab words is an sc1 load, so the arrival needs no agent-scope release
 // (its L2 write-back cost ~6.5 us per step with a freshly written 18 KB slab) and no acquire
@@ -44,14 +44,19 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
     asm volatile("" : "+v"(off));
     int* c = ctr + off;
     __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int limit = spin > 0 ? spin : kSgdSpins;
-    int spins = 0;
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > limit) {
-        *s_dead = 1;
-        err[off] = 1;
-        break;
+    if (spin < 0) {  // test hook: every wait gives up at once (a co-residency miss, deterministically)
+      *s_dead = 1;
+      err[off] = 1;
+    } else {
+      const int limit = spin > 0 ? spin : kSgdSpins;
+      int spins = 0;
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > limit) {
+          *s_dead = 1;
+          err[off] = 1;
+          break;
+        }
       }
     }
   }

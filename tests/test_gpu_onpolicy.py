@@ -356,7 +356,8 @@ def test_persistent_launch_timeouts_raise_in_the_product_path():
     """A multi-workgroup persistent launch whose arrival wait times out leaves invalid parameters: the product
     path (OnPolicyNets.update_critic / update_actor as PPO_AcM.update runs them, and the AcM epochs of
     update_acm) must raise SppError, not continue.  The timeout is forced with the spin-limit test hook
-    (sppSetSgdSpinLimit(1): the first workgroup to arrive at a barrier gives up)."""
+    (sppSetSgdSpinLimit(-1): every arrival wait gives up at once, as a co-residency miss would; a small positive
+    limit is timing-dependent: the workgroups of a short epoch can all arrive before anyone's first poll)."""
     import spprl
     from spprl import _lib
     from spprl.onpolicy import OnPolicyNets
@@ -377,7 +378,7 @@ def test_persistent_launch_timeouts_raise_in_the_product_path():
     n0.update_critic(obs, nobs, rew, done)
     n0.update_actor(adv, obs, act, lp, nobs)
     try:
-        _lib.call("sppSetSgdSpinLimit", 1)
+        _lib.call("sppSetSgdSpinLimit", -1)
         n1 = OnPolicyNets(OB, AOUT, max_batch=N, critic_num_target_updates=1, num_critic_updates_per_target=3,
                           device=DEV, seed=1)
         with pytest.raises(_lib.SppError, match="timed out"):

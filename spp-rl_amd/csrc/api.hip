@@ -783,7 +783,7 @@ struct DwSet {
   int B = -1;
   int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
   int nlds[2] = {0, 0};  // leading items of a phase that run as k_dw_big (256 x 256 fp32 jobs)
-  int64_t max_elems[2] = {1, 1};  // largest [N*K | N] image per phase (reduce grid)
+  int64_t max_elems[2] = {1, 1};  // reduce lanes per phase: largest [N*K | N] image x its dw_red_group
   bool bf16 = false;              // bf16 MFMA job set (k_dw<true>)
   void release() { slab.release(); jobs.release(); items.release(); }
 };
@@ -1156,8 +1156,10 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
         }
       }
     D.max_elems[ph] = 1;
-    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j)
-      D.max_elems[ph] = std::max<int64_t>(D.max_elems[ph], (int64_t)jobs[j].N * (jobs[j].K0 + jobs[j].K1) + jobs[j].N);
+    for (int j = D.j0[ph]; j < D.j0[ph] + D.nj[ph]; ++j) {
+      const int64_t el = (int64_t)jobs[j].N * (jobs[j].K0 + jobs[j].K1) + jobs[j].N;
+      D.max_elems[ph] = std::max<int64_t>(D.max_elems[ph], el * dw_red_group(jobs[j].nsplit * jobs[j].wsplit, el));
+    }
     D.ioff[ph] = (int)items.size();
     D.nitems[ph] = (int)jj.size();
     items.insert(items.end(), jj.begin(), jj.end());

@@ -427,19 +427,36 @@ __global__ void k_dw_reduce(const DwJob* __restrict__ jobs) {
   const int N = J.N, K = J.K0 + J.K1;
   const int64_t nw = (int64_t)N * K;
   const int64_t total = nw + (J.db ? N : 0);
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
+  const int G = dw_red_group(nslab, nw + N);  // lanes per element (as the host sized the grid; a power of 2 dividing 64)
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = gid / G;
+  const int g = (int)(gid % G);
+  if (e >= total) return;  // whole groups: e is the same for the G lanes of a group
   const float* p = J.slab + e;
   float s = 0.f;
-  int sp = 0;
-  for (; sp + 16 <= nslab; sp += 16) {
-    float v[16];
+  if (G == 1) {
+    int sp = 0;
+    for (; sp + 16 <= nslab; sp += 16) {
+      float v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = p[(int64_t)(sp + u) * J.slab_stride];
+      for (int u = 0; u < 16; ++u) v[u] = p[(int64_t)(sp + u) * J.slab_stride];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) s += v[u];
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; sp < nslab; ++sp) s += p[(int64_t)sp * J.slab_stride];
+  } else {
+    // lane g sums slabs g, g + G, ... (16 loads per round trip), then a fixed butterfly over the group; lane 0's
+    // operand order is the same on every run, and only lane 0 writes
+    for (int sp = g; sp < nslab; sp += 16 * G) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = sp + u * G < nslab ? p[(int64_t)(sp + u * G) * J.slab_stride] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (g != 0) return;
   }
-  for (; sp < nslab; ++sp) s += p[(int64_t)sp * J.slab_stride];
   if (e < nw) {
     const int n = (int)(e / K), k = (int)(e % K);
     if (n < J.nrow2) J.dW[(int64_t)n * K + k] = s;

@@ -30,6 +30,12 @@ struct DwJob {
 // bf16 MFMA jobs (DwJob::bf16).
 void launch_dw_kernels(const DwJob* jobs, const int* item_job, const int* item_split, int nitems, int nlds,
                        int njobs, int64_t max_elems, bool bf16, hipStream_t st);
+// k_dw_reduce: lanes that sum one output element of a job with nslab partial slabs of `elems` elements
+// (fixed-order reduce).  One lane per element (consecutive lanes read consecutive elements of a slab:
+// coalesced) for the split-K GEMM jobs; a group of 16 lanes per element for the few-element, many-slab jobs
+// (the fused fc3 jobs' 257 x one-partial-per-wave), whose one-lane serial sums were the launch's critical
+// path; max_elems counts lanes
+inline __host__ __device__ int dw_red_group(int nslab, int64_t elems) { return nslab >= 64 && elems <= 4096 ? 16 : 1; }
 
 // fragment-image pack job: logical L[n][k] of a source matrix S (row stride ld)
 //   L[n][k] = trans ? S[k][coff + n] : S[n][coff + k]; source rows >= split come from W2

@@ -1962,7 +1962,8 @@ static int mlp_sgd_max_wg(int num_cu) {
 // up to 128 rows per workgroup, at least 2 workgroups (its LDS has no room for the single-workgroup form's
 // canonical gradient staging).  Measured round 5 (1049-row PPO ACM steps, profiles/r05/ab_acm_wv.txt): 8 waves
 // on 9 workgroups 17.3 us per step against 13.4 us for 4 waves on 17: the MFMA work per CU doubles while the
-// second wave per SIMD hides less than that, so the default stays 4 (A/B: -DSPP_ACM_WV=8).  bs <= 64 always runs
+// second wave per SIMD hides less than that, so the default stays 4 (A/B: -DSPP_ACM_WV=8; 2 waves on 33
+// workgroups measured 17.0 us too).  bs <= 64 always runs
 // the single-workgroup 4-wave form.
 #ifndef SPP_ACM_WV
 #define SPP_ACM_WV 4

@@ -72,7 +72,7 @@ struct MlpSgdArgs {
 
 template <int IN, int H2, int OUT, int HEAD, int WV = 4>
 struct MlCfg {
-  static_assert(WV == 4 || WV == 8, "4 or 8 waves per workgroup");
+  static_assert(WV == 2 || WV == 4 || WV == 8, "2, 4 or 8 waves per workgroup");
   static constexpr int R = 16 * WV;                 // rows per workgroup and step (16 per wave)
   static constexpr int TH = 64 * WV;                // threads
   static constexpr int RS = R + 4;                  // image row stride (result-layout stores: 64 distinct banks)

@@ -157,6 +157,7 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
     if not force and up_to_date():
         if verbose:
             print("libspprl.so up to date")
+        build_c_host(verbose)
         return OUT
     os.makedirs(OBJ, exist_ok=True)
     t0 = time.time()  # the library is stamped with this time: a source edited during the build stays newer
@@ -176,7 +177,27 @@ def build(force=False, verbose=True, prof=False, hopper_only=False, jobs=None, n
     os.utime(OUT, (t0, t0))
     if verbose:
         print("built %s in %.0fs" % (OUT, time.time() - t0))
+    build_c_host(verbose)
     return OUT
+
+
+C_HOST = os.path.join(REPO, "examples", "c_host", "sac_acm_step")
+INC = os.path.join(REPO, "include")
+
+
+def build_c_host(verbose=True):
+    """The plain-C host of the C-ABI (examples/c_host/sac_acm_step.c: gcc, include/spprl.h, libspprl.so and the
+    HIP runtime only), in-tree next to its source; tests/test_gpu_c_host.py runs it on the GPU box."""
+    src = C_HOST + ".c"
+    if not os.path.exists(src) or (os.path.exists(C_HOST) and os.path.getmtime(C_HOST) >= max(
+            os.path.getmtime(src), os.path.getmtime(os.path.join(INC, "spprl.h")))):
+        return C_HOST
+    subprocess.check_call(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I" + INC, src,
+                           "-L" + os.path.join(HERE, "spprl"), "-lspprl", "-L/opt/rocm/lib", "-lamdhip64",
+                           "-Wl,-rpath,$ORIGIN/../../spp-rl_amd/spprl", "-Wl,-rpath,/opt/rocm/lib", "-o", C_HOST])
+    if verbose:
+        print("built %s" % C_HOST)
+    return C_HOST
 
 
 if __name__ == "__main__":

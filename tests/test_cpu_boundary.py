@@ -116,3 +116,17 @@ def test_unknown_reference_kwargs_raise_and_no_effect_ones_are_listed():
     assert {"use_gpu", "log_dir", "verbose", "render", "acm_val_buffer_size"} <= set(config.NO_EFFECT_KWARGS)
     assert "obs_norm_alpha" in config.ON_POLICY_NO_EFFECT_KWARGS
     config.check_kwargs("x", {"use_gpu": True, "tensorboard_comment": "c"})
+
+
+def test_c_host_example_compiles_against_the_header():
+    """examples/c_host/sac_acm_step.c is plain C11 against include/spprl.h (no C++, no torch types): a C host
+    can bind the boundary directly (its GPU run: tests/test_gpu_c_host.py)."""
+    import shutil
+
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not on PATH")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([gcc, "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-I", os.path.join(repo, "include"),
+                        os.path.join(repo, "examples", "c_host", "sac_acm_step.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

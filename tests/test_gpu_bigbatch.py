@@ -102,6 +102,26 @@ def check_sac(ag, o, ol, grad_tol, loss_tol, params_check=True, params0=None):
     ("Ant-v2", 111, 8, 4096, "bf16_acmc0"),
 ])
 def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
+    _sac_update_vs_oracle(env_name, ob, ac, B, bf16)
+
+
+# ragged and minimal batches: Bp = B rounded up to 32 with dead samples in the last tile (B = 1: one live sample
+# in the whole launch), a tile count below the grid, one live sample past a tile boundary
+@pytest.mark.parametrize("env_name,ob,ac,B,bf16", [
+    ("Hopper-v2", 11, 3, 1, False),
+    ("Hopper-v2", 11, 3, 31, False),
+    ("Hopper-v2", 11, 3, 33, False),
+    ("Hopper-v2", 11, 3, 1001, False),
+    ("Ant-v2", 111, 8, 33, True),
+    ("Ant-v2", 111, 8, 1, "acmc0"),
+])
+def test_sac_acm_update_ragged_batches_match_oracle(env_name, ob, ac, B, bf16):
+    # Adam's first step moves a parameter by ~lr whatever its gradient's size, so at a few samples the many
+    # near-zero gradients make the post-step comparison a sign test; gradients and losses are compared instead
+    _sac_update_vs_oracle(env_name, ob, ac, B, bf16, params_check=B >= 1000)
+
+
+def _sac_update_vs_oracle(env_name, ob, ac, B, bf16, params_check=True):
     rng = np.random.RandomState(B % 1000 + ob)
     acmc = bf16 not in ("acmc0", "bf16_acmc0")
     bf16 = bf16 in (True, "bf16_acmc0")
@@ -120,10 +140,10 @@ def test_sac_acm_update_large_batch_matches_oracle(env_name, ob, ac, B, bf16):
     if bf16:
         check_sac(ag, o, ol, grad_tol=6e-2, loss_tol=3e-2, params_check=False)
     else:
-        check_sac(ag, o, ol, grad_tol=2e-4, loss_tol=1e-4)
+        check_sac(ag, o, ol, grad_tol=2e-4, loss_tol=1e-4, params_check=params_check)
 
 
-@pytest.mark.parametrize("B", [65536, 409600, 819200])  # 819,200 = rho * E: the ddpg_hcheetah bench batch
+@pytest.mark.parametrize("B", [1, 33, 65536, 409600, 819200])  # 819,200 = rho * E: the ddpg_hcheetah bench batch
 def test_ddpg_acm_update_large_batch_matches_oracle(B):
     ob, ac = 17, 6
     rng = np.random.RandomState(B % 977)
@@ -145,6 +165,8 @@ def test_ddpg_acm_update_large_batch_matches_oracle(B):
     for k in ("critic", "actor", "ddpg", "dist"):
         assert abs(gl[k] - ol[k]) <= 1e-4 * abs(ol[k]) + 1e-6, (k, gl[k], ol[k])
     for k in ("actor", "critic"):
+        if B < 1000:  # a few samples: post-Adam parameters are a sign test of near-zero gradients (see above)
+            break
         d = np.abs(ag.params[DDPG_NETS[k]].cpu().numpy() - o.flat(k))
         assert d.max() <= 2 * 5e-4 * 1.01 and np.mean(d > 1e-5) < 2e-3, (k, d.max())
 

@@ -49,8 +49,8 @@ def test_rccl_one_rank_exchange_matches_single_gpu(config):
 @pytest.mark.parametrize("config", ["sac_hopper", "ddpg_hcheetah"])
 def test_rccl_exchange_overlap_changes_no_result(config):
     """The actor bucket's all-reduce runs on the exchange stream beside the ACM step's gradients
-    (spprl.trainer._exchange); with SPP_DP_OVERLAP=0 the same operations run in the serial order.  The
-    parameters after the run (a checksum of per-tensor sums) and the losses must be identical."""
+    (spprl.trainer._exchange, SPP_DP_OVERLAP=1); with SPP_DP_OVERLAP=0 (the default) the same operations run in the
+    serial order.  The parameters after the run (a checksum of per-tensor sums) and the losses must be identical."""
     env = {"SPP_DP_FORCE": "1", "SPP_DIST_BACKEND": "nccl"}
     serial = _bench(config, dict(env, SPP_DP_OVERLAP="0"), launcher=True)
     over = _bench(config, dict(env, SPP_DP_OVERLAP="1"), launcher=True)

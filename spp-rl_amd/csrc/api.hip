@@ -782,7 +782,7 @@ struct DwSet {
   DevArray<int> items;
   int B = -1;
   int j0[2] = {0, 0}, nj[2] = {0, 0}, ioff[2] = {0, 0}, nitems[2] = {0, 0};
-  int nlds[2] = {0, 0};  // leading items of a phase that run as k_dw_big (256 x 256 fp32 jobs)
+  int nlds[2] = {0, 0};  // leading items of a phase that run as k_dw_big / k_dw_big16 (256 x 256 jobs)
   int64_t max_elems[2] = {1, 1};  // reduce lanes per phase: largest [N*K | N] image x its dw_red_group
   bool bf16 = false;              // bf16 MFMA job set (k_dw<true>)
   void release() { slab.release(); jobs.release(); items.release(); }
@@ -1080,6 +1080,10 @@ static void launch_pack(sppAgent* a, int off, int n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(k_pack_matrix, dim3(64, n), dim3(256), 0, st, (const PackJob*)(a->d_pj.ptr + off));
 }
 
+// bf16 sets' 256 x 256 bf16-operand weight gradients on the LDS-staged k_dw_big16 (0: k_dw<true>, the A/B)
+#ifndef SPP_DW_BIG16
+#define SPP_DW_BIG16 1
+#endif
 // Split assignment, slab arena, item table and upload of a job set.
 static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp, int B, int num_cu) {
   // Sample splits: the large (>= 128x128 padded) GEMMs of a phase share ~one
@@ -1090,7 +1094,11 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
   };
   // 256 x 256 fp32 jobs run as their own launch (k_dw_big); the other large jobs share k_dw's launch
   // (small batches -- vanilla SAC's B = 100, PPO minibatches -- keep one launch: k_dw's register tiles)
-  auto lds_big = [Bp](const DwJob& j) { return Bp >= 8192 && !j.bf16 && j.N == 256 && j.K0 == 256 && j.K1 == 0; };
+  // (bf16 sets: the 256 x 256 jobs whose A and X rows are both bf16 run as k_dw_big16, in 64-sample steps)
+  auto lds_big = [Bp](const DwJob& j) {
+    return Bp >= 8192 && j.N == 256 && j.K0 == 256 && j.K1 == 0 &&
+           (!j.bf16 || (SPP_DW_BIG16 && j.a_bf && j.x_bf && Bp % 64 == 0));
+  };
   auto assign_splits = [&](int first, int count) {
     double big[2] = {0.0, 0.0};  // MACs of the large jobs per launch
     for (int i = first; i < first + count; ++i)
@@ -1111,7 +1119,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
       // 32-sample unit instead of a serial chain over the whole batch
       if (!is_big(j)) ns = std::max(ns, std::min(cdiv(Bp, 32 * j.wsplit), 4));
       ns = std::max(1, std::min(ns, std::max(1, Bp / 32)));
-      j.split_len = (int)round_up(cdiv(Bp, ns), 32 * j.wsplit);
+      j.split_len = (int)round_up(cdiv(Bp, ns), lds_big(j) && j.bf16 ? 64 : 32 * j.wsplit);
       j.nsplit = cdiv(Bp, j.split_len);
     }
   };

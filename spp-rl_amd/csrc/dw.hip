@@ -243,6 +243,82 @@ __device__ __forceinline__ void dw_big_lds(const DwJob& J, int b_begin, int nste
   }
 }
 
+// 256 x 256 jobs with bf16 A and X rows (the bf16 sets' hidden-layer weight gradients): the same LDS-DMA staging
+// with a 64-sample step, which is again one 128-B line per row (8 slots of 8 bf16, the same swizzle): the rows are
+// addressed as 4-byte words (ld = Bp / 2, the step 32 words), so the DMA issue is dw_big_lds's.  A step holds 4
+// k-steps of v_mfma_f32_32x32x16_bf16; k-step s reads one 16-B slot per row, slot 2s + h (lane half h takes
+// samples 8h..8h+7 of the k-step on both operands, as dw_tile's bf16 form), double-buffered across the k-steps.
+// Per item the k-steps run in sample order, as in k_dw<true>.  Needs b_begin and the item's range multiples of 64.
+__device__ __forceinline__ void dw_big_lds16(const DwJob& J, int b_begin, int nsteps, int nb0, int kb0, bool db,
+                                             f32x16 (&acc)[4][4], float (&bs)[4]) {
+  __shared__ __attribute__((aligned(16))) float lds[2][512 * 32];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int64_t ld = J.Bp / 2;  // words per bf16 row
+  const int pe = (lane & 7) ^ ((lane >> 4) & 3);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const float* wsel = wu < 2 ? J.A : J.X0;
+  const uint64_t wbits = (uint64_t)(size_t)wsel;
+  const uint64_t wbu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wbits) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wbits >> 32)) << 32);
+  const int64_t ldu = (int64_t)__builtin_amdgcn_readfirstlane((int)ld);
+  const int bbu = __builtin_amdgcn_readfirstlane(b_begin / 2);  // first sample's word
+  const float* wb = opaque(reinterpret_cast<const float*>((size_t)wbu) + (int64_t)(128 * (wu & 1)) * ldu + bbu);
+  const uint32_t off0 = (uint32_t)((lane >> 3) * ld + 4 * pe), off1 = off0 ^ 16u;
+  auto issue = [&](int t, int buf) {
+    const uint32_t dst = (uint32_t)(size_t)(lds_void*)&lds[buf][(128 * wu) * 32];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float* src = opaque(wb + ((int64_t)(8 * k) * ldu + 32 * t)) + ((k & 1) ? off1 : off0);
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst + 1024u * k)
+                   : "memory");
+    }
+  };
+  const int sw = (c >> 1) & 7;
+  auto rd = [&](const float* L, int s, float4 (&ra)[4], float4 (&rx)[4]) {
+    const int q = (2 * s + h) ^ sw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i] = *reinterpret_cast<const float4*>(L + (32 * (nb0 + i) + c) * 32 + 4 * q);
+      rx[i] = *reinterpret_cast<const float4*>(L + (256 + 32 * (kb0 + i) + c) * 32 + 4 * q);
+    }
+  };
+  auto mm = [&](const float4 (&ra)[4], const float4 (&rx)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (db) bs[i] += sum_bf8(ra[i]);
+      const bf16x8 av = as_bf8(ra[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(av, as_bf8(rx[j]), acc[i][j]);
+    }
+  };
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nsteps > 1) issue(1, 1);
+  float4 ra0[4], rx0[4], ra1[4], rx1[4];
+  rd(lds[0], 0, ra0, rx0);
+#pragma unroll 1
+  for (int t = 0; t < nsteps; ++t) {
+    const float* L = lds[t & 1];
+    rd(L, 1, ra1, rx1);
+    mm(ra0, rx0);
+    rd(L, 2, ra0, rx0);
+    mm(ra1, rx1);
+    rd(L, 3, ra1, rx1);
+    mm(ra0, rx0);
+    if (t + 1 < nsteps) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // my DMA for t + 1 landed, my reads of t done
+      __syncthreads();  // every wave's DMA landed and every wave is done reading buffer t & 1
+      if (t + 2 < nsteps) issue(t + 2, t & 1);
+      rd(lds[(t + 1) & 1], 0, ra0, rx0);
+    }
+    mm(ra1, rx1);
+  }
+}
+
 // Partial (or final) result of an item's (nb0, kb0) quadrant; rows >= nrow2 go to the second output
 // (dW2 / db2).
 __device__ __forceinline__ void dw_store(const DwJob& J, int split, int part, int nb0, int kb0, int ni, int nj,
@@ -413,6 +489,29 @@ __global__ __launch_bounds__(kDwThreads, 1) void k_dw_big(const DwJob* __restric
     for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
   if (nsteps > 0) dw_big_lds(J, b_begin, nsteps, nb0, kb0, db, acc, bs);
+  dw_store(J, split, 0, nb0, kb0, 4, 4, db, acc, bs);
+}
+
+// 256 x 256 bf16-operand items (host: as k_dw_big's, both operands bf16, item ranges multiples of 64 samples).
+__global__ __launch_bounds__(kDwThreads, 1) void k_dw_big16(const DwJob* __restrict__ jobs,
+                                                            const int* __restrict__ item_job,
+                                                            const int* __restrict__ item_split) {
+  const int item = blockIdx.x;
+  const DwJob J = jobs[item_job[item]];
+  const int split = item_split[item];
+  const int w = threadIdx.x >> 6;
+  const int nb0 = 4 * (w >> 1), kb0 = 4 * (w & 1);
+  const int b_begin = split * J.split_len;
+  const int b_end = min(b_begin + J.split_len, J.Bp);
+  const int nsteps = (b_end - b_begin) / 64;  // ranges are multiples of 64 samples (host: lds_big)
+  const bool db = J.db != nullptr && kb0 == 0;
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero16();
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (nsteps > 0) dw_big_lds16(J, b_begin, nsteps, nb0, kb0, db, acc, bs);
   dw_store(J, split, 0, nb0, kb0, 4, 4, db, acc, bs);
 }
 

@@ -26,8 +26,8 @@ struct DwJob {
 
 // dw.hip (own translation unit, ks_dw.hip): the split-K weight-gradient launch + fixed-order reduce
 // over nitems work items of jobs[0, njobs); item_job / item_split index the job table; the first
-// nlds items are 256 x 256 fp32 jobs (k_dw_big), the rest run in k_dw; bf16: the set's jobs are
-// bf16 MFMA jobs (DwJob::bf16).
+// nlds items are 256 x 256 jobs staged through LDS (k_dw_big; bf16 sets: k_dw_big16, bf16 A and X rows), the
+// rest run in k_dw; bf16: the set's jobs are bf16 MFMA jobs (DwJob::bf16).
 void launch_dw_kernels(const DwJob* jobs, const int* item_job, const int* item_split, int nitems, int nlds,
                        int njobs, int64_t max_elems, bool bf16, hipStream_t st);
 // k_dw_reduce: lanes that sum one output element of a job with nslab partial slabs of `elems` elements

@@ -179,6 +179,16 @@ class OnPolicyNets:
         self.last_epochs = 0
         mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
         one_launch = self._epoch_kernel_ok(mb)
+        # One-launch epochs keep the device busy across the epoch loop's one host round trip (the KL early stop):
+        # the epoch's KL goes to pinned memory by an async copy behind the launch, and the next epoch's permutation
+        # (it does not depend on the KL) is enqueued before the host waits for that copy, so its sort runs while the
+        # host wakes up instead of after the next launch.  Permutation k uses counter (_perm_ctr + 1 + k) * N, as
+        # when each epoch drew its own; the counter advances by the epochs run, so a permutation drawn ahead for an
+        # epoch the KL stop skipped is never used and the sequence is the same.
+        ahead = generator is None and one_launch
+        nxt_perm = device_randperm(N, self._perm_seed, (self._perm_ctr + 1) * N, self.device) if ahead else None
+        if ahead and getattr(self, "_kl_host", None) is None:
+            self._kl_host = torch.zeros(1).pin_memory()
         for i in range(self.max_ppo_epochs):
             if kl >= self.kl_div_threshold:
                 break
@@ -188,6 +198,8 @@ class OnPolicyNets:
             # stream every epoch)
             if generator is not None:
                 perm = torch.randperm(N, generator=generator).to(self.device)
+            elif ahead:
+                perm = nxt_perm
             else:
                 self._perm_ctr += 1
                 perm = device_randperm(N, self._perm_seed, self._perm_ctr * N, self.device)
@@ -195,6 +207,8 @@ class OnPolicyNets:
             if one_launch:  # the whole epoch in one persistent launch (the ragged last minibatch included)
                 call("sppOnpActorEpoch", self._h, ptr(obs), ptr(actions), ptr(logprobs), ptr(adv), ptr(nxt),
                      ptr(perm), N, mb, ptr(outs), stream_handle())
+                if ahead:
+                    self._kl_host.copy_(outs[-1, 1:2], non_blocking=True)
                 self._sync_flag_copy()
                 self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
             else:
@@ -206,8 +220,16 @@ class OnPolicyNets:
                     self.actor_step(o_p[s:e], a_p[s:e], l_p[s:e], d_p[s:e], n_p[s:e] if n_p is not None else None,
                                     out=outs[k])
             sums += outs.sum(0)
-            kl = float(outs[-1, 1].item())  # KL of the epoch's last minibatch (ppo.py:188)
-            self._sync_check()
+            if ahead:
+                if i + 1 < self.max_ppo_epochs:
+                    nxt_perm = device_randperm(N, self._perm_seed, (self._perm_ctr + 2 + i) * N, self.device)
+                self._sync_check()  # waits for the event behind the KL copy, not for the permutation drawn ahead
+                kl = float(self._kl_host[0])  # KL of the epoch's last minibatch (ppo.py:188)
+            else:
+                kl = float(outs[-1, 1].item())
+                self._sync_check()
+        if ahead:
+            self._perm_ctr += self.last_epochs
         # the reference divides by i + 1 after the loop: the epochs run when none stopped early, one more than
         # that when the KL check broke the loop (on_policy.py:210-216, ppo.py:190-192)
         s = sums.cpu().numpy().astype(np.float64)

@@ -827,6 +827,7 @@ static bool find_kset(int algo, int ob, int aout, int ac, bool acmc, bool bf16, 
 struct sppAgent {
   sppAgentConfig cfg{};
   int device = 0, num_cu = 256;
+  bool team_ok = true;  // SPP_SAC_TEAM=0: the one-wave phase kernels at every batch (A/B)
   KernelSet ks{};
   NetBufs net[SPP_NET_COUNT];
   int64_t nsize[SPP_NET_COUNT] = {};
@@ -1189,6 +1190,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
 // (Re)build a weight-gradient job set for batch size B.
 //   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
 static int phase_grid(sppAgent* a, int Bp);
+static int sac_grid(sppAgent* a, int Bp);
 static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int Bp = (int)round_up(B, 32);
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
@@ -1280,7 +1282,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       }
       J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
       jobs.back().fused = 1;
-      jobs.back().nsplit = phase_grid(a, Bp) * kWavesPerWG;
+      jobs.back().nsplit = sac_grid(a, Bp) * kWavesPerWG;
       jobs.back().wsplit = 1;
       fused_idx[i] = (int)jobs.size() - 1;
     }
@@ -1397,6 +1399,13 @@ static int phase_grid(sppAgent* a, int Bp) {
   const int ntiles = Bp / 32;
   return std::max(1, std::min(cdiv(ntiles, kWavesPerWG), a->num_cu));
 }
+// SAC phases: the team kernels (one workgroup per tile, sac_team.h) while the tiles fit one per CU
+static bool sac_team(sppAgent* a, int Bp) {
+  return a->ks.critic_team && a->ks.actor_team && a->team_ok && Bp / 32 <= a->num_cu;
+}
+static int sac_grid(sppAgent* a, int Bp) {
+  return sac_team(a, Bp) ? std::max(1, std::min(Bp / 32, a->num_cu)) : phase_grid(a, Bp);
+}
 
 static sppStatus check_ready(sppAgent* a) {
   SPP_REQUIRE(a->ddpg || (a->alpha_state && a->alpha_f32), SPP_E_STATE, "alpha not bound");
@@ -1433,6 +1442,10 @@ sppStatus sppAgentCreate(sppAgentHandle* out, const sppAgentConfig* cfg, int dev
   hipDeviceProp_t prop;
   SPP_CHECK_HIP(hipGetDeviceProperties(&prop, device));
   a->num_cu = prop.multiProcessorCount;
+  {
+    const char* t = getenv("SPP_SAC_TEAM");
+    a->team_ok = !(t && t[0] == '0');
+  }
   const int ob = cfg->ob, aout = cfg->aout, ac = cfg->ac;
   a->cin = ob + (cfg->acm_critic ? ac : aout);
   a->ddpg = cfg->algo == SPP_ALGO_DDPG_ACM;
@@ -1604,9 +1617,9 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
   launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size() + a->pj_targ.size() + a->pj_critic_fwd.size()),
               st);
   SacArgs p = make_args(a, B);
-  const int grid = phase_grid(a, p.Bp);
+  const int grid = sac_grid(a, p.Bp);
   tmark(a, 0, st);
-  hipLaunchKernelGGL(a->ks.critic, dim3(grid), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(sac_team(a, p.Bp) ? a->ks.critic_team : a->ks.critic, dim3(grid), dim3(256), 0, st, p);
   tmark(a, 0, st);
   SPP_CHECK_HIP(hipGetLastError());
   tmark(a, 2, st);
@@ -1650,9 +1663,9 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   launch_pack(a, a->o_cfwd, (int)a->pj_critic_fwd.size(), st);
   SacArgs p = make_args(a, B);
   AcmScratch z{a->Z1, a->Z2, a->T3, a->GAD, a->MASK};
-  const int grid = phase_grid(a, p.Bp);
+  const int grid = sac_grid(a, p.Bp);
   tmark(a, 1, st);
-  hipLaunchKernelGGL(a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
+  hipLaunchKernelGGL(sac_team(a, p.Bp) ? a->ks.actor_team : a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
   if (a->ks.actor_heads) hipLaunchKernelGGL(a->ks.actor_heads, dim3(grid), dim3(256), 0, st, p, z);
   tmark(a, 1, st);
   SPP_CHECK_HIP(hipGetLastError());

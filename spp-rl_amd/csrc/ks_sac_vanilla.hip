@@ -10,6 +10,9 @@ bool kset_sac_vanilla(int ob, int aout, int ac, bool acmc, KernelSet* ks) {
   if (acmc || aout != ac) return false;
   if (ob == 17 && ac == 6) {
     *ks = make_kset<17, 6, 6, false>();
+    using C = Cfg<17, 6, 6, false>;
+    ks->critic_team = k_sac_critic_team<C>;
+    ks->actor_team = k_sac_actor_team<C>;
     return true;
   }
   return false;

@@ -4,6 +4,7 @@
 #pragma once
 #include "sac.hip"
 #include "ddpg.hip"
+#include "sac_team.h"
 
 namespace spp {
 
@@ -18,6 +19,10 @@ struct KernelSet {
   void (*dactor)(SacArgs, BAcmScratch);
   void (*dact)(SacArgs, ActArgs, BAcmScratch);
   void (*dreg)(SacArgs, BAcmRegArgs);
+  // small-batch (team) forms of the SAC phases: one 4-wave workgroup per 32-sample tile (sac_team.h);
+  // null where the shapes have none
+  void (*critic_team)(SacArgs);
+  void (*actor_team)(SacArgs, AcmScratch);
 };
 
 template <int OB, int AOUT, int AC, bool ACMC, bool BF = false>

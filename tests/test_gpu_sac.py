@@ -128,3 +128,33 @@ def test_vanilla_sac_fused_loop_runs():
     assert ag.stats_logger.frames == 4 * E
     for k, v in ag.loss.items():
         assert np.isfinite(v), k
+
+
+@pytest.mark.parametrize("B", [1, 33, 100, 1000, 8192])
+def test_vanilla_sac_team_kernels_match_float64_oracle(B, monkeypatch):
+    """Small batches (at most one 32-sample tile per CU) run the team forms of the phase kernels
+    (csrc/sac_team.h: one 4-wave workgroup per tile, layers split by output blocks); SPP_SAC_TEAM=0 forces the
+    one-wave kernels.  Both against the float64 oracle at the same tolerance, and not bit-identical to each other
+    (a different q / fc3 summation order: evidence the team kernels ran)."""
+    ob, ac = 17, 6
+    rng = np.random.RandomState(B)
+    batch = (rng.randn(B, ob).astype(np.float32), rng.randn(B, ob).astype(np.float32),
+             rng.uniform(-1, 1, (B, ac)).astype(np.float32), rng.randn(B).astype(np.float32),
+             (rng.rand(B) < 0.1).astype(np.int8))
+    e1, e2 = rng.randn(B, ac).astype(np.float32), rng.randn(B, ac).astype(np.float32)
+    grads = {}
+    for team in ("1", "0"):
+        monkeypatch.setenv("SPP_SAC_TEAM", team)
+        ag = build(None, B, seed=5)
+        params = {k: {n: v.numpy().copy() for n, v in ag.net_state(net).items()} for k, net in NAMES.items()}
+        ag.update(*batch, eps_next=e1, eps_cur=e2)
+        torch.cuda.synchronize()
+        o = OracleSac(ob, ac, params=params, dtype=torch.float64)
+        ol = o.update(*batch, e1, e2)
+        for k in ("critic_1", "critic_2", "actor"):
+            g = ag.grads[NAMES[k]].cpu().numpy()
+            e = relerr(g, o.last["grads"][k])
+            assert e < 2e-4, (team, k, e)
+            assert ag.loss[k] == pytest.approx(ol[k], rel=1e-4, abs=1e-6), (team, k)
+            grads[team, k] = g
+    assert any(not np.array_equal(grads["1", k], grads["0", k]) for k in ("critic_1", "critic_2", "actor"))

@@ -35,7 +35,7 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
-KSET_DEPS = ("kset.h", "sac.hip", "ddpg.hip", "sac_kernels.h", "mlp.h", "common.h")
+KSET_DEPS = ("kset.h", "sac.hip", "sac_team.h", "ddpg.hip", "sac_kernels.h", "mlp.h", "common.h")
 
 
 def _obj(src):

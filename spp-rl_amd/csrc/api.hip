@@ -1191,6 +1191,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
 //   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
 static int phase_grid(sppAgent* a, int Bp);
 static int sac_grid(sppAgent* a, int Bp);
+static bool sac_team(sppAgent* a, int Bp);
 static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int Bp = (int)round_up(B, 32);
   const int ob = a->cfg.ob, aout = a->cfg.aout, ac = a->cfg.ac;
@@ -1282,7 +1283,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       }
       J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
       jobs.back().fused = 1;
-      jobs.back().nsplit = sac_grid(a, Bp) * kWavesPerWG;
+      jobs.back().nsplit = sac_grid(a, Bp) * (sac_team(a, Bp) ? kTeamCritic : kWavesPerWG);
       jobs.back().wsplit = 1;
       fused_idx[i] = (int)jobs.size() - 1;
     }
@@ -1619,7 +1620,8 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
   SacArgs p = make_args(a, B);
   const int grid = sac_grid(a, p.Bp);
   tmark(a, 0, st);
-  hipLaunchKernelGGL(sac_team(a, p.Bp) ? a->ks.critic_team : a->ks.critic, dim3(grid), dim3(256), 0, st, p);
+  const bool team = sac_team(a, p.Bp);
+  hipLaunchKernelGGL(team ? a->ks.critic_team : a->ks.critic, dim3(grid), dim3(team ? 64 * kTeamCritic : 256), 0, st, p);
   tmark(a, 0, st);
   SPP_CHECK_HIP(hipGetLastError());
   tmark(a, 2, st);
@@ -1665,7 +1667,8 @@ static sppStatus actor_grads(sppAgentHandle a, float* losses, hipStream_t st) {
   AcmScratch z{a->Z1, a->Z2, a->T3, a->GAD, a->MASK};
   const int grid = sac_grid(a, p.Bp);
   tmark(a, 1, st);
-  hipLaunchKernelGGL(sac_team(a, p.Bp) ? a->ks.actor_team : a->ks.actor, dim3(grid), dim3(256), 0, st, p, z);
+  const bool team = sac_team(a, p.Bp);
+  hipLaunchKernelGGL(team ? a->ks.actor_team : a->ks.actor, dim3(grid), dim3(team ? 64 * kTeamActor : 256), 0, st, p, z);
   if (a->ks.actor_heads) hipLaunchKernelGGL(a->ks.actor_heads, dim3(grid), dim3(256), 0, st, p, z);
   tmark(a, 1, st);
   SPP_CHECK_HIP(hipGetLastError());
@@ -2124,6 +2127,8 @@ sppStatus sppPolicyAct(sppAgentHandle a, const float* obs, int E, const float* e
   const int grid = std::max(1, std::min(cdiv(cdiv(E, 32), kWavesPerWG), a->num_cu));
   if (a->ddpg)
     hipLaunchKernelGGL(a->ks.dact, dim3(grid), dim3(256), 0, st, p, g, a->bz);
+  else if (a->plain && a->ks.act_team && a->team_ok && cdiv(E, 32) <= a->num_cu)  // one tile per CU (sac_team.h)
+    hipLaunchKernelGGL(a->ks.act_team, dim3(cdiv(E, 32)), dim3(64 * kTeamCritic), 0, st, p, g);
   else
     hipLaunchKernelGGL(a->ks.act, dim3(grid), dim3(256), 0, st, p, g);
   SPP_CHECK_HIP(hipGetLastError());

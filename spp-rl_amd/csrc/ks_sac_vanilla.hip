@@ -13,6 +13,7 @@ bool kset_sac_vanilla(int ob, int aout, int ac, bool acmc, KernelSet* ks) {
     using C = Cfg<17, 6, 6, false>;
     ks->critic_team = k_sac_critic_team<C>;
     ks->actor_team = k_sac_actor_team<C>;
+    ks->act_team = k_policy_act_team<C>;
     return true;
   }
   return false;

@@ -23,6 +23,7 @@ struct KernelSet {
   // null where the shapes have none
   void (*critic_team)(SacArgs);
   void (*actor_team)(SacArgs, AcmScratch);
+  void (*act_team)(SacArgs, ActArgs);  // plain handles' rollout action
 };
 
 template <int OB, int AOUT, int AC, bool ACMC, bool BF = false>

@@ -4,12 +4,15 @@
 // k_sac_critic_phase / k_sac_actor_phase give each 32-sample tile to ONE wave, which runs every layer of the
 // phase as a serial chain of 32x32x2 f32 MFMAs; at B = 100 that is 4 waves on 4 SIMDs of one CU, and the
 // phase is that chain's length (MFMA-bound: ~8 layer-equivalents x 1,024 MFMAs x 64 cycles).  Here a tile
-// gets a workgroup: its 4 waves (one per SIMD) share the tile's LDS image, and each 256-wide layer is split
-// by output blocks -- wave w computes blocks 2w, 2w+1 (units 64w .. 64w+63) -- with a workgroup barrier
-// between a layer's last image read and its first image write, and another before the next layer reads.
-// The per-sample work (squash, log-prob, targets, losses, the 1-block heads) is computed by every wave on
-// the same values in the same order, so every wave holds the same scalars and the barrier sequence is
-// uniform; HBM writes of replicated values are made by wave 0 only.  Each tile runs on its own CU, one tile
+// gets a workgroup of TW waves sharing the tile's LDS image: 8 for the critic phase (two per SIMD: one's
+// MFMA chain covers the other's LDS / weight-load latency), 4 for the actor phase (more live state).  Each
+// 256-wide layer is split by output blocks -- wave w computes the 8/TW blocks from (8/TW)*w -- and each
+// 1-block layer (the heads, the critics' action-input gradient) by input blocks, its TW partial tiles summed
+// through LDS in wave order.  A workgroup barrier separates a
+// layer's last image read from its first image write, another the write from the next layer's reads.  The
+// per-sample work (squash, log-prob, targets, losses) is computed by every wave on the same values in the
+// same order, so every wave holds the same scalars and the barrier sequence is uniform; HBM writes of
+// replicated values are made by wave 0 only.  Each tile runs on its own CU, one tile
 // per workgroup (grid = min(tiles, CUs), api.hip's sac_grid).
 //
 // Same math as the one-wave kernels (sac.hip); the summation order of the q reduction and of the fused fc3
@@ -20,7 +23,57 @@
 
 namespace spp {
 
+// waves per tile: the critic phase runs 8 (two per SIMD); the actor phase 4 (its live state does not fit 8
+// waves' 256-register budget without spilling)
+constexpr int kTeamCritic = 8, kTeamActor = 4;
+
 __device__ __forceinline__ void team_sync() { __syncthreads(); }
+
+// A 1-output-block layer over the 256-unit image (ib-major image with one output block), split by input
+// blocks: wave w's 16 MFMAs over block w, the 8 partial tiles summed through LDS (part) in wave order, the
+// bias first.  Every wave returns the same tile.  Reads the image and part; team-synchronised on return (the
+// image may be written, part reused).
+template <bool BIAS, int TW>
+__device__ __forceinline__ f32x16 dense1_ksplit(const float4* __restrict__ Wf, const float* img, const float* biasL,
+                                                float (*part)[16][64], int w) {
+  constexpr int NIB = 8 / TW;  // input blocks per wave
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const float* l = img + 4 * h * 32 + (lane & 31);
+  const rsrc_t wr = rsrc(Wf);
+  const uint32_t l16 = 16u * lane;
+  float4 c[NIB][4];
+  f32x16 x[NIB];
+#pragma unroll
+  for (int k = 0; k < NIB; ++k) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[k][q] = wfrag(wr, l16, ((NIB * w + k) * 4 + q) * 1024);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[k][r] = l[(32 * (NIB * w + k) + ru(r)) * 32];
+  }
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int k = 0; k < NIB; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc = mfma(c[k][q].x, x[k][4 * q + 0], acc);
+      acc = mfma(c[k][q].y, x[k][4 * q + 1], acc);
+      acc = mfma(c[k][q].z, x[k][4 * q + 2], acc);
+      acc = mfma(c[k][q].w, x[k][4 * q + 3], acc);
+    }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) part[w][r][lane] = acc[r];
+  team_sync();
+  f32x16 t;
+  if constexpr (BIAS) t = bias_tile(biasL, 0, h);
+  else t = zero16();
+#pragma unroll
+  for (int v = 0; v < TW; ++v)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] += part[v][r][lane];
+  team_sync();
+  return t;
+}
 
 // This wave's NOW output blocks ob0 .. ob0+NOW-1 of a 256-input layer (input: the team's LDS image, all 8
 // input blocks) whose ib-major image has NBT output blocks: Wf[((ib*NBT + ob)*4 + rq)*64 + lane].  Weight
@@ -83,35 +136,37 @@ __device__ __forceinline__ void dense_lds_team(const float4* __restrict__ Wf, in
   for (int j = 0; j < NOW; ++j) epi(ob0 + j, acc[j]);
 }
 
-// This wave's 2 output blocks of a register-input layer with 8 output blocks (ob-major image, sac.hip's
-// dense); the epilogue may write the image: the caller has synchronised after the team's last image read.
-template <int NBI, uint64_t RV, typename Epi>
+// This wave's NOW output blocks ob0 .. of a register-input layer with 8 output blocks (ob-major image,
+// sac.hip's dense); the epilogue may write the image: the caller has synchronised after the team's last image
+// read.
+template <int NBI, uint64_t RV, int NOW, typename Epi>
 __device__ __forceinline__ void dense_team(const float4* __restrict__ Wf, int ob0, const f32x16 (&in)[NBI],
                                            const float* biasL, Epi&& epi) {
-  dense<NBI, RV>(Wf + (size_t)ob0 * NBI * 4 * 64, 2, in, biasL + 32 * ob0,
+  dense<NBI, RV>(Wf + (size_t)ob0 * NBI * 4 * 64, NOW, in, biasL + 32 * ob0,
                  [&](int j, const f32x16& acc) { epi(ob0 + j, acc); });
 }
-template <int NBI, uint64_t RV, typename Epi>
+template <int NBI, uint64_t RV, int NOW, typename Epi>
 __device__ __forceinline__ void dense_team(const float4* __restrict__ Wf, int ob0, const f32x16 (&in)[NBI],
                                            decltype(nullptr), Epi&& epi) {
-  dense<NBI, RV>(Wf + (size_t)ob0 * NBI * 4 * 64, 2, in, nullptr,
+  dense<NBI, RV>(Wf + (size_t)ob0 * NBI * 4 * 64, NOW, in, nullptr,
                  [&](int j, const f32x16& acc) { epi(ob0 + j, acc); });
 }
 
 // Actor trunk (sac.hip actor_trunk), team form: h1 / h2 split by blocks (masks of the wave's own blocks only),
-// heads (one block) computed by every wave from the full h2 image and written to rows [0, 2*AOUT) by wave 0.
+// heads (one block, split by input blocks) written to rows [0, 2*AOUT) by wave 0.
 // Returns with the heads in the image, team-synchronised.
-template <class C, bool ST>
+template <class C, bool ST, int TW>
 __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float* X, int xbytes, const Lane& L,
-                                                 int w, float* H1g, float* H2g, uint64_t& m1lo, uint64_t& m1hi,
-                                                 uint64_t& m2lo, uint64_t& m2hi) {
+                                                 int w, float* H1g, float* H2g, float (*part)[16][64],
+                                                 uint64_t& m1lo, uint64_t& m1hi, uint64_t& m2lo, uint64_t& m2hi) {
   static_assert(C::NB_H2 == 1, "team heads: one output block");
-  const int ob0 = 2 * w;
+  constexpr int NOW = 8 / TW;
+  const int ob0 = NOW * w;
   {
     f32x16 x[C::NB_OB];
     gm_load<C::NB_OB>(x, X, xbytes, C::OB, L.ld4, L.vo);
     const rsrc_t hr = rsrc(H1g);
-    dense_team<C::NB_OB, C::RV_X>(A.W1, ob0, x, L.tbl + A.tb1, [&](int ob, const f32x16& acc) {
+    dense_team<C::NB_OB, C::RV_X, NOW>(A.W1, ob0, x, L.tbl + A.tb1, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -127,7 +182,7 @@ __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float*
   team_sync();
   {
     const rsrc_t hr = rsrc(H2g);
-    dense_lds_team<2, 8, true>(A.W2, ob0, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
+    dense_lds_team<NOW, 8, true>(A.W2, ob0, L.img, L.tbl + A.tb2, [&](int ob, const f32x16& acc) {
       uint32_t bits = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -141,29 +196,29 @@ __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float*
     });
   }
   team_sync();
-  dense_lds_team<1, 1, true>(A.Wh, 0, L.img, L.tbl + A.tbh, [&](int, const f32x16& acc) {
-    if (w == 0) {
+  const f32x16 hd = dense1_ksplit<true, TW>(A.Wh, L.img, L.tbl + A.tbh, part, w);
+  if (w == 0) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int ur = ru(q);
-        if (ur + L.h4 < 2 * C::AOUT) L.bl[ur * 32] = acc[q];
-      }
+    for (int q = 0; q < 16; ++q) {
+      const int ur = ru(q);
+      if (ur + L.h4 < 2 * C::AOUT) L.bl[ur * 32] = hd[q];
     }
-  });
+  }
   team_sync();
 }
 
 // Critic forward through L2 (sac.hip critic_forward), team form: returns q (every wave the same value; the
 // per-wave partials of w3 . relu(h2) summed in wave order through red).  H2L: h2 of the wave's own blocks
 // goes to the image (the fused fc3 weight gradient reads it there).  Caller: the image is free to write.
-template <class C, bool ST, bool H2L>
+template <class C, bool ST, bool H2L, int TW>
 __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN],
                                                      const Lane& L, int w, float* H1g, float* H2g,
                                                      float (*red)[64], uint64_t& m1lo, uint64_t& m1hi,
                                                      uint64_t& m2lo, uint64_t& m2hi) {
-  const int ob0 = 2 * w;
+  constexpr int NOW = 8 / TW;
+  const int ob0 = NOW * w;
   const rsrc_t h1r = rsrc(H1g), h2r = rsrc(H2g);
-  dense_team<C::NB_CIN, C::RV_CIN>(Q.W1, ob0, xin, L.tbl + Q.tb1, [&](int ob, const f32x16& acc) {
+  dense_team<C::NB_CIN, C::RV_CIN, NOW>(Q.W1, ob0, xin, L.tbl + Q.tb1, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -178,7 +233,7 @@ __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f
   team_sync();
   float qp = 0.f;
   const float* w3 = L.tbl + Q.tw3;
-  dense_lds_team<2, 8, true>(Q.W2, ob0, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
+  dense_lds_team<NOW, 8, true>(Q.W2, ob0, L.img, L.tbl + Q.tb2, [&](int ob, const f32x16& acc) {
     uint32_t bits = 0;
     float tv[16];
     tvals(w3, ob, L.h4, tv);
@@ -195,32 +250,37 @@ __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f
   const int lane = lane_id();
   red[w][lane] = qp;
   team_sync();
-  const float s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  float s = red[0][lane];
+#pragma unroll
+  for (int v = 1; v < TW; ++v) s += red[v][lane];
   return s + __shfl_xor(s, 32, 64) + *Q.b3;
 }
 
 // ============================================================================ critic phase, team form
-template <class C>
-__global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
+template <class C, int TW = kTeamCritic>
+__global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
   static_assert(!C::ACMC && !C::BF && C::F3 && C::NB_PAIR == 1, "team critic phase: vanilla fp32 shapes");
   __shared__ float img[kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
-  __shared__ float red[kWavesPerWG][64];
-  __shared__ float s_dq[kWavesPerWG][32];
+  constexpr int NOW = 8 / TW;
+  constexpr int UW = 32 * NOW;  // fc3 units per wave
+  __shared__ float red[TW][64];
+  __shared__ float s_dq[TW][32];
+  __shared__ float part[TW][16][64];
   load_table(p, tbl);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int ob0 = 2 * w;
+  const int ob0 = NOW * w;
   const int ntiles = p.Bp / 32;
   const int ld = p.Bp;
   const float alpha = *p.alpha;
-  float w3a = 0.f, w3b = 0.f, b3a = 0.f, b3b = 0.f;  // fused fc3 grads of unit 64w + lane (bias: wave 0)
+  float w3a = 0.f, w3b = 0.f, b3a = 0.f, b3b = 0.f;  // fused fc3 grads of unit UW*w + lane % UW (bias: wave 0)
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const Lane L = make_lane(img, img + kSmallRow * 32, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
     uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
     // ---- target action a' ~ pi(s'), logpi'   (sac.py:230-236)
-    actor_trunk_team<C, false>(p.actor, p.S2, C::OB * L.ld4, L, w, nullptr, nullptr, d0, d1, d2, d3);
+    actor_trunk_team<C, false, TW>(p.actor, p.S2, C::OB * L.ld4, L, w, nullptr, nullptr, part, d0, d1, d2, d3);
     float lp2;
     {
       f32x16 hd[C::NB_PAIR];
@@ -233,8 +293,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
     load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, img, C::AOUT);
     team_sync();
     // ---- soft-min twin target (sac.py:237-241)
-    const float q1t = critic_forward_team<C, false, false>(p.targ[0], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
-    const float q2t = critic_forward_team<C, false, false>(p.targ[1], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
+    const float q1t = critic_forward_team<C, false, false, TW>(p.targ[0], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
+    const float q2t = critic_forward_team<C, false, false, TW>(p.targ[1], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
     const float notdone = 1.f - p.DN[b];
     const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
     // ---- both critics: forward, MSE grad, backward to the weight-gradient operands (sac.py:243-252)
@@ -245,24 +305,28 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
       f32x16 xin[C::NB_CIN];
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
-      const float q = critic_forward_team<C, true, true>(Q, xin, L, w, p.H1[i], nullptr, red, m1lo, m1hi, m2lo, m2hi);
+      const float q = critic_forward_team<C, true, true, TW>(Q, xin, L, w, p.H1[i], nullptr, red, m1lo, m1hi, m2lo, m2hi);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
       if (i == 0) lq0 = lqi; else lq1 = lqi;
-      // fc3 weight gradient of this wave's units (dW3 = dq . h2^T, db3 = sum dq): h2 rows 64w .. 64w+63 are
-      // this wave's own image rows
+      // fc3 weight gradient of this wave's units (dW3 = dq . h2^T, db3 = sum dq): h2 rows UW*w .. are this
+      // wave's own image rows; lane l sums unit UW*w + l % UW over its 32*UW/64 samples (a lane half each when
+      // UW = 32, combined across the halves)
       if (L.h == 0) s_dq[w][L.s] = dq;
       SPP_XLANE_SYNC();
       {
-        const int u = 64 * w + lane;
+        constexpr int NS = 32 * UW / 64;
+        const int u = UW * w + lane % UW;
+        const int s0 = NS * (lane / UW);
         const float* row = img + u * 32;
         float acc = 0.f;
 #pragma unroll 8
-        for (int j = 0; j < 32; ++j) {
-          const int s2 = (j + u) & 31;
+        for (int j = 0; j < NS; ++j) {
+          const int s2 = s0 + ((j + u) & (NS - 1));
           acc = fmaf(row[s2], s_dq[w][s2], acc);
         }
+        if constexpr (UW == 32) acc += __shfl_xor(acc, 32, 64);
         if (i == 0) w3a += acc; else w3b += acc;
       }
       const float dsum = wave_sum(L.h == 0 ? dq : 0.f);
@@ -272,7 +336,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
       const rsrc_t d2r = rsrc(p.D2[i]);
       const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < NOW; ++k) {
         const int ob = ob0 + k;
         float tv[16];
         tvals(w3, ob, L.h4, tv);
@@ -287,7 +351,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
       team_sync();
       // delta1 = (W2^T delta2) * relu'(h1), own blocks
       const rsrc_t d1r = rsrc(p.D1[i]);
-      dense_lds_team<2, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds_team<NOW, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2)
           fm_st_op(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
@@ -299,14 +363,18 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
       p.part[tile * kParts + 1] = s1;
     }
   }
-  // this wave's fc3 partials [256 weights | bias] per critic: unit 64w + lane, zeros elsewhere
-  const int64_t wg = (int64_t)blockIdx.x * kWavesPerWG + w;
+  // this wave's fc3 partials [256 weights | bias] per critic: units UW*w .. (from lanes 0 .. UW-1), zeros
+  // elsewhere (k_dw_reduce sums the TW slots of each workgroup)
+  const int64_t wg = (int64_t)blockIdx.x * TW + w;
   float* o0 = p.W3P[0] + wg * p.w3p_stride;
   float* o1 = p.W3P[1] + wg * p.w3p_stride;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    o0[lane + 64 * k] = k == w ? w3a : 0.f;
-    o1[lane + 64 * k] = k == w ? w3b : 0.f;
+    const int idx = lane + 64 * k;
+    const bool own = idx / UW == w;
+    const float va = __shfl(w3a, idx % UW, 64), vb = __shfl(w3b, idx % UW, 64);
+    o0[idx] = own ? va : 0.f;
+    o1[idx] = own ? vb : 0.f;
   }
   if (lane == 0) {
     o0[256] = w == 0 ? b3a : 0.f;
@@ -315,15 +383,19 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_team(SacArgs p) {
 }
 
 // ============================================================================ actor phase, team form
-template <class C>
-__global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch) {
+template <class C, int TW = kTeamActor>
+__global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScratch) {
   static_assert(!C::ACMC && !C::BF && C::NB_PAIR == 1 && C::NB_CA == 1, "team actor phase: vanilla fp32 shapes");
   __shared__ float img[kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
-  __shared__ float red[kWavesPerWG][64];
+  constexpr int NOW = 8 / TW;
+  __shared__ float red[TW][64];
+  __shared__ float part[TW][16][64];
+  __shared__ float hpark[16][64];  // the heads tile (mu | raw log-std), parked by wave 0 through the critics
+  __shared__ float apark[8 * 32];  // a_d rows [0, AOUT) of the image: the second critic's action input
   load_table(p, tbl);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int ob0 = 2 * w;
+  const int ob0 = NOW * w;
   const int ntiles = p.Bp / 32;
   const int ld = p.Bp;
   const float alpha = *p.alpha;
@@ -334,19 +406,33 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
     const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
     // ---- a, logpi = actor(s)  (sac.py:262-266)
     uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
-    actor_trunk_team<C, true>(p.actor, p.S, C::OB * L.ld4, L, w, p.AH1, p.AH2, a1lo, a1hi, a2lo, a2hi);
+    actor_trunk_team<C, true, TW>(p.actor, p.S, C::OB * L.ld4, L, w, p.AH1, p.AH2, part, a1lo, a1hi, a2lo, a2hi);
     f32x16 hd[C::NB_PAIR];
     load_pair<C>(hd, img);
     team_sync();
     const float lp = squash_write<C>(p, hd, p.EPS2, L);  // a_d -> image rows [0, AOUT), every wave the same
+    if (w == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hpark[r][lane] = hd[0][r];
+    }
     team_sync();
-    f32x16 cin[C::NB_CIN];
-    load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, img, C::AOUT);
-    team_sync();
+    if (w == 0) {
+      for (int i = lane; i < C::AOUT * 32; i += 64) apark[i] = img[i];
+    }
+    float q1, q2;
     // ---- q = min(Q1, Q2)(s, a)  (sac.py:267-270), own-block masks kept for the backward
     uint64_t ma0 = 0, ma1 = 0, ma2 = 0, ma3 = 0, mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0;
-    const float q1 = critic_forward_team<C, false, false>(p.critic[0], cin, L, w, nullptr, nullptr, red, ma0, ma1, ma2, ma3);
-    const float q2 = critic_forward_team<C, false, false>(p.critic[1], cin, L, w, nullptr, nullptr, red, mb0, mb1, mb2, mb3);
+    {
+      f32x16 cin[C::NB_CIN];
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, img, C::AOUT);
+      team_sync();
+      q1 = critic_forward_team<C, false, false, TW>(p.critic[0], cin, L, w, nullptr, nullptr, red, ma0, ma1, ma2, ma3);
+    }
+    {
+      f32x16 cin[C::NB_CIN];  // (apark: written by wave 0 before the first critic's barriers)
+      load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, apark, C::AOUT);
+      q2 = critic_forward_team<C, false, false, TW>(p.critic[1], cin, L, w, nullptr, nullptr, red, mb0, mb1, mb2, mb3);
+    }
     const float qmin = fminf(q1, q2);
     const float gq = valid ? -p.inv_B : 0.f;
     const float dqa = q1 < q2 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
@@ -360,7 +446,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
       const float dqi = i ? dqb : dqa;
       const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < NOW; ++k) {
         const int ob = ob0 + k;
         float tv[16];
         tvals(w3, ob, L.h4, tv);
@@ -368,12 +454,12 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tv[q] : 0.f;
       }
       team_sync();
-      dense_lds_team<2, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
+      dense_lds_team<NOW, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
       });
       team_sync();
-      dense_lds_team<1, 1, false>(Q.W1Ta, 0, img, nullptr, [&](int, const f32x16& acc) { dca += acc; });
+      dca += dense1_ksplit<false, TW>(Q.W1Ta, img, nullptr, part, w);
     }
     // d loss / d a_d into image rows [0, AOUT) (the heads backward reads it in the pairing layout)
 #pragma unroll
@@ -382,6 +468,8 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
       if (ur + L.h4 < C::AOUT) L.bl[ur * 32] = dca[q];
     }
     team_sync();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hd[0][r] = hpark[r][lane];
     // ---- heads backward in the pairing layout (squash, denorm, custom loss, logpi): sac.hip's actor phase
     float sac_part = (valid && L.h == 0) ? fsub_rn(alpha * lp, qmin) : 0.f;
     float dist_part = 0.f;
@@ -443,7 +531,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
     }
     team_sync();  // the image rows read by the heads backward (L.pl) are rewritten below
     // ---- dh2 = Wh^T dheads * relu'(h2) (own blocks); dh1 = W2^T dh2 * relu'(h1)
-    dense_team<C::NB_PAIR, C::RV_PAIR>(p.actor.WhT, ob0, hd, nullptr, [&](int ob, const f32x16& acc) {
+    dense_team<C::NB_PAIR, C::RV_PAIR, NOW>(p.actor.WhT, ob0, hd, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
@@ -453,7 +541,7 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
       }
     });
     team_sync();
-    dense_lds_team<2, 8, false>(p.actor.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
+    dense_lds_team<NOW, 8, false>(p.actor.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q)
         fm_st_op(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
@@ -466,6 +554,66 @@ __global__ __launch_bounds__(256, 1) void k_sac_actor_team(SacArgs p, AcmScratch
       p.part[tile * kParts + 3] = pd;
       p.part[tile * kParts + 4] = pl;
     }
+  }
+}
+
+}  // namespace spp
+
+namespace spp {
+
+// ============================================================================ rollout action, team form
+// k_policy_act (sac.hip) for the plain (vanilla SAC) handles: the actor trunk of each 32-env tile split over a
+// TW-wave workgroup (actor_trunk_team), then the per-env action of DDPG.noise_action / SAC sampling
+// (ddpg.py:171-180, sac.py:182-196) computed by every wave and written by wave 0.  Same arithmetic as
+// k_policy_act's plain branch.
+template <class C, int TW = kTeamCritic>
+__global__ __launch_bounds__(TW * 64, 1) void k_policy_act_team(SacArgs p, ActArgs a) {
+  static_assert(C::NB_PAIR == 1, "team act: one pairing block");
+  __shared__ float img[kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
+  __shared__ float part[TW][16][64];
+  load_table(p, tbl);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int ntiles = (a.E + 31) / 32;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int e = tile * 32 + (lane & 31);
+    const bool valid = e < a.E;
+    const int er = valid ? e : 0;
+    Lane L = make_lane(img, img + kSmallRow * 32, tbl, 1, er * C::OB);  // row-major obs: ld = 1
+    const bool use_actor = a.mode == 1 || a.mode == 2;
+    f32x16 hd[C::NB_PAIR];
+    if (use_actor) {
+      uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+      actor_trunk_team<C, false, TW>(p.actor, a.obs, a.E * C::OB * 4, L, w, nullptr, nullptr, part, d0, d1, d2, d3);
+      load_pair<C>(hd, img);
+    }
+    const int h8 = 8 * L.h;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int j = r + h8;
+      if (j < C::AOUT) {
+        const float lim = actor_lim<true>(p, L.tbl, j);
+        float act;
+        if (a.mode == 0 || a.mode == 3) {
+          act = valid ? a.eps[er * C::AOUT + j] : 0.f;  // action_space.sample() drawn by the caller
+        } else {  // DDPG.noise_action: a + act_noise * N(0,1), clip to [-lim, lim]
+          const float mu = hd[0][r];
+          float u = mu;
+          if (a.mode == 1 && a.eps) {
+            const float ls = fminf(fmaxf(hd[0][r + 8], -20.f), 2.f);
+            u = fadd_rn(mu, fmul_rn(valid ? a.eps[er * C::AOUT + j] : 0.f, expf(ls)));
+          }
+          act = fmul_rn(tanhf(u), lim);
+          if (a.mode == 1 && a.noise) act = fadd_rn(act, a.act_noise * (valid ? a.noise[er * C::AOUT + j] : 0.f));
+          act = fminf(fmaxf(act, -lim), lim);
+        }
+        if (valid && w == 0) {
+          a.target_out[er * C::AOUT + j] = act;
+          a.env_out[er * C::AOUT + j] = act;  // process_action: identity (ddpg.py:371-384)
+        }
+      }
+    }
+    team_sync();  // the next tile's trunk rewrites the image the heads were read from
   }
 }
 

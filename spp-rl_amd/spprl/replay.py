@@ -162,9 +162,22 @@ class BufferAcMOffPolicy:
                                 [bool(done)], [bool(end)], acm)
 
     # ------------------------------------------------------------------ reads
+    def _idx_dev(self, idx):
+        """Host indices (sample_batch's numpy draw) -> device int64, through pinned memory and an async copy:
+        a pageable upload synchronises the stream (the device would drain before every grad step of the
+        reference schedule).  torch's pinned-block cache keeps the block until the copy has completed."""
+        if isinstance(idx, torch.Tensor) and idx.device == self.device:
+            return idx.to(torch.int64).contiguous()
+        h = torch.as_tensor(np.asarray(idx) if not isinstance(idx, torch.Tensor) else idx, dtype=torch.int64)
+        if self.device.type != "cuda":
+            return h.contiguous()
+        pin = torch.empty(h.shape, dtype=torch.int64, pin_memory=True)
+        pin.copy_(h)
+        return pin.to(self.device, non_blocking=True)
+
     def gather(self, idx):
         """Tuples for given indices, reference layout (sample_batch :385-398)."""
-        idx = torch.as_tensor(idx, dtype=torch.int64).to(self.device).contiguous()
+        idx = self._idx_dev(idx)
         B = idx.numel()
         f = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa
         obs, nobs, act, rew, acm = f(B, self.obs_shape), f(B, self.obs_shape), f(B, self.act_shape), f(B), f(

@@ -121,6 +121,12 @@ def parse():
     ap.add_argument("--rehearse-world", type=int, default=None,
                     help="ppo_hcheetah on one GPU: the per-rank work of a W-rank job (ACM cadence scaled for W ranks, "
                          "update on a W-rank union's shape); value = W x this rank's env-steps/s (projection)")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="vanilla_sac_hcheetah: R independent single-env runs (separate processes, seeds i) sharing "
+                         "the GPU, timed together -- the layout of the reference's own configs[0] script (a pool of "
+                         "independent runs) and of this line's cpu_baseline; value = R x steps / the slowest "
+                         "replica's timed span")
+    ap.add_argument("--replica-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--host-env", action="store_true",
                     help="step the envs on the host CPU (HostSynthEnv: vectorised numpy SynthEnv behind pinned "
                          "staging + side-stream copies, the update overlapping the host step): the PCIe-inclusive "
@@ -652,8 +658,85 @@ def launch_ranks(n):
     return p.wait()
 
 
+def run_replicas(args):
+    """--replicas R: R worker processes of this script (one vanilla-SAC run each, seed = replica index), started
+    before this process touches the GPU; each reports READY after its warm-up and starts its timed steps on GO,
+    which this process sends to all of them at once."""
+    import subprocess
+
+    argv, skip = [], False
+    for a in sys.argv[1:]:
+        if skip:
+            skip = False
+            continue
+        if a == "--replicas":
+            skip = True
+            continue
+        if a.startswith("--replicas="):
+            continue
+        argv.append(a)
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--replica-worker", "--no-cpu-baseline", "--no-pmc",
+                                                                 "--no-rocprof"]
+    procs = []
+    for i in range(args.replicas):
+        env = dict(os.environ, SPP_REPLICA_INDEX=str(i))
+        procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env))
+    try:
+        for p in procs:
+            while True:
+                line = p.stdout.readline()
+                if not line:
+                    raise RuntimeError("replica worker exited before READY (status %s)" % p.wait())
+                if line.strip() == "READY":
+                    break
+        t0 = time.perf_counter()
+        for p in procs:
+            p.stdin.write("GO\n")
+            p.stdin.flush()
+        outs = []
+        for p in procs:
+            out, _ = p.communicate(timeout=1200)
+            lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+            if p.returncode != 0 or not lines:
+                raise RuntimeError("replica worker failed (status %s)" % p.returncode)
+            outs.append(json.loads(lines[-1]))
+        wall = time.perf_counter() - t0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    spans = [o["ms_per_step"] * o["steps"] / 1e3 for o in outs]
+    res = dict(outs[0])
+    res["value"] = round(args.replicas * args.steps / max(spans), 1)
+    res["ms_per_step"] = round(max(spans) / args.steps * 1e3, 4)
+    res["config"] = dict(res["config"], workload=res["config"]["workload"] + "; %d independent replicas sharing one "
+                         "GPU" % args.replicas, parallelism="%d replicas, 1 GPU" % args.replicas)
+    res["replicas"] = {"n": args.replicas, "per_replica_value": [o["value"] for o in outs],
+                       "per_replica_ms_per_step": [o["ms_per_step"] for o in outs],
+                       "param_checksums": [o.get("param_checksum") for o in outs],
+                       "wall_s_incl_teardown": round(wall, 3),
+                       "note": "value = replicas x steps / the slowest replica's timed span (each replica times its "
+                               "own steps from the common GO); the same layout as cpu_baseline (concurrent "
+                               "independent single-thread runs) and the reference's train/vanilla_sac_hcheetah.py "
+                               "(a multiprocessing pool of independent runs)"}
+    for k in ("roofline", "kernels_ms_per_launch", "kernels_tflops", "step_tflops"):
+        res.pop(k, None)
+    res["roofline"] = outs[0].get("roofline")
+    if res["roofline"] is not None:
+        res["roofline"] = dict(res["roofline"], scope="replica 0's critic-phase launches, measured while all "
+                                                      "replicas ran")
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_report(args.config, args.cpu_seconds, args.cpu_procs or default_cpu_procs())
+    print(json.dumps(res), flush=True)
+
+
 def main():
     args = parse()
+    if args.replicas > 1 and not args.replica_worker:
+        if args.config != "vanilla_sac_hcheetah" or args.gpus != 1:
+            sys.stderr.write("bench.py: --replicas is for --config vanilla_sac_hcheetah on one GPU\n")
+            sys.exit(2)
+        return run_replicas(args)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -695,7 +778,7 @@ def main():
     batch_size = a.pop("batch_size")
     rho = a["update_batch_size"] * a["grad_steps"] / a["update_freq"]
     sigma = a["acm_update_batches"] * a["acm_batch_size"] / a["acm_update_freq"] if not vanilla else 0.0
-    seed = shard_seed(1000, rank)
+    seed = shard_seed(1000, rank + int(os.environ.get("SPP_REPLICA_INDEX", "0")))
     if vanilla:
         Agent = spprl.SAC
         B, BA = a["update_batch_size"], 0
@@ -765,6 +848,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if args.replica_worker:  # run_replicas: start the timed steps together
+        print("READY", flush=True)
+        sys.stdin.readline()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -843,7 +929,7 @@ def main():
         allc = [torch.empty_like(chk) for _ in range(world)]
         dist.all_gather(allc, chk)
         result["replicas_identical"] = bool(all(torch.equal(allc[0], c) for c in allc))
-    if world == 1:
+    if world == 1 and not args.replica_worker:
         result["hbm_kernels"] = hbm_kernels(ag, cfg, B, E)
     if rank == 0 and world == 1 and not args.no_rocprof:
         kt_ms, kt_src = rocprof_kernel_ms(args, E, cap, kname)

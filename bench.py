@@ -880,6 +880,9 @@ def main():
     bf16 = cfg.get("bf16", False)
     peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     kname = "k_ddpg_critic_phase" if cfg["algo"] == "ddpg" else "k_sac_critic_phase"
+    if vanilla and os.environ.get("SPP_SAC_TEAM", "1") != "0" and \
+            -(-B // 32) <= torch.cuda.get_device_properties(dev).multi_processor_count:
+        kname = "k_sac_critic_team"  # small batches: the team form (csrc/sac_team.h, api.hip sac_team)
     grad_steps_per_step = k_cnt["critic_phase"] / args.steps
     flop_step = 2.0 * (mac["update"] * B * grad_steps_per_step + mac["acm_reg"] * BA + mac["act"] * E)
     metric = {"sac": "SPP-SAC ", "ddpg": "SPP-DDPG ", "vanilla": "vanilla SAC "}[cfg["algo"]] + cfg["env"]

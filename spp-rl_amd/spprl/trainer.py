@@ -548,8 +548,17 @@ class OffPolicyLoop:
         (make_unbiased_update, ddpg_acm.py:59-73): the sampled next obs is the critic's action."""
         if self.update_condition():
             unbiased = getattr(self, "unbiased_update", False)
+            rb = self.replay_buffer
+            # vanilla SAC on the device: the same MT19937 index draw as sample_batch (replay_buffer.py:234), staged
+            # feature-major straight from the ring (one gather kernel instead of a row-major gather + restage) with
+            # the rsample noise drawn on the device
+            staged = getattr(self, "VANILLA", False) and self.device.type == "cuda"
             for _ in range(self.grad_steps):
-                batch = self.replay_buffer.sample_batch(self.update_batch_size, self.device)
+                if staged:
+                    idx = np.random.randint(0, len(rb), self.update_batch_size)
+                    self.update_from_replay(rb._idx_dev(idx), self._key_update, self._next())
+                    continue
+                batch = rb.sample_batch(self.update_batch_size, self.device)
                 if unbiased:
                     batch[2] = batch[1]
                 self.update(*batch)

@@ -1191,6 +1191,7 @@ static sppStatus finalize_dw(DwSet& D, std::vector<DwJob>& jobs, int nph, int Bp
 //   set 0: SAC (phase 0 = both critics, phase 1 = actor); set 1: ACM regression
 static int phase_grid(sppAgent* a, int Bp);
 static int sac_grid(sppAgent* a, int Bp);
+static int sac_critic_grid(sppAgent* a, int Bp);
 static bool sac_team(sppAgent* a, int Bp);
 static sppStatus build_dw(sppAgent* a, int set, int B) {
   const int Bp = (int)round_up(B, 32);
@@ -1283,7 +1284,7 @@ static sppStatus build_dw(sppAgent* a, int set, int B) {
       }
       J(nullptr, 1, nullptr, 256, nullptr, 0, gw3, gb3);
       jobs.back().fused = 1;
-      jobs.back().nsplit = sac_grid(a, Bp) * (sac_team(a, Bp) ? kTeamCritic : kWavesPerWG);
+      jobs.back().nsplit = sac_critic_grid(a, Bp) * (sac_team(a, Bp) ? kTeamCritic : kWavesPerWG);
       jobs.back().wsplit = 1;
       fused_idx[i] = (int)jobs.size() - 1;
     }
@@ -1406,6 +1407,11 @@ static bool sac_team(sppAgent* a, int Bp) {
 }
 static int sac_grid(sppAgent* a, int Bp) {
   return sac_team(a, Bp) ? std::max(1, std::min(Bp / 32, a->num_cu)) : phase_grid(a, Bp);
+}
+// the team critic phase splits each tile's two critics over two workgroups while 2 x tiles fit the CUs
+static int sac_critic_grid(sppAgent* a, int Bp) {
+  const int nt = std::max(1, Bp / 32);
+  return sac_team(a, Bp) && 2 * nt <= a->num_cu ? 2 * nt : sac_grid(a, Bp);
 }
 
 static sppStatus check_ready(sppAgent* a) {
@@ -1618,7 +1624,7 @@ static sppStatus critic_grads_staged(sppAgentHandle a, float* losses, hipStream_
   launch_pack(a, a->o_actor, (int)(a->pj_actor.size() + a->pj_acm.size() + a->pj_targ.size() + a->pj_critic_fwd.size()),
               st);
   SacArgs p = make_args(a, B);
-  const int grid = sac_grid(a, p.Bp);
+  const int grid = sac_critic_grid(a, p.Bp);
   tmark(a, 0, st);
   const bool team = sac_team(a, p.Bp);
   hipLaunchKernelGGL(team ? a->ks.critic_team : a->ks.critic, dim3(grid), dim3(team ? 64 * kTeamCritic : 256), 0, st, p);

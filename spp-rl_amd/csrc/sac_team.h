@@ -274,7 +274,12 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
   const int ld = p.Bp;
   const float alpha = *p.alpha;
   float w3a = 0.f, w3b = 0.f, b3a = 0.f, b3b = 0.f;  // fused fc3 grads of unit UW*w + lane % UW (bias: wave 0)
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // critic split (grid = 2 x tiles, api.hip sac_critic_grid): workgroup 2t + c runs tile t's target (both target
+  // critics, computed by both workgroups of the tile) and critic c only; else every critic of every tile
+  const bool split = (int)gridDim.x == 2 * ntiles;
+  const int c0 = split ? (int)(blockIdx.x & 1) : 0, c1 = split ? c0 + 1 : 2;
+  const int tstride = split ? ntiles : (int)gridDim.x;
+  for (int tile = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x; tile < ntiles; tile += tstride) {
     const Lane L = make_lane(img, img + kSmallRow * 32, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
@@ -300,7 +305,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
     // ---- both critics: forward, MSE grad, backward to the weight-gradient operands (sac.py:243-252)
     float lq0 = 0.f, lq1 = 0.f;
 #pragma unroll 1
-    for (int i = 0; i < 2; ++i) {
+    for (int i = c0; i < c1; ++i) {
       uint64_t m1lo = 0, m1hi = 0, m2lo = 0, m2hi = 0;
       f32x16 xin[C::NB_CIN];
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, p.ACT, C::CA, L.ld4, L.vo);
@@ -359,8 +364,8 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
     }
     const float s0 = wave_sum(lq0), s1 = wave_sum(lq1);
     if (w == 0 && lane == 0) {
-      p.part[tile * kParts + 0] = s0;
-      p.part[tile * kParts + 1] = s1;
+      if (c0 == 0) p.part[tile * kParts + 0] = s0;
+      if (c1 == 2) p.part[tile * kParts + 1] = s1;
     }
   }
   // this wave's fc3 partials [256 weights | bias] per critic: units UW*w .. (from lanes 0 .. UW-1), zeros

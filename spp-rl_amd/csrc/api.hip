@@ -1710,10 +1710,9 @@ sppStatus sppSacAcmDrawEps(sppAgentHandle a, uint64_t seed, uint64_t counter, vo
   const int B = a->cur_B, Bp = (int)round_up(B, 32);
   SPP_REQUIRE((int64_t)a->cfg.aout * Bp < ((int64_t)1 << 31), SPP_E_SHAPE, "draw_eps: aout * Bp >= 2^31");
   const int64_t quads = (int64_t)a->cfg.aout * Bp / 4;
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(quads, 256)), dim3(256), 0, S(stream), a->EPS1, a->cfg.aout, B, Bp, seed,
-                     2 * counter);
-  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(quads, 256)), dim3(256), 0, S(stream), a->EPS2, a->cfg.aout, B, Bp, seed,
-                     2 * counter + 1);
+  // EPS1 (counter 2c) and EPS2 (2c + 1) in one launch (grid.y)
+  hipLaunchKernelGGL(k_eps_fm, dim3(cdiv(quads, 256), 2), dim3(256), 0, S(stream), a->EPS1, a->cfg.aout, B, Bp, seed,
+                     2 * counter, a->EPS2, 2 * counter + 1);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }

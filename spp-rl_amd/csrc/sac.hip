@@ -1267,7 +1267,11 @@ __device__ __forceinline__ void box_muller_hw(uint32_t a, uint32_t b, float& n0,
 }
 // eps [aout][Bp] (padding columns b >= B zero): one philox block -> 4 normals -> one 16-B store
 // (Bp is a multiple of 32, so a quad never crosses a row).
-__global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint64_t ctr) {
+__global__ void k_eps_fm(float* E, int aout, int B, int Bp, uint64_t seed, uint64_t ctr, float* E2, uint64_t ctr2) {
+  if (blockIdx.y) {  // (a second array in the same launch: the update's two rsample draws)
+    E = E2;
+    ctr = ctr2;
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;  // quad index; aout * Bp < 2^31 (host check)
   if (4 * i >= aout * Bp) return;
   const u32x4 r = philox(seed, ctr, (uint64_t)i);

@@ -29,6 +29,13 @@ constexpr int kTeamCritic = 8, kTeamActor = 4;
 
 __device__ __forceinline__ void team_sync() { __syncthreads(); }
 
+// ReLU masks of the wave's own output blocks only (k = ob - ob0 < 8/TW <= 2): 16 bits per block in one register
+__device__ __forceinline__ void setown(uint32_t& m, int k, uint32_t bits) {
+  m |= bits << (16 * k);
+  asm volatile("" : "+v"(m));
+}
+__device__ __forceinline__ bool getown(uint32_t m, int k, int q) { return (m >> (16 * k + q)) & 1u; }
+
 // A 1-output-block layer over the 256-unit image (ib-major image with one output block), split by input
 // blocks: wave w's 16 MFMAs over block w, the 8 partial tiles summed through LDS (part) in wave order, the
 // bias first.  Every wave returns the same tile.  Reads the image and part; team-synchronised on return (the
@@ -158,7 +165,7 @@ __device__ __forceinline__ void dense_team(const float4* __restrict__ Wf, int ob
 template <class C, bool ST, int TW>
 __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float* X, int xbytes, const Lane& L,
                                                  int w, float* H1g, float* H2g, float (*part)[16][64],
-                                                 uint64_t& m1lo, uint64_t& m1hi, uint64_t& m2lo, uint64_t& m2hi) {
+                                                 uint32_t& m1, uint32_t& m2) {
   static_assert(C::NB_H2 == 1, "team heads: one output block");
   constexpr int NOW = 8 / TW;
   const int ob0 = NOW * w;
@@ -176,7 +183,7 @@ __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float*
         if constexpr (ST) fm_st_op(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
-      setbits(m1lo, m1hi, ob, bits);
+      setown(m1, ob - ob0, bits);
     });
   }
   team_sync();
@@ -192,7 +199,7 @@ __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float*
         if constexpr (ST) fm_st_op(hr, ur, L.ld4, L.vo, v);
         bits |= (uint32_t)(v > 0.f) << q;
       }
-      setbits(m2lo, m2hi, ob, bits);
+      setown(m2, ob - ob0, bits);
     });
   }
   team_sync();
@@ -213,8 +220,7 @@ __device__ __forceinline__ void actor_trunk_team(const ActorDev& A, const float*
 template <class C, bool ST, bool H2L, int TW>
 __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f32x16 (&xin)[C::NB_CIN],
                                                      const Lane& L, int w, float* H1g, float* H2g,
-                                                     float (*red)[64], uint64_t& m1lo, uint64_t& m1hi,
-                                                     uint64_t& m2lo, uint64_t& m2hi) {
+                                                     float (*red)[64], uint32_t& m1, uint32_t& m2) {
   constexpr int NOW = 8 / TW;
   const int ob0 = NOW * w;
   const rsrc_t h1r = rsrc(H1g), h2r = rsrc(H2g);
@@ -228,7 +234,7 @@ __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f
       if constexpr (ST) fm_st_op(h1r, ur, L.ld4, L.vo, v);
       bits |= (uint32_t)(v > 0.f) << q;
     }
-    setbits(m1lo, m1hi, ob, bits);
+    setown(m1, ob - ob0, bits);
   });
   team_sync();
   float qp = 0.f;
@@ -245,7 +251,7 @@ __device__ __forceinline__ float critic_forward_team(const CriticDev& Q, const f
       qp = fmaf(v, tv[q], qp);
       bits |= (uint32_t)(v > 0.f) << q;
     }
-    setbits(m2lo, m2hi, ob, bits);
+    setown(m2, ob - ob0, bits);
   });
   const int lane = lane_id();
   red[w][lane] = qp;
@@ -283,9 +289,9 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
     const Lane L = make_lane(img, img + kSmallRow * 32, tbl, ld, tile * 32 + (lane & 31));
     const int b = L.b;
     const bool valid = b < p.B;
-    uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    uint32_t d0 = 0, d1 = 0;
     // ---- target action a' ~ pi(s'), logpi'   (sac.py:230-236)
-    actor_trunk_team<C, false, TW>(p.actor, p.S2, C::OB * L.ld4, L, w, nullptr, nullptr, part, d0, d1, d2, d3);
+    actor_trunk_team<C, false, TW>(p.actor, p.S2, C::OB * L.ld4, L, w, nullptr, nullptr, part, d0, d1);
     float lp2;
     {
       f32x16 hd[C::NB_PAIR];
@@ -298,19 +304,19 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
     load_cat_gl<C::NB_OB, C::NB_CA>(tin, p.S2, C::OB * L.ld4, C::OB, L.ld4, L.vo, img, C::AOUT);
     team_sync();
     // ---- soft-min twin target (sac.py:237-241)
-    const float q1t = critic_forward_team<C, false, false, TW>(p.targ[0], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
-    const float q2t = critic_forward_team<C, false, false, TW>(p.targ[1], tin, L, w, nullptr, nullptr, red, d0, d1, d2, d3);
+    const float q1t = critic_forward_team<C, false, false, TW>(p.targ[0], tin, L, w, nullptr, nullptr, red, d0, d1);
+    const float q2t = critic_forward_team<C, false, false, TW>(p.targ[1], tin, L, w, nullptr, nullptr, red, d0, d1);
     const float notdone = 1.f - p.DN[b];
     const float y = fadd_rn(p.R[b], fmul_rn(p.gamma * notdone, fsub_rn(fminf(q1t, q2t), alpha * lp2)));
     // ---- both critics: forward, MSE grad, backward to the weight-gradient operands (sac.py:243-252)
     float lq0 = 0.f, lq1 = 0.f;
 #pragma unroll 1
     for (int i = c0; i < c1; ++i) {
-      uint64_t m1lo = 0, m1hi = 0, m2lo = 0, m2hi = 0;
+      uint32_t m1 = 0, m2 = 0;
       f32x16 xin[C::NB_CIN];
       load_cat_gg<C::NB_OB, C::NB_CA>(xin, p.S, C::OB, p.ACT, C::CA, L.ld4, L.vo);
       const CriticDev& Q = p.critic[i];
-      const float q = critic_forward_team<C, true, true, TW>(Q, xin, L, w, p.H1[i], nullptr, red, m1lo, m1hi, m2lo, m2hi);
+      const float q = critic_forward_team<C, true, true, TW>(Q, xin, L, w, p.H1[i], nullptr, red, m1, m2);
       const float diff = fsub_rn(q, y);
       const float dq = valid ? fmul_rn(2.f * diff, p.inv_B) : 0.f;
       const float lqi = (valid && L.h == 0) ? diff * diff : 0.f;
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2) {
           const int ur = 32 * ob + ru(q2);
-          const float v = getbit(m2lo, m2hi, ob, q2) ? dq * tv[q2] : 0.f;
+          const float v = getown(m2, k, q2) ? dq * tv[q2] : 0.f;
           L.bl[ur * 32] = v;
           fm_st_op(d2r, ur, L.ld4, L.vo, v);
         }
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_critic_team(SacArgs p) {
       dense_lds_team<NOW, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
         for (int q2 = 0; q2 < 16; ++q2)
-          fm_st_op(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getbit(m1lo, m1hi, ob, q2) ? acc[q2] : 0.f);
+          fm_st_op(d1r, 32 * ob + ru(q2), L.ld4, L.vo, getown(m1, ob - ob0, q2) ? acc[q2] : 0.f);
       });
     }
     const float s0 = wave_sum(lq0), s1 = wave_sum(lq1);
@@ -398,6 +404,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
   __shared__ float part[TW][16][64];
   __shared__ float hpark[16][64];  // the heads tile (mu | raw log-std), parked by wave 0 through the critics
   __shared__ float apark[8 * 32];  // a_d rows [0, AOUT) of the image: the second critic's action input
+  __shared__ float dpark[16][64];  // the first critic's d loss / d a tile
   load_table(p, tbl);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int ob0 = NOW * w;
@@ -410,8 +417,8 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
     const bool valid = b < p.B;
     const float g_lp = valid ? alpha * p.inv_B : 0.f;  // d loss / d logpi_b
     // ---- a, logpi = actor(s)  (sac.py:262-266)
-    uint64_t a1lo = 0, a1hi = 0, a2lo = 0, a2hi = 0;
-    actor_trunk_team<C, true, TW>(p.actor, p.S, C::OB * L.ld4, L, w, p.AH1, p.AH2, part, a1lo, a1hi, a2lo, a2hi);
+    uint32_t a1 = 0, a2 = 0;
+    actor_trunk_team<C, true, TW>(p.actor, p.S, C::OB * L.ld4, L, w, p.AH1, p.AH2, part, a1, a2);
     f32x16 hd[C::NB_PAIR];
     load_pair<C>(hd, img);
     team_sync();
@@ -426,28 +433,28 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
     }
     float q1, q2;
     // ---- q = min(Q1, Q2)(s, a)  (sac.py:267-270), own-block masks kept for the backward
-    uint64_t ma0 = 0, ma1 = 0, ma2 = 0, ma3 = 0, mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0;
+    uint32_t ma1 = 0, ma2 = 0, mb1 = 0, mb2 = 0;
     {
       f32x16 cin[C::NB_CIN];
       load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, img, C::AOUT);
       team_sync();
-      q1 = critic_forward_team<C, false, false, TW>(p.critic[0], cin, L, w, nullptr, nullptr, red, ma0, ma1, ma2, ma3);
+      q1 = critic_forward_team<C, false, false, TW>(p.critic[0], cin, L, w, nullptr, nullptr, red, ma1, ma2);
     }
     {
       f32x16 cin[C::NB_CIN];  // (apark: written by wave 0 before the first critic's barriers)
       load_cat_gl<C::NB_OB, C::NB_CA>(cin, p.S, C::OB * L.ld4, C::OB, L.ld4, L.vo, apark, C::AOUT);
-      q2 = critic_forward_team<C, false, false, TW>(p.critic[1], cin, L, w, nullptr, nullptr, red, mb0, mb1, mb2, mb3);
+      q2 = critic_forward_team<C, false, false, TW>(p.critic[1], cin, L, w, nullptr, nullptr, red, mb1, mb2);
     }
     const float qmin = fminf(q1, q2);
     const float gq = valid ? -p.inv_B : 0.f;
     const float dqa = q1 < q2 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
     const float dqb = q2 < q1 ? gq : (q1 == q2 ? 0.5f * gq : 0.f);
     // ---- back through both critics to their action input
-    f32x16 dca = zero16();
+    f32x16 dca;  // d loss / d a: critic 0's tile parked in LDS (dpark) through critic 1's backward
 #pragma unroll 1
     for (int i = 0; i < 2; ++i) {
       const CriticDev& Q = p.critic[i];
-      const uint64_t k0 = i ? mb0 : ma0, k1 = i ? mb1 : ma1, k2 = i ? mb2 : ma2, k3 = i ? mb3 : ma3;
+      const uint32_t k1m = i ? mb1 : ma1, k2m = i ? mb2 : ma2;
       const float dqi = i ? dqb : dqa;
       const float* w3 = tbl + Q.tw3;
 #pragma unroll 1
@@ -456,15 +463,24 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
         float tv[16];
         tvals(w3, ob, L.h4, tv);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k2, k3, ob, q) ? dqi * tv[q] : 0.f;
+        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getown(k2m, k, q) ? dqi * tv[q] : 0.f;
       }
       team_sync();
       dense_lds_team<NOW, 8, false>(Q.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getbit(k0, k1, ob, q) ? acc[q] : 0.f;
+        for (int q = 0; q < 16; ++q) L.bl[(32 * ob + ru(q)) * 32] = getown(k1m, ob - ob0, q) ? acc[q] : 0.f;
       });
       team_sync();
-      dca += dense1_ksplit<false, TW>(Q.W1Ta, img, nullptr, part, w);
+      const f32x16 t = dense1_ksplit<false, TW>(Q.W1Ta, img, nullptr, part, w);
+      if (i == 0) {
+        if (w == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dpark[r][lane] = t[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dca[r] = (0.f + dpark[r][lane]) + t[r];
+      }
     }
     // d loss / d a_d into image rows [0, AOUT) (the heads backward reads it in the pairing layout)
 #pragma unroll
@@ -540,7 +556,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int ur = 32 * ob + ru(q);
-        const float v = getbit(a2lo, a2hi, ob, q) ? acc[q] : 0.f;
+        const float v = getown(a2, ob - ob0, q) ? acc[q] : 0.f;
         L.bl[ur * 32] = v;
         fm_st_op(rsrc(p.AD2), ur, L.ld4, L.vo, v);
       }
@@ -549,7 +565,7 @@ __global__ __launch_bounds__(TW * 64, 1) void k_sac_actor_team(SacArgs p, AcmScr
     dense_lds_team<NOW, 8, false>(p.actor.W2T, ob0, img, nullptr, [&](int ob, const f32x16& acc) {
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        fm_st_op(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getbit(a1lo, a1hi, ob, q) ? acc[q] : 0.f);
+        fm_st_op(rsrc(p.AD1), 32 * ob + ru(q), L.ld4, L.vo, getown(a1, ob - ob0, q) ? acc[q] : 0.f);
     });
     const float ps = wave_sum(sac_part);
     const float pd = wave_sum(dist_part);
@@ -588,8 +604,8 @@ __global__ __launch_bounds__(TW * 64, 1) void k_policy_act_team(SacArgs p, ActAr
     const bool use_actor = a.mode == 1 || a.mode == 2;
     f32x16 hd[C::NB_PAIR];
     if (use_actor) {
-      uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-      actor_trunk_team<C, false, TW>(p.actor, a.obs, a.E * C::OB * 4, L, w, nullptr, nullptr, part, d0, d1, d2, d3);
+      uint32_t d0 = 0, d1 = 0;
+      actor_trunk_team<C, false, TW>(p.actor, a.obs, a.E * C::OB * 4, L, w, nullptr, nullptr, part, d0, d1);
       load_pair<C>(hd, img);
     }
     const int h8 = 8 * L.h;

@@ -121,6 +121,13 @@ def parse():
     ap.add_argument("--rehearse-world", type=int, default=None,
                     help="ppo_hcheetah on one GPU: the per-rank work of a W-rank job (ACM cadence scaled for W ranks, "
                          "update on a W-rank union's shape); value = W x this rank's env-steps/s (projection)")
+    ap.add_argument("--ppo-minibatch", type=int, default=None,
+                    help="ppo_hcheetah: the clip-loss minibatch (default 512 x s, the cadence rule of every sample "
+                         "count; 512 = the reference's absolute minibatch, round 5's line)")
+    ap.add_argument("--ppo-dp", choices=["shard", "union"], default="shard",
+                    help="ppo_hcheetah data parallel update: each rank on its own rollout with one gradient all-reduce "
+                         "per critic / actor step (shard), or one all-gather of the rollouts and the whole update on "
+                         "the union on every rank (union, round 5)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="vanilla_sac_hcheetah: R independent single-env runs (separate processes, seeds i) sharing "
                          "the GPU, timed together -- the layout of the reference's own configs[0] script (a pool of "
@@ -431,7 +438,7 @@ def hbm_kernels(ag, cfg, B, E):
 
 
 # ------------------------------------------------------------------ PPO_AcM (configs[3])
-def bench_ppo(args, world, rank, dev):
+def bench_ppo(args, world, rank, dev, comm=None):
     """configs[3]: SPP-PPO HalfCheetah-v2, 16384 envs over 8 GPUs = 2048 per GPU (train/spp_ppo_hcheetah.py
     hyper-parameters).  One step = one PPO_AcM iteration: T = 16 vector steps of rollout (actor sample,
     AcM, env, ACM ring writes), 10 x 10 full-batch critic steps, GAE over [T][E], <= 10 clip-loss epochs of
@@ -452,20 +459,23 @@ def bench_ppo(args, world, rank, dev):
     E = args.envs or 2048
     T = 16
     N = T * E
-    ref_batch, ref_ring, ref_acm_bs, acm_epochs, acm_freq = 2000, 110_000, 64, 5, 3
+    ref_batch, ref_ring, ref_acm_bs, ref_ppo_mb, acm_epochs, acm_freq = 2000, 110_000, 64, 512, 5, 3
     # N > 1: the ACM ring is replicated (every rank holds every rank's rows, spprl/ppo_acm.py), so the ACM
     # cadence is scaled by the frames of all ranks
     rw = args.rehearse_world or 0  # (one-GPU rehearsal of a rw-rank job's per-rank work)
     wj = max(world, rw)  # ranks of the job whose cadence is run
     scale = wj * N / ref_batch
     acm_bs = int(round(ref_acm_bs * scale))
+    # the actor's minibatch follows the same rule (ppo.py:158-188: ppo_batch_size = 512 against 2000 frames, ~4
+    # sequential clip-loss steps per epoch): 512 * s, so every sample count of the iteration scales by s alike
+    ppo_mb = args.ppo_minibatch or int(round(ref_ppo_mb * scale))
     seed = shard_seed(1000, rank)
     ag = spprl.PPO_AcM(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=3e-4, critic_lr=3e-4, batch_size=N,
-                       ppo_batch_size=512, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
+                       ppo_batch_size=ppo_mb, kl_div_threshold=0.1, max_ppo_epochs=10, entropy_coef=0.0,
                        custom_loss=0.1, norm_closs=True, min_max_denormalize=True, denormalize_actor_out=True,
                        acm_epochs=acm_epochs, acm_batch_size=acm_bs, acm_update_freq=acm_freq, acm_lr=3e-4,
                        acm_ring_size=int(round(ref_ring * scale)), n_envs=E, device=dev, seed=0, loop_seed=seed,
-                       rehearse_world=rw or None)
+                       rehearse_world=rw or None, dp_update=args.ppo_dp, comm=comm)
     rb = ag.replay_buffer
     ob, ac = ag.ob_dim, ag.ac_dim
     sigma = acm_epochs * rb.size / (acm_freq * N * wj)
@@ -526,28 +536,38 @@ def bench_ppo(args, world, rank, dev):
                       "steps_per_iteration": T, "frames_per_iteration": N, "cadence_scale": round(scale, 4),
                       "acm_ring": rb.size, "acm_batch": acm_bs, "acm_epochs_every_3_iterations": acm_epochs,
                       "acm_sigma": round(sigma, 3), "acm_updates_timed": epochs["acm_updates"],
-                      "ppo_epochs_timed": epochs["ppo"], "ppo_minibatch": 512,
+                      "ppo_epochs_timed": epochs["ppo"], "ppo_minibatch": ppo_mb,
                       "flop_per_env_step": round(per_env_step), "parallelism": "dp%d" % world,
                       "cadence": "reference train/spp_ppo_hcheetah.py per iteration with every sample count x "
-                                 "N/2000 (critic full batch N, ACM ring 1.1e5*s, ACM batch 64*s); sigma = ACM "
-                                 "samples per env-step (reference 91.67)"},
+                                 "s = world*N/2000 (critic full batch N, PPO minibatch 512*s, ACM ring 1.1e5*s, "
+                                 "ACM batch 64*s): the reference's sequential step counts per iteration (~4 clip-loss "
+                                 "steps per epoch, 1719 ACM steps per epoch); sigma = ACM samples per env-step "
+                                 "(reference 91.67)"},
            "roofline": {"bound": "mfma", "kernel": "whole iteration (64-wide MLPs, latency-bound chain of "
                                                     "dependent optimizer steps)",
                         "achieved": round(flop / elapsed / 1e12, 4), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": None, "traffic": None,
                         "note": "achieved = the timed iterations' algorithmic FLOPs (critic, actor epochs run, ACM, "
-                                "rollout: SURVEY §8d) / elapsed; 5 x 1719 sequential ACM steps every 3 iterations and "
-                                "~64 sequential 512-sample actor steps per epoch bound the iteration by latency"},
+                                "rollout: SURVEY §8d) / elapsed; 5 x 1719 sequential ACM steps every 3 iterations "
+                                "bound the iteration by latency"},
            "losses": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in ag.loss.items()}}
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / PEAK_FP32_MFMA_TFLOPS, 5)
-    if ag.dp:
+    if ag.dp and ag.dp_update == "union":
         res["config"]["update_batch"] = ("union of %d ranks' rollouts, %d rows, replicated on every rank (one "
                                          "all-gather per iteration; no per-step gradient exchange)" % (wj, wj * N))
+    elif ag.dp:
+        res["config"]["update_batch"] = ("sharded: each rank's own %d rows, one gradient all-reduce per critic step "
+                                         "and per clip-loss step (minibatch %d per rank = %d / %d), %s" % (
+                                             N, ppo_mb // wj, ppo_mb, wj,
+                                             "libspprl RCCL on the compute stream" if comm else "torch.distributed"))
     if rw:
-        res["config"]["rehearsal"] = ("one GPU running the per-rank work of a %d-rank job: ACM ring / batch scaled "
-                                      "for %d ranks, update(mem) on the local rollout tiled to the %d-rank union "
-                                      "shape; value = %d x this GPU's env-steps/s (a projection, not a "
-                                      "multi-GPU measurement)" % (rw, rw, rw, rw))
+        res["config"]["rehearsal"] = (
+            "one GPU running the per-rank work of a %d-rank job: ACM ring / batch scaled for %d ranks and the "
+            "replicated ring written with %d ranks' rows per iteration; %s; value = %d x this GPU's env-steps/s (a "
+            "projection, not a multi-GPU measurement: the per-step all-reduces run on a one-rank communicator, so "
+            "their 8-GPU latency is not in it)" % (
+                rw, rw, rw, "update(mem) on the local rollout tiled to the %d-rank union shape" % rw
+                if ag.dp_update == "union" else "update(mem) on the local rollout with the per-step exchange", rw))
     if world > 1:  # the replicas must stay bit-identical (identical union batch, ring and permutation streams)
         chk = torch.stack([t.double().sum() for t in (ag.nets.params[0], ag.nets.params[1], ag.acm.params[5])] +
                           [t.double().abs().sum() for t in (ag.nets.params[0], ag.nets.params[1],
@@ -751,6 +771,9 @@ def main():
     backend = os.environ.get("SPP_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
+    if args.config == "ppo_hcheetah" and (args.rehearse_world or 0) > 1 and args.ppo_dp == "shard":
+        # a sharded update's per-rank work includes its per-step exchange: rehearsed on a one-rank communicator
+        os.environ["SPP_DP_FORCE"] = "1"
     # SPP_DP_FORCE=1 (rehearsal): the process group and the exchange also run with one rank
     distributed = world > 1 or os.environ.get("SPP_DP_FORCE", "0") == "1"
     if distributed:
@@ -763,7 +786,10 @@ def main():
     torch.cuda.set_device(dev)
 
     if args.config == "ppo_hcheetah":
-        return bench_ppo(args, world, rank, dev)
+        comm = None
+        if distributed and backend == "nccl" and args.dp_comm == "native":
+            comm = native_comm(world, rank, local)
+        return bench_ppo(args, world, rank, dev, comm)
     import spprl
     from spprl import flops
     from spprl.dp import shard_seed

@@ -257,8 +257,10 @@ sppStatus sppAgentStageFromReplay(sppAgentHandle h, sppReplayHandle r, const int
                                   void* stream);
 /* The rest of sample_batch / make_update on the staged batch, in place:
  *   normalize          obs and next_obs through the bound normaliser (ReplayBuffer._sample_batch with
- *                      obs_norm, rltoolkit/buffer/replay_buffer.py:247-249; min-max or z-score per the
- *                      agent's min_max_denormalize, memory.py:76-88)
+ *                      obs_norm, rltoolkit/buffer/replay_buffer.py:247-249): 1 = min-max or z-score per the
+ *                      agent's min_max_denormalize (memory.py:76-88), 2 = z-score with the bound mean / std
+ *                      whatever that flag (vanilla SAC's plain ReplayBuffer, whose MemoryMeta keeps
+ *                      min_max_denormalize False: sac.py via ddpg.py:107-115)
  *   act_from_next_obs  the critic's action operand := the (normalised) next obs
  *                      (DDPG_AcM.make_unbiased_update, rltoolkit/acm/off_policy/ddpg_acm.py:59-73:
  *                      update(action=next_obs)); needs acm_critic = 0 and aout == ob. */
@@ -338,10 +340,16 @@ sppStatus sppAcmSgdStatusAsync(sppAgentHandle h, int* timed_out_pinned, void* st
 /* Largest bs sppAcmSgd accepts on this device for this agent: every workgroup of a step must be resident
  * at once (the arrival barrier), so min(32768, 64 x occupancy x CUs).  Larger batches: SPP_E_SHAPE. */
 int sppAcmSgdMaxBatch(sppAgentHandle h);
-/* Co-resident workgroups (one per CU) one sppAcmSgd / sppAcmSgdEpoch step of bs rows runs on: 1 for bs <= 64
- * (4 waves), else max(2, ceil(bs / 128)) (8 waves, two per SIMD); 0 for handles without the AcM kernel. */
+/* Co-resident workgroups (one per CU) one sppAcmSgd / sppAcmSgdEpoch step of bs rows runs on: 1 for bs <= 64,
+ * else max(2, ceil(bs / 64)) workgroups of 4 waves (17 at bs = 1,049); 0 for handles without the AcM kernel.
+ * (A library built with -DSPP_ACM_WV=8, the 8-wave A/B variant, returns max(2, ceil(bs / 128)).) */
 int sppAcmSgdWorkgroups(sppAgentHandle h, int bs);
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx_dev, int B, float* x, float* y, void* stream);
+/* AcMTrainer(acm_ob_idx=...) (acm.py:94-99, 148, 260-264): sppReplayGatherAcm then writes
+ * x = [obs[:, cols] | next_obs[:, cols]].  n = ob index entries (a permutation or any list of ob columns, each
+ * in [0, ob)), or n = 0 for the identity (the default).  Lists of another length are refused: the reference's
+ * AcM takes ob + n inputs (acm.py:148) while acm_cat gives it 2n, so only n = ob runs there.  Synchronous. */
+sppStatus sppReplaySetAcmColumns(sppReplayHandle h, const int* cols_host, int n);
 
 /* Per-kernel device timing (HIP events on the launch stream), for measurement:
  * kinds 0 critic-phase, 1 actor-phase, 2 weight-grad GEMMs, 3 Adam, 4 ACM regression.

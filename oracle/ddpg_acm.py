@@ -83,18 +83,21 @@ class OracleDdpgAcm:
         return nets.flatten(self.p[k]).numpy()
 
 
-def make_unbiased_update(oracle, ring, B, grad_steps, mt, norm=None):
+def make_unbiased_update(oracle, ring, B, grad_steps, mt, norm=None, eps=None):
     """DDPG_AcM.make_unbiased_update (acm/off_policy/ddpg_acm.py:59-73): grad_steps batches of
     sample_batch (replay_buffer.py:233-261, 385-398; with obs_norm the buffer normalises obs and next obs,
     :247-249), each updated with action = next_obs.  ``ring`` is an OracleReplay, ``mt`` its index stream,
-    ``norm`` the buffer's normaliser when obs_norm (None: raw obs).  Returns the last step's losses and the
-    sampled indices [grad_steps][B]."""
+    ``norm`` the buffer's normaliser when obs_norm (None: raw obs); ``eps`` (SAC_AcM, which inherits this
+    make_update: sac_acm.py:12) the rsample draws of each update in call order, [2 grad_steps][B][aout].  Returns
+    the last step's losses and the sampled indices [grad_steps][B]."""
     losses, idxs = None, []
     for _ in range(grad_steps):
         (obs, next_obs, _, rew, done, acm), idx = ring.sample_batch(B, mt)
         if norm is not None:
             obs = norm.normalize(torch.from_numpy(obs)).numpy()
             next_obs = norm.normalize(torch.from_numpy(next_obs)).numpy()
-        losses = oracle.update(obs, next_obs, next_obs, rew, done, acm)
+        k = len(idxs)
+        extra = () if eps is None else (eps[2 * k], eps[2 * k + 1])
+        losses = oracle.update(obs, next_obs, next_obs, rew, done, acm, *extra)
         idxs.append(idx)
     return losses, np.stack(idxs)

@@ -217,7 +217,7 @@ sppStatus sppReplayDestroy(sppReplayHandle h) {
   hipSetDevice(h->device);
   hipDeviceSynchronize();
   ReplayDev& d = h->d;
-  hipFree(d.obs); hipFree(d.obs_idx); hipFree(d.rec);
+  hipFree(d.obs); hipFree(d.obs_idx); hipFree(d.rec); hipFree((void*)d.acm_cols);
   for (int i = 0; i < sppReplay::kRing; ++i) {
     if (h->pinned[i]) hipHostFree(h->pinned[i]);
     if (h->dev_meta[i]) hipFree(h->dev_meta[i]);
@@ -1906,11 +1906,13 @@ sppStatus sppAgentStagePost(sppAgentHandle a, int normalize, int act_from_next_o
   if (!normalize && !act_from_next_obs) return SPP_OK;
   SPP_REQUIRE(!act_from_next_obs || (!a->cfg.acm_critic && a->cfg.aout == a->cfg.ob && a->ACT), SPP_E_INVALID_ARG,
               "stage_post: action = next_obs needs a critic on (obs, actor output) with aout == ob");
-  SPP_REQUIRE(!normalize || (a->cfg.min_max_denormalize ? (a->lo && a->hi) : (a->mean && a->std)), SPP_E_STATE,
+  SPP_REQUIRE(normalize >= 0 && normalize <= 2, SPP_E_INVALID_ARG, "stage_post: normalize %d", normalize);
+  const int mm = normalize == 2 ? 0 : a->cfg.min_max_denormalize;  // 2: z-score whatever the agent's mode
+  SPP_REQUIRE(!normalize || (mm ? (a->lo && a->hi) : (a->mean && a->std)), SPP_E_STATE,
               "stage_post: normalizer not bound");
   const int B = a->cur_B, Bp = (int)round_up(B, 32), ob = a->cfg.ob;
   hipLaunchKernelGGL(k_stage_post, dim3(cdiv((int64_t)ob * B, 256)), dim3(256), 0, S(stream), a->S, a->S2, a->ACT, ob,
-                     B, Bp, a->lo, a->hi, a->mean, a->std, a->cfg.min_max_denormalize, normalize, act_from_next_obs);
+                     B, Bp, a->lo, a->hi, a->mean, a->std, mm, normalize != 0, act_from_next_obs);
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
 }
@@ -2108,6 +2110,24 @@ sppStatus sppAcmRegressStep(sppAgentHandle a, const float* x, const float* y, in
   sppStatus s = sppAcmRegressGrads(a, x, y, B, loss, stream);
   if (s) return s;
   return sppAcmRegressApply(a, stream);
+}
+
+sppStatus sppReplaySetAcmColumns(sppReplayHandle h, const int* cols, int n) {
+  SPP_REQUIRE(h && (n == 0 || (cols && n == h->d.ob)), SPP_E_INVALID_ARG,
+              "acm columns: %d columns for ob = %d (acm_cat feeds the AcM 2 x len(acm_ob_idx) inputs, which it takes "
+              "only when len(acm_ob_idx) = ob)", n, h ? h->d.ob : 0);
+  for (int i = 0; i < n; ++i)
+    SPP_REQUIRE(cols[i] >= 0 && cols[i] < h->d.ob, SPP_E_INVALID_ARG, "acm columns: index %d out of range", cols[i]);
+  SPP_CHECK_HIP(hipSetDevice(h->device));
+  SPP_CHECK_HIP(hipDeviceSynchronize());  // (a gather in flight may still read the old map)
+  SPP_CHECK_HIP(hipFree((void*)h->d.acm_cols));
+  h->d.acm_cols = nullptr;
+  if (n == 0) return SPP_OK;
+  int* d = nullptr;
+  SPP_CHECK_HIP(hipMalloc(&d, sizeof(int) * n));
+  SPP_CHECK_HIP(hipMemcpy(d, cols, sizeof(int) * n, hipMemcpyHostToDevice));
+  h->d.acm_cols = d;
+  return SPP_OK;
 }
 
 sppStatus sppReplayGatherAcm(sppReplayHandle h, const int64_t* idx, int B, float* x, float* y, void* stream) {

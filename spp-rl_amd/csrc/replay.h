@@ -21,6 +21,7 @@ struct ReplayDev {
   int64_t cap;
   int ob, aout, ac;
   int rw;            // record words: 4 + ac + aout rounded up to 16 (a multiple of 64 B)
+  const int* acm_cols;  // AcMTrainer.acm_ob_idx (acm.py:94-99, 260-264): the ob columns of acm_cat, or null
 };
 constexpr int kRecAcm = 4;  // first ACM word
 __host__ __device__ inline int rec_words(int aout, int ac) { return (kRecAcm + ac + aout + 15) / 16 * 16; }

@@ -254,8 +254,9 @@ __global__ __launch_bounds__(1024) void k_replay_last_rollout(const uint32_t* __
 }
 
 // rbuffer_sample_acm (:404-430) + AcMTrainer.acm_cat (acm.py:260-264): row-major
-// x[b] = [obs | next_obs], y[b] = acm action; kStageTile samples per workgroup,
-// consecutive lanes read and write consecutive floats of one row.
+// x[b] = [obs[:, acm_ob_idx] | next_obs[:, acm_ob_idx]] (the identity when r.acm_cols is null),
+// y[b] = acm action; kStageTile samples per workgroup, consecutive lanes read and write
+// consecutive floats of one row.
 __global__ __launch_bounds__(256) void k_replay_gather_acm(ReplayDev r, const int64_t* __restrict__ idx, int B,
                                                            float* x, float* y) {
   __shared__ int64_t rt[kStageTile], ro[kStageTile], rn[kStageTile];
@@ -272,7 +273,9 @@ __global__ __launch_bounds__(256) void k_replay_gather_acm(ReplayDev r, const in
   const int ob = r.ob, w = 2 * ob;
   for (int i = threadIdx.x; i < valid * w; i += blockDim.x) {
     const int s = i / w, f = i - s * w;
-    x[(b0 + s) * w + f] = f < ob ? r.obs[ro[s] * ob + f] : r.obs[rn[s] * ob + (f - ob)];
+    const int c = f < ob ? f : f - ob;
+    const int col = r.acm_cols ? r.acm_cols[c] : c;
+    x[(b0 + s) * w + f] = r.obs[(f < ob ? ro[s] : rn[s]) * ob + col];
   }
   for (int i = threadIdx.x; i < valid * r.ac; i += blockDim.x) {
     const int s = i / r.ac, f = i - s * r.ac;

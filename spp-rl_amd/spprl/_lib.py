@@ -111,6 +111,7 @@ _SIGS = {
     "sppAcmRegressGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "sppAcmRegressApply": (c_int, [c_void_p, c_void_p]),
     "sppReplayGatherAcm": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "sppReplaySetAcmColumns": (c_int, [c_void_p, c_void_p, c_int]),
     "sppAgentSetTiming": (c_int, [c_void_p, c_int]),
     "sppAgentGetTiming": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppSynthEnvStep": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

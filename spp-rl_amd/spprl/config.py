@@ -89,3 +89,21 @@ def default_max_batch(update_batch_size, kw):
     if E > 1 and kw.get("schedule", "fused") == "fused":
         out = max(out, int(round(rho * E)), int(round(sigma * E)))
     return out
+
+
+def acm_columns(acm_ob_idx, ob):
+    """AcMTrainer's acm_ob_idx (acm/acm.py:94-99): None for the whole observation vector, else the list of ob
+    columns acm_cat takes from obs and next_obs (acm.py:260-264).  The reference builds the AcM with ob +
+    len(acm_ob_idx) inputs (acm.py:148) but feeds it 2 * len(acm_ob_idx) (acm_cat), so only lists of length ob
+    (a permutation, or repeats) run there; shorter lists fail at the first ACM update in the reference and are
+    refused here at construction.  Returns None (identity) or the list."""
+    if acm_ob_idx is None:
+        return None
+    cols = [int(i) for i in acm_ob_idx]
+    if any(i < 0 or i >= ob for i in cols):
+        raise ValueError("acm_ob_idx out of range for ob_dim %d: %r" % (ob, cols))  # (acm.py:98-99 asserts)
+    if len(cols) != ob:
+        raise ValueError("acm_ob_idx of length %d with ob_dim %d: the reference's AcM takes ob + %d inputs "
+                         "(acm/acm.py:148) but acm_cat gives it 2 x %d (acm.py:260-264), so only length-ob lists "
+                         "run in the reference" % (len(cols), ob, len(cols), len(cols)))
+    return None if cols == list(range(ob)) else cols

@@ -29,7 +29,7 @@ class DDPG_AcM(OffPolicyLoop):
                  acm_critic=config.ACM_CRITIC, custom_loss=0.0, norm_closs=config.NORM_CLOSS,
                  min_max_denormalize=config.MIN_MAX_DENORMALIZE, denormalize_actor_out=config.DENORMALIZE_ACTOR_OUT,
                  obs_norm=config.OBS_NORM, max_batch=None, device="cuda", env_spec=None, seed=None,
-                 unbiased_update=False, **loop_kw):
+                 unbiased_update=False, acm_ob_idx=None, **loop_kw):
         self._check_kwargs(loop_kw)
         _lib.load()
         ob, ac, ac_high, _ = env_spec or config.ENV_SPECS[env_name]
@@ -87,6 +87,10 @@ class DDPG_AcM(OffPolicyLoop):
                                                 n_envs=int(loop_kw.get("n_envs", 1)))
         rb = self.replay_buffer
         call("sppAgentBindNormalizer", self._h, ptr(rb.min_obs), ptr(rb.max_obs), ptr(rb.obs_mean), ptr(rb.obs_std))
+        self.acm_ob_idx = list(range(ob)) if acm_ob_idx is None else [int(i) for i in acm_ob_idx]
+        cols = config.acm_columns(acm_ob_idx, ob)  # AcMTrainer's acm_ob_idx (acm.py:94-99, 260-264)
+        if cols is not None:
+            rb.set_acm_columns(cols)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
         self.acm_kind = "basic"  # BasicAcM: per-step regression path
         self._init_loop(update_batch_size=update_batch_size, **loop_kw)

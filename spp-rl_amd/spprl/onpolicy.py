@@ -82,6 +82,7 @@ class OnPolicyNets:
 
         self.allreduce, self.allreduce_sum = make_allreduce(), make_allreduce_sum()
         self.world = torch.distributed.get_world_size() if self.allreduce is not None else 1
+        self.shards = self.world  # ranks the global minibatch ppo_batch_size is split over
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -177,7 +178,7 @@ class OnPolicyNets:
         kl, i = 0.0, 0
         sums = torch.zeros(4, device=self.device)
         self.last_epochs = 0
-        mb = max(1, self.ppo_batch_size // self.world)  # global minibatch = ppo_batch_size
+        mb = max(1, self.ppo_batch_size // self.shards)  # global minibatch = ppo_batch_size
         one_launch = self._epoch_kernel_ok(mb)
         # One-launch epochs keep the device busy across the epoch loop's one host round trip (the KL early stop):
         # the epoch's KL goes to pinned memory by an async copy behind the launch, and the next epoch's permutation

@@ -48,12 +48,15 @@ class PPO_AcM:
                  iterations=1001,
                  stats_freq=1, test_episodes=None, return_done=None, max_frames=None, n_envs=1, env=None,
                  env_spec=None, device="cuda", seed=None, loop_seed=0, epsilon=None, obs_norm=False,
-                 rehearse_world=None, **unused):
+                 rehearse_world=None, dp_update=None, comm=None, acm_ob_idx=None, **unused):
         # unknown keywords raise (the reference's MetaLearner takes no **kwargs, rl.py:17-26); `epsilon` is the
         # reference's name of the clip range (PPO.__init__, ppo.py:17), ppo_epsilon this class's older one
         config.check_kwargs("PPO_AcM", unused, config.ON_POLICY_NO_EFFECT_KWARGS)
-        if obs_norm:
-            raise NotImplementedError("PPO_AcM with obs_norm=True (a normalised ACM ring) is not on the device path")
+        # obs_norm only sets ReplayBufferAcM.obs_norm (acm.py:127-139), read by the ring's normalize() and
+        # _sample_batch (replay_buffer.py:77-81, 246-249), neither of which the on-policy loop calls: the rollout
+        # normalises through its own Memory (a2c.py:165, on_policy.py:107-112) and the ACM trains on raw ring rows
+        # (acm.py:273-282, replay_buffer.py:404-430).  Accepted; it changes nothing computed.
+        self.obs_norm = bool(obs_norm)
         if epsilon is not None:
             ppo_epsilon = epsilon
         ob, ac, ac_high, max_ep = env_spec or config.ENV_SPECS[env_name]
@@ -84,14 +87,24 @@ class PPO_AcM:
         # times -- the shape, and so the per-rank work, of a W-rank job's union batch -- with no collective
         self.rehearse_world = int(rehearse_world or 0)
         dp_world = max(dp_world, self.rehearse_world)
+        # data parallel update (dp_update): "shard" -- each rank updates on its own rollout with one gradient
+        # all-reduce per critic / actor step (the reference's per-step losses are batch means, so equal shards
+        # average to the union's gradient); "union" -- one all-gather of the rollouts per iteration and every rank
+        # runs the whole update on the union (no per-step exchange, replicas equal one process on the union)
+        import os
+
+        self.dp_update = dp_update or os.environ.get("SPP_PPO_DP_UPDATE", "shard")
+        if self.dp_update not in ("shard", "union"):
+            raise ValueError("dp_update must be 'shard' or 'union', got %r" % (self.dp_update,))
         self.nets = OnPolicyNets(ob, ob, ac_lim=lim, actor_lr=actor_lr, critic_lr=critic_lr, ppo_epsilon=ppo_epsilon,
                                  entropy_coef=entropy_coef, gamma=gamma, gae_lambda=gae_lambda,
                                  critic_num_target_updates=critic_num_target_updates,
                                  num_critic_updates_per_target=num_critic_updates_per_target,
                                  max_ppo_epochs=max_ppo_epochs, ppo_batch_size=ppo_batch_size,
                                  kl_div_threshold=kl_div_threshold, normalize_adv=normalize_adv,
-                                 max_batch=max(dp_world * Nmax, ppo_batch_size), device=self.device, seed=seed,
-                                 custom_loss=custom_loss)
+                                 max_batch=max((dp_world if self.dp_update == "union" else 1) * Nmax,
+                                               ppo_batch_size),
+                                 device=self.device, seed=seed, custom_loss=custom_loss)
         # the AcM and its replay ring (acm.py:127-141: size = pre-train samples * 1.1)
         ring = int(acm_ring_size or acm_pre_train_samples * 1.1)
         self.acm = SAC_AcM(env_name=env_name, env_spec=(ob, ac, ac_high, max_ep), acm_lr=acm_lr, buffer_size=ring,
@@ -101,7 +114,7 @@ class PPO_AcM:
                            acm_update_batches=acm_update_batches, acm_pre_train_samples=acm_pre_train_samples,
                            acm_pre_train_epochs=acm_pre_train_epochs, acm_scheduler_step=acm_scheduler_step,
                            acm_scheduler_gamma=acm_scheduler_gamma, acm_keep_pretrain=acm_keep_pretrain,
-                           loop_seed=loop_seed + 17)
+                           acm_ob_idx=acm_ob_idx, loop_seed=loop_seed + 17)
         self.replay_buffer = self.acm.replay_buffer
         # Data parallel: the ACM ring is REPLICATED (every rank writes every rank's transitions, in rank
         # order, at the end of each iteration: ReplayBufferAcM.add_buffer, replay_buffer.py:284-297), so the
@@ -116,8 +129,20 @@ class PPO_AcM:
         self.dp = self.nets.allreduce is not None or self.rehearse_world > 1
         self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
         self.rank = dist.get_rank() if self.world > 1 else 0
-        self.nets.allreduce = self.nets.allreduce_sum = None  # (the nets see the union: no per-step exchange)
-        self.nets.world = 1
+        if self.dp_update == "union":
+            self.nets.allreduce = self.nets.allreduce_sum = None  # (the nets see the union: no per-step exchange)
+            self.nets.world = 1
+        else:
+            if comm is not None and self.nets.allreduce is not None:  # the per-step exchange on the compute stream
+                inv = 1.0 / comm.world
+
+                def allreduce(t):
+                    comm.allreduce_sum(t)
+                    t.mul_(inv)
+
+                self.nets.allreduce, self.nets.allreduce_sum = allreduce, comm.allreduce_sum
+            # the global minibatch ppo_batch_size is split over the ranks (a rehearsal: over rehearse_world)
+            self.nets.shards = max(self.world, self.rehearse_world)
         if self.world > 1 and E == 1:
             # one env per rank collects whole episodes: the ranks' ring-write records ("start" per episode)
             # then differ in count and kind, which the rank-major all-gather of _flush_ring cannot carry
@@ -224,7 +249,7 @@ class PPO_AcM:
         next rollout wait for both, as in the reference's order.  The results are the serial order's."""
         self._ret_sums.zero_()
         mem = self.collect_batch()
-        if self.dp:
+        if self.dp and self.dp_update == "union":
             mem = self._union(mem)  # every rank's rollout, before the ACM's side stream starts
         acm_now = bool(self.acm_update_freq) and self.iteration % self.acm_update_freq == 0
         side = self._acm_side_stream() if acm_now else None
@@ -291,10 +316,12 @@ class PPO_AcM:
             return
         E, ob, ac = self.n_envs, self.ob_dim, self.ac_dim
         W = self.world
+        R = self.rehearse_world if W == 1 and self.rehearse_world > 1 else 1
         if self._prev_all is None:
-            self._prev_all = [None] * W
+            self._prev_all = [None] * max(W, R)
         if W == 1:
-            blocks = [log]
+            # (a rehearsal of R ranks: the replicated ring takes R ranks' writes per iteration -- this rank's R times)
+            blocks = [log] * R
         else:
             import torch.distributed as dist
 
@@ -444,7 +471,7 @@ class PPO_AcM:
     def update(self, mem):
         """critic, GAE, actor on the iteration's batch: this rank's rollout, or (data parallel) the union of every
         rank's (self._union; a caller may pass the union itself)."""
-        if self.dp:
+        if self.dp and self.dp_update == "union":
             mem = self._union(mem)
         T, E, ob = mem["T"], mem.get("E", self.n_envs), self.ob_dim
         N = T * E

@@ -92,6 +92,14 @@ class BufferAcMOffPolicy:
             _lib.load().sppReplayDestroy(h)
             self._h = None
 
+    def set_acm_columns(self, cols):
+        """AcMTrainer.acm_ob_idx (acm.py:94-99, 260-264): the ob columns of acm_cat's obs / next_obs in every ACM
+        gather (sppReplaySetAcmColumns); None restores the whole observation vector."""
+        n = 0 if cols is None else len(cols)
+        arr = np.asarray(cols if cols is not None else [0], np.int32)
+        call("sppReplaySetAcmColumns", self._h, arr.ctypes.data_as(ctypes.c_void_p) if n else None, n)
+        self.acm_cols = None if cols is None else list(cols)
+
     # ------------------------------------------------------------------ state
     def _state(self):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

@@ -54,9 +54,8 @@ class SAC_AcM(OffPolicyLoop):
         self.acm_critic, self.custom_loss, self.norm_closs = bool(acm_critic), float(custom_loss), bool(norm_closs)
         self.unbiased_update = bool(unbiased_update)  # DDPG_AcM.make_update (ddpg_acm.py:59-79), inherited
         self.min_max_denormalize, self.denormalize_actor_out = bool(min_max_denormalize), bool(denormalize_actor_out)
-        self.acm_ob_idx = list(range(ob)) if acm_ob_idx is None else list(acm_ob_idx)
-        if len(self.acm_ob_idx) != ob:
-            raise NotImplementedError("acm_ob_idx subsets are not on the device path")
+        self._acm_cols = config.acm_columns(acm_ob_idx, ob)  # (acm.py:94-99; refuses lists the reference can't run)
+        self.acm_ob_idx = list(range(ob)) if acm_ob_idx is None else [int(i) for i in acm_ob_idx]
         self.actor_output_dim = ac if vanilla else len(self.acm_ob_idx)
         # acm.py:102-108 actor limit
         if vanilla:
@@ -120,19 +119,24 @@ class SAC_AcM(OffPolicyLoop):
         call("sppAgentBindAlpha", self._h, ptr(self.alpha_state), ptr(self.alpha_f32))
         call("sppAgentBindAlphaGrad", self._h, ptr(self.alpha_grad))
         if vanilla:
-            if obs_norm:
-                raise NotImplementedError("vanilla SAC with obs_norm=True is not on the device path")
-            self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=False,
+            # obs_norm (DDPG.__init__, ddpg.py:101-115): the plain ReplayBuffer normalises sampled obs / next obs
+            # (z-score, replay_buffer.py:246-249) and the rollout's act input (ddpg.py:203); its statistics start
+            # as zeros / ones (replay_buffer.py:113-115), i.e. only the clip, until the first update_obs_mean_std
+            self.replay_buffer = ReplayBuffer(buffer_size, ob, ac, device=self.device, obs_norm=bool(obs_norm),
                                               n_envs=int(loop_kw.get("n_envs", 1)))
-            # identity denormalisation of the actor output: min-max over [-1, 1] is 0 + x * 1, exact
-            self._ident = torch.stack([-torch.ones(ob), torch.ones(ob), torch.zeros(ob), torch.ones(ob)]).to(self.device)
-            call("sppAgentBindNormalizer", self._h, ptr(self._ident[0]), ptr(self._ident[1]), ptr(self._ident[2]),
-                 ptr(self._ident[3]))
+            # identity denormalisation of the actor output: min-max over [-1, 1] is 0 + x * 1, exact; the z-score
+            # pair is the ring's own statistics (the staged batch's obs_norm normalisation, sppAgentStagePost 2)
+            self._ident = torch.stack([-torch.ones(ob), torch.ones(ob)]).to(self.device)
+            rb = self.replay_buffer
+            call("sppAgentBindNormalizer", self._h, ptr(self._ident[0]), ptr(self._ident[1]), ptr(rb.obs_mean),
+                 ptr(rb.obs_std))
         else:
             self.replay_buffer = BufferAcMOffPolicy(buffer_size, ob, aout, ac, device=self.device,
                                                     min_max_denormalize=self.min_max_denormalize, obs_norm=obs_norm,
                                                     n_envs=int(loop_kw.get("n_envs", 1)))
             self.bind_normalizer(self.replay_buffer)
+            if self._acm_cols is not None:
+                self.replay_buffer.set_acm_columns(self._acm_cols)
         self._losses = torch.zeros(_lib.NUM_LOSSES, device=self.device)
         self._init_loop(update_batch_size=update_batch_size, **loop_kw)
 

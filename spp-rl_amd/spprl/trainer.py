@@ -608,6 +608,8 @@ class OffPolicyLoop:
         rb = self.replay_buffer
         call("sppAgentStageFromReplay", self._h, rb._h, ptr(idx), idx.numel(), st)
         norm = bool(rb.obs_norm) and not (rb.min_max_denormalize and not rb._have_minmax)  # normalize() no-ops
+        if norm and not rb.HAS_ACM:  # the plain ReplayBuffer (vanilla SAC): z-score (zeros / ones before any stats)
+            norm = 2
         unbiased = bool(getattr(self, "unbiased_update", False)) and not self.acm_critic  # acm_critic: acm_action
         if norm or unbiased:
             call("sppAgentStagePost", self._h, int(norm), int(unbiased), st)

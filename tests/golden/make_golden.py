@@ -469,6 +469,75 @@ def gen_sac_vanilla(seed=41, B=100, steps=2):
     save("sac_vanilla_hcheetah.npz", **out)
 
 
+def gen_sac_vanilla_obsnorm(seed=43):
+    """Vanilla SAC with obs_norm=True (configs[0]'s algorithm; DDPG.__init__ ddpg.py:101-115 gives the plain
+    ReplayBuffer obs_norm): make_update (ddpg.py:231-237) over two cadences of the ring -- the first with the
+    buffer's initial zeros / ones statistics (replay_buffer.py:113-115: only the +-10 clip, some obs beyond it),
+    the second after update_obs_mean_std (rl.py:93-112, replay_buffer.py:83-96) -- each sample_batch z-scored
+    (replay_buffer.py:246-249); rsample draws injected and stored."""
+    torch.manual_seed(0)
+    size, B, gsteps, ufreq = 400, 40, 2, 10
+    m = SAC(env_name="HalfCheetah-v2", gamma=0.99, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3, alpha=0.2,
+            buffer_size=size, update_batch_size=B, grad_steps=gsteps, update_freq=ufreq, obs_norm=True,
+            use_gpu=False)
+    ob, ac = m.ob_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic_1": m._critic_1, "critic_2": m._critic_2,
+            "critic_1_targ": m.critic_1_targ, "critic_2_targ": m.critic_2_targ}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    buf = m.replay_buffer
+    assert buf.obs_norm and not buf.min_max_denormalize
+    ops, obs_log, act_log, rew_log, done_log, end_log = [], [], [], [], [], []
+    scale = (rng.uniform(0.5, 14.0, ob) * np.where(rng.rand(ob) < 0.5, -1, 1)).astype(np.float32)
+    for L in rng.randint(5, 40, 9):  # ragged episodes, no wrap; columns of very different scales (some > 10)
+        o = (rng.randn(1, ob) * scale + scale).astype(np.float32)
+        prev = buf.add_obs(torch.from_numpy(o))
+        obs_log.append(o[0])
+        ops.append((0, prev, -1))
+        for t in range(L):
+            a = torch.from_numpy(rng.uniform(-1, 1, (1, ac)).astype(np.float32))
+            o = (rng.randn(1, ob) * scale + scale).astype(np.float32)
+            nxt = buf.add_obs(torch.from_numpy(o))
+            r = float(rng.randn())
+            end = t == L - 1
+            done = bool(end and rng.rand() < 0.5)
+            buf.add_timestep(prev, nxt, a, r, done, end)
+            ops.append((1, prev, nxt))
+            obs_log.append(o[0])
+            act_log.append(a.numpy()[0])
+            rew_log.append(r)
+            done_log.append(done)
+            end_log.append(end)
+            prev = nxt
+    out = dict(dims=np.array([ob, ac, B, gsteps, ufreq, size]), seed=np.array(seed), alpha0=np.array(m.alpha),
+               target_entropy=np.array(m.target_entropy), tau=np.array(m.tau), gamma=np.array(m.gamma),
+               ops=np.array(ops, np.int64), obs=np.array(obs_log, np.float32), act=np.array(act_log, np.float32),
+               rew=np.array(rew_log, np.float32), done=np.array(done_log, np.bool_), end=np.array(end_log, np.bool_))
+    losses, idxs, eps, stats, np_seeds = [], [], [], [], [401, 502]
+    for c, s in enumerate(np_seeds):
+        if c == 1:
+            m.replay_buffer = m.update_obs_mean_std(m.replay_buffer)
+            buf = m.replay_buffer
+        stats.append(np.stack([buf.obs_mean.numpy(), buf.obs_std.numpy()]))
+        m.stats_logger.frames = ufreq * (c + 1)
+        assert m.update_condition()
+        np.random.seed(s)
+        idxs.append(np.stack([np.random.randint(0, len(buf), B) for _ in range(gsteps)]))
+        e = [rng.randn(B, ac).astype(np.float32) for _ in range(2 * gsteps)]
+        eps.append(np.stack(e))
+        EPS.q = list(e)
+        np.random.seed(s)
+        m.make_update()
+        assert not EPS.q
+        losses.append([m.loss[k] for k in ("critic_1", "critic_2", "actor")])
+    out.update(np_seeds=np.array(np_seeds), idx=np.stack(idxs), eps=np.stack(eps), stats=np.stack(stats),
+               losses=np.array(losses), log_alpha=np.array(float(m.log_alpha)), alpha=np.array(m.alpha))
+    for k, mod in nets.items():
+        out["post_" + k] = flat_params(mod)
+    save("sac_vanilla_obsnorm_hcheetah.npz", **out)
+
+
 # ---------------------------------------------------------------- on-policy (A2C / PPO_AcM)
 def onp_batch(rng, N, ob):
     obs = (rng.randn(N, ob) * 1.2).astype(np.float32)
@@ -686,23 +755,9 @@ def gen_interop(seed=61):
 
 
 # ---------------------------------------------------------------- DDPG_AcM.make_update, unbiased_update=True
-def gen_ddpg_unbiased(seed=81):
-    """DDPG_AcM(unbiased_update=True).make_update (acm/off_policy/ddpg_acm.py:59-85) over two update
-    cadences: each samples grad_steps batches from the ring (np.random.randint after np.random.seed) and
-    updates with action = next_obs (normalised: obs_norm=True, z-score).  acm_critic=False, so the critic
-    takes (obs, action) and the unbiased branch changes what it learns; custom_loss with norm_closs."""
-    torch.manual_seed(0)
-    env, size, B, gsteps, ufreq = "HalfCheetah-v2", 400, 40, 2, 10
-    m = DDPG_AcM(env_name=env, unbiased_update=True, gamma=0.97, actor_lr=5e-4, critic_lr=5e-4, buffer_size=size,
-                 acm_pre_train_samples=10, acm_val_buffer_size=None, update_batch_size=B, grad_steps=gsteps,
-                 update_freq=ufreq, custom_loss=0.3, norm_closs=True, acm_critic=False, min_max_denormalize=False,
-                 denormalize_actor_out=True, obs_norm=True, use_gpu=False)
-    ob, aout, ac = m.ob_dim, m.actor_output_dim, m.ac_dim
-    nets = {"actor": m._actor, "critic": m._critic, "actor_targ": m.actor_targ, "critic_targ": m.critic_targ}
-    for i, (k, mod) in enumerate(nets.items()):
-        load(mod, seed * 100 + i)
-    rng = np.random.RandomState(seed)
-    buf = m.replay_buffer
+def unbiased_ring(buf, rng, ob, aout, ac):
+    """The unbiased-update fixtures' ring: z-score statistics, then 9 ragged episodes (no wrap) written through
+    the reference buffer's add_obs / add_acm_action / add_timestep; returns the logged writes."""
     buf.obs_mean = torch.from_numpy((rng.randn(ob) * 0.3).astype(np.float32))
     buf.obs_std = torch.from_numpy(rng.uniform(0.5, 1.5, ob).astype(np.float32))
     ops, obs_log, act_log, acm_log, rew_log, done_log, end_log = [], [], [], [], [], [], []
@@ -729,12 +784,31 @@ def gen_ddpg_unbiased(seed=81):
             done_log.append(done)
             end_log.append(end)
             prev = nxt
+    return dict(norm=np.stack([buf.obs_mean.numpy(), buf.obs_std.numpy()]), ops=np.array(ops, np.int64),
+                obs=np.array(obs_log, np.float32), act=np.array(act_log, np.float32), acm=np.array(acm_log, np.float32),
+                rew=np.array(rew_log, np.float32), done=np.array(done_log, np.bool_), end=np.array(end_log, np.bool_))
+
+
+def gen_ddpg_unbiased(seed=81):
+    """DDPG_AcM(unbiased_update=True).make_update (acm/off_policy/ddpg_acm.py:59-85) over two update
+    cadences: each samples grad_steps batches from the ring (np.random.randint after np.random.seed) and
+    updates with action = next_obs (normalised: obs_norm=True, z-score).  acm_critic=False, so the critic
+    takes (obs, action) and the unbiased branch changes what it learns; custom_loss with norm_closs."""
+    torch.manual_seed(0)
+    env, size, B, gsteps, ufreq = "HalfCheetah-v2", 400, 40, 2, 10
+    m = DDPG_AcM(env_name=env, unbiased_update=True, gamma=0.97, actor_lr=5e-4, critic_lr=5e-4, buffer_size=size,
+                 acm_pre_train_samples=10, acm_val_buffer_size=None, update_batch_size=B, grad_steps=gsteps,
+                 update_freq=ufreq, custom_loss=0.3, norm_closs=True, acm_critic=False, min_max_denormalize=False,
+                 denormalize_actor_out=True, obs_norm=True, use_gpu=False)
+    ob, aout, ac = m.ob_dim, m.actor_output_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic": m._critic, "actor_targ": m.actor_targ, "critic_targ": m.critic_targ}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    buf = m.replay_buffer
     out = dict(dims=np.array([ob, aout, ac, B, gsteps, ufreq, size]), seed=np.array(seed),
-               norm=np.stack([buf.obs_mean.numpy(), buf.obs_std.numpy()]),
-               actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32), tau=np.array(m.tau), gamma=np.array(m.gamma),
-               ops=np.array(ops, np.int64), obs=np.array(obs_log, np.float32), act=np.array(act_log, np.float32),
-               acm=np.array(acm_log, np.float32), rew=np.array(rew_log, np.float32),
-               done=np.array(done_log, np.bool_), end=np.array(end_log, np.bool_))
+               actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32), tau=np.array(m.tau), gamma=np.array(m.gamma))
+    out.update(unbiased_ring(buf, rng, ob, aout, ac))
     m.iteration = 0  # no ACM update in these cadences (ddpg_acm.py:52-57)
     losses, idxs, np_seeds = [], [], [101, 202]
     for c, s in enumerate(np_seeds):
@@ -751,9 +825,56 @@ def gen_ddpg_unbiased(seed=81):
     save("ddpg_unbiased_hcheetah.npz", **out)
 
 
+# ---------------------------------------------------------------- SAC_AcM.make_update, unbiased_update=True
+def gen_sac_unbiased(seed=91):
+    """SAC_AcM(unbiased_update=True).make_update -- DDPG_AcM.make_update inherited (acm/off_policy/ddpg_acm.py:
+    59-85; SAC_AcM(DDPG_AcM), sac_acm.py:12) -- over two update cadences on the unbiased ring: each samples
+    grad_steps batches (np.random.randint after np.random.seed) and updates with action = next_obs (normalised:
+    obs_norm=True, z-score).  acm_critic=False (the critics take (obs, action)), custom_loss with norm_closs; the
+    rsample draws of every update (two per update, in call order) are injected and stored."""
+    torch.manual_seed(0)
+    env, size, B, gsteps, ufreq = "HalfCheetah-v2", 400, 40, 2, 10
+    m = SAC_AcM(env_name=env, unbiased_update=True, gamma=0.97, actor_lr=1e-3, critic_lr=1e-3, alpha_lr=1e-3,
+                alpha=0.2, buffer_size=size, acm_pre_train_samples=10, acm_val_buffer_size=None, update_batch_size=B,
+                grad_steps=gsteps, update_freq=ufreq, custom_loss=0.3, norm_closs=True, acm_critic=False,
+                min_max_denormalize=False, denormalize_actor_out=True, obs_norm=True, use_gpu=False)
+    assert m.unbiased_update
+    ob, aout, ac = m.ob_dim, m.actor_output_dim, m.ac_dim
+    nets = {"actor": m._actor, "critic_1": m._critic_1, "critic_2": m._critic_2,
+            "critic_1_targ": m.critic_1_targ, "critic_2_targ": m.critic_2_targ}
+    for i, (k, mod) in enumerate(nets.items()):
+        load(mod, seed * 100 + i)
+    rng = np.random.RandomState(seed)
+    buf = m.replay_buffer
+    out = dict(dims=np.array([ob, aout, ac, B, gsteps, ufreq, size]), seed=np.array(seed),
+               actor_ac_lim=m.actor_ac_lim.numpy().astype(np.float32), tau=np.array(m.tau), gamma=np.array(m.gamma),
+               alpha0=np.array(m.alpha), target_entropy=np.array(m.target_entropy))
+    out.update(unbiased_ring(buf, rng, ob, aout, ac))
+    m.iteration = 0  # no ACM update in these cadences (ddpg_acm.py:52-57)
+    losses, idxs, eps, np_seeds = [], [], [], [201, 302]
+    for c, s in enumerate(np_seeds):
+        m.stats_logger.frames = ufreq * (c + 1)
+        assert m.update_condition()
+        np.random.seed(s)
+        idxs.append(np.stack([np.random.randint(0, len(buf), B) for _ in range(gsteps)]))
+        e = [rng.randn(B, aout).astype(np.float32) for _ in range(2 * gsteps)]
+        eps.append(np.stack(e))
+        EPS.q = list(e)
+        np.random.seed(s)
+        m.make_update()
+        assert not EPS.q
+        losses.append([m.loss.get(k, 0.0) for k in ("critic_1", "critic_2", "actor", "sac", "dist")])
+    out.update(np_seeds=np.array(np_seeds), idx=np.stack(idxs), eps=np.stack(eps), losses=np.array(losses),
+               log_alpha=np.array(float(m.log_alpha)), alpha=np.array(m.alpha))
+    for k, mod in nets.items():
+        out["post_" + k] = flat_params(mod)
+    save("sac_unbiased_hcheetah.npz", **out)
+
+
 GROUPS = {"interop": gen_interop, "randint": gen_randint, "replay": gen_replay, "ddpg": gen_ddpg, "acm": gen_acm, "ppo": gen_ppo,
           "sac_vanilla": gen_sac_vanilla, "onpolicy": gen_onpolicy, "ppo_epochs": gen_ppo_epochs,
-          "ddpg_unbiased": gen_ddpg_unbiased}
+          "ddpg_unbiased": gen_ddpg_unbiased, "sac_unbiased": gen_sac_unbiased,
+          "sac_vanilla_obsnorm": gen_sac_vanilla_obsnorm}
 
 if __name__ == "__main__":
     which = sys.argv[1:] or list(GROUPS) + ["sac"]

@@ -107,15 +107,21 @@ def normalize_adv_ref(adv):
     return ((a - a.mean()) / (a.std() + 1.2e-7)).numpy()
 
 
-def ddpg_unbiased_case():
-    """DDPG_AcM(unbiased_update=True).make_update fixture (tests/golden/ddpg_unbiased_hcheetah.npz):
-    (fixture, params, norm (z-score), ring ops replayer).  acm_critic=False: critic on (obs, actor output)."""
+def ddpg_unbiased_case(name="ddpg_unbiased_hcheetah"):
+    """DDPG_AcM / SAC_AcM (unbiased_update=True).make_update fixtures (tests/golden/ddpg_unbiased_hcheetah.npz,
+    sac_unbiased_hcheetah.npz): (fixture, params, layouts, norm (z-score), ring ops replayer).  acm_critic=False:
+    critics on (obs, actor output)."""
     from oracle.nets import critic_layout, ddpg_actor_layout
-    fx = load("ddpg_unbiased_hcheetah")
+    fx = load(name)
     ob, aout, ac = (int(v) for v in fx["dims"][:3])
     seed = int(fx["seed"])
-    layouts = {"actor": ddpg_actor_layout(ob, aout), "critic": critic_layout(ob + aout),
-               "actor_targ": ddpg_actor_layout(ob, aout), "critic_targ": critic_layout(ob + aout)}
+    if name.startswith("sac"):
+        layouts = {"actor": nets.sac_actor_layout(ob, aout), "critic_1": critic_layout(ob + aout),
+                   "critic_2": critic_layout(ob + aout), "critic_1_targ": critic_layout(ob + aout),
+                   "critic_2_targ": critic_layout(ob + aout)}
+    else:
+        layouts = {"actor": ddpg_actor_layout(ob, aout), "critic": critic_layout(ob + aout),
+                   "actor_targ": ddpg_actor_layout(ob, aout), "critic_targ": critic_layout(ob + aout)}
     params = {k: fill_params(lay, seed * 100 + i) for i, (k, lay) in enumerate(layouts.items())}
     mu, sd = fx["norm"]
     norm = Norm(False, mean=torch.from_numpy(mu), std=torch.from_numpy(sd))

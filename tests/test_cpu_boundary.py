@@ -130,3 +130,30 @@ def test_c_host_example_compiles_against_the_header():
     r = subprocess.run([gcc, "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-I", os.path.join(repo, "include"),
                         os.path.join(repo, "examples", "c_host", "sac_acm_step.c")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_acm_ob_idx_validation_follows_what_the_reference_can_run():
+    """acm_ob_idx (acm/acm.py:94-99): None and the identity mean the whole vector; a length-ob list (a permutation,
+    repeats allowed) is the column map of acm_cat (acm.py:260-264); other lengths are refused at construction (the
+    reference builds its AcM with ob + k inputs, acm.py:148, and feeds it 2k), as are out-of-range entries."""
+    from spprl.config import acm_columns
+
+    assert acm_columns(None, 5) is None
+    assert acm_columns(range(5), 5) is None
+    assert acm_columns([4, 3, 2, 1, 0], 5) == [4, 3, 2, 1, 0]
+    assert acm_columns([0, 0, 1, 2, 3], 5) == [0, 0, 1, 2, 3]
+    for bad in ([0, 1, 2], [0, 1, 2, 3, 5], [-1, 0, 1, 2, 3]):
+        with pytest.raises(ValueError):
+            acm_columns(bad, 5)
+
+
+def test_acm_columns_are_checked_at_the_boundary(lib_built):
+    """sppReplaySetAcmColumns refuses a map whose length is not ob (or an entry out of range) before touching the
+    device, with the reason in sppGetLastError."""
+    import ctypes
+
+    from spprl import _lib
+
+    lib = _lib.load()
+    cols = (ctypes.c_int * 3)(0, 1, 2)
+    assert lib.sppReplaySetAcmColumns(None, cols, 3) != 0

@@ -24,7 +24,7 @@ E, T = 64, 8
 KW = dict(env_name="HalfCheetah-v2", batch_size=E * T, ppo_batch_size=256, max_ppo_epochs=3, acm_epochs=1,
           acm_batch_size=64, acm_update_freq=0, acm_pre_train_samples=1000, acm_pre_train_epochs=1,
           acm_ring_size=8192, critic_num_target_updates=2, num_critic_updates_per_target=3, kl_div_threshold=1e9,
-          custom_loss=0.1, seed=3)
+          custom_loss=0.1, seed=3, dp_update="union")
 MEM = ("obs", "act", "lp", "rew", "done", "end", "next_obs")
 
 

@@ -379,7 +379,7 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     the oracle's AcMTrainer.batch_update sequence on the same replay batches (acm.py:246-264):
     losses rtol 1e-4; parameters after K Adam steps within 1e-5 * max(1, |p|) except for a
     few lr-sized flips of near-zero-moment coordinates.  bs 700 / 1049 (the PPO bench's scaled
-    ACM batch) run the multi-workgroup form: each step over max(2, ceil(bs/128)) 8-wave workgroups whose gradients
+    ACM batch) run the multi-workgroup form: each step over max(2, ceil(bs/64)) 4-wave workgroups whose gradients
     are summed behind one arrival barrier per step (its timeout flag must stay clear)."""
     ag = _filled_agent(env_name, ob, ac, 2000, seed=4)
     rb = ag.replay_buffer
@@ -414,7 +414,7 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
 def test_acm_sgd_epoch_ragged_last_batch_matches_oracle(bs, nrows):
     """sppAcmSgdEpoch: one update_acm epoch (DataLoader batches of bs, drop_last=False: acm.py:270-297) in
     ONE launch, the ragged last batch included: at 3 x 1049 + 2 rows the last step has 2 rows, so 16 of
-    its 9 workgroups hold none; its loss is that batch's own mean.  Same tolerance as above."""
+    its 17 workgroups hold none; its loss is that batch's own mean.  Same tolerance as above."""
     ag = _filled_agent("HalfCheetah-v2", 17, 6, 4000, seed=8)
     rb = ag.replay_buffer
     params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}

@@ -6,7 +6,9 @@ grad_steps batches and updates with action = next_obs) on the GPU path:
   * the fused (staged) schedule: sppAgentStageFromReplay + sppAgentStagePost (obs normalised in place,
     action := next obs) leaves the same parameters, bit for bit, as the caller-batch update on the explicitly
     gathered, normalised tuples with action = next_obs (DDPG_AcM and SAC_AcM, whose eps draws are read back
-    through sppAgentReadEps)."""
+    through sppAgentReadEps);
+  * SAC_AcM's inherited make_update (sac_acm.py:12) against the reference's own SAC_AcM.make_update
+    (tests/golden/sac_unbiased_hcheetah.npz: the same ring, seeds and injected rsample draws)."""
 import numpy as np
 import pytest
 import torch
@@ -115,3 +117,53 @@ def test_unbiased_staged_update_equals_caller_batch(algo):
         a3.update_from_replay_dp(idx, 77, 5)
     torch.cuda.synchronize()
     assert not torch.equal(a1.params[_lib.SPP_NET_CRITIC1], a3.params[_lib.SPP_NET_CRITIC1])
+
+
+SAC_NAMES = {"actor": _lib.SPP_NET_ACTOR, "critic_1": _lib.SPP_NET_CRITIC1, "critic_2": _lib.SPP_NET_CRITIC2,
+             "critic_1_targ": _lib.SPP_NET_CRITIC1_TARG, "critic_2_targ": _lib.SPP_NET_CRITIC2_TARG}
+
+
+def test_sac_unbiased_make_update_matches_reference_fixture():
+    """The reference cadence of SAC_AcM(unbiased_update=True): make_update's MT19937 index draws, the obs_norm
+    gather and action = next obs, two SAC_AcM updates per cadence, with the reference's rsample draws injected
+    into each update in call order.  Losses rtol 1e-4; parameters within the Adam first-step allowance."""
+    fx, params, _, norm, replay = ddpg_unbiased_case("sac_unbiased_hcheetah")
+    ob, aout, ac, B, gsteps, ufreq, size = (int(v) for v in fx["dims"])
+    ag = spprl.SAC_AcM(env_name="custom", env_spec=(ob, ac, 1.0, 1000), gamma=float(fx["gamma"]), actor_lr=1e-3,
+                       critic_lr=1e-3, alpha_lr=1e-3, alpha=float(fx["alpha0"]), acm_critic=False, custom_loss=0.3,
+                       norm_closs=True, min_max_denormalize=False, denormalize_actor_out=True, obs_norm=True,
+                       unbiased_update=True, update_batch_size=B, grad_steps=gsteps, update_freq=ufreq,
+                       buffer_size=size, max_batch=B, device=DEV, seed=0)
+    assert ag.schedule == "reference" and ag.unbiased_update
+    for k, net in SAC_NAMES.items():
+        ag.load_net(net, params[k])
+    rb = ag.replay_buffer
+    rb.obs_mean.copy_(norm.mean)
+    rb.obs_std.copy_(norm.std)
+    replay(rb.add_obs, rb.add_acm_action, rb.add_timestep)
+    ag.iteration = 0
+    queue = []
+    orig = ag.update
+
+    def update(*batch, **kw):  # the reference's rsample draws, two per update (eps_next, eps_cur)
+        e1, e2 = queue.pop(0), queue.pop(0)
+        return orig(*batch, eps_next=torch.from_numpy(e1).to(DEV), eps_cur=torch.from_numpy(e2).to(DEV), **kw)
+
+    ag.update = update
+    for c, s in enumerate(fx["np_seeds"]):
+        ag.stats_logger.frames = ufreq * (c + 1)
+        queue[:] = list(fx["eps"][c])
+        np.random.seed(int(s))
+        ag.make_update()
+        assert not queue
+        for j, k in enumerate(("critic_1", "critic_2", "actor", "sac", "dist")):
+            assert ag.loss[k] == pytest.approx(float(fx["losses"][c][j]), rel=1e-4, abs=1e-6), (c, k)
+    torch.cuda.synchronize()
+    lr, n = 1e-3, len(fx["np_seeds"]) * gsteps
+    for k, net in SAC_NAMES.items():
+        got = ag.params[net].cpu().numpy()
+        d = np.abs(got - fx["post_" + k])
+        scale = 1.0 if not k.endswith("targ") else float(fx["tau"])
+        assert d.max() <= 2 * n * lr * scale * 1.01 + 1e-6, (k, d.max())
+        assert np.mean(d > 1e-5 * max(scale, 0.05)) < 2e-3, (k, np.mean(d > 1e-5))
+    assert ag.current_alpha() == pytest.approx(float(fx["alpha"]), rel=1e-5)

@@ -149,6 +149,28 @@ def test_ddpg_acm_unbiased_make_update_matches_reference():
     assert np.abs(o2.flat("critic") - fx["post_critic"]).max() > 1e-4
 
 
+def test_sac_acm_unbiased_make_update_matches_reference():
+    """SAC_AcM inherits DDPG_AcM.make_update (sac_acm.py:12, ddpg_acm.py:59-85): the unbiased branch over two
+    cadences of the reference's ring (action = normalised next obs, acm_critic=False, z-score obs_norm), with the
+    reference's injected rsample draws: sampled indices, losses, post-step parameters and alpha."""
+    fx, params, layouts, norm, replay = ddpg_unbiased_case("sac_unbiased_hcheetah")
+    ob, aout, ac, B, gsteps, ufreq, size = (int(v) for v in fx["dims"])
+    rb = OracleReplay(size, ob, aout, ac)
+    replay(rb.add_obs, rb.add_acm_action, rb.add_timestep)
+    params = dict(params, acm={n: np.zeros(s, np.float32) for n, s in nets.acm_layout(2 * ob, ac)})
+    o = OracleSacAcm(ob, aout, ac, acm_critic=False, custom_loss=0.3, norm_closs=True, norm=norm,
+                     actor_lim=fx["actor_ac_lim"], gamma=float(fx["gamma"]), tau=float(fx["tau"]),
+                     alpha=float(fx["alpha0"]), target_entropy=float(fx["target_entropy"]), params=params)
+    for c, s in enumerate(fx["np_seeds"]):
+        losses, idx = make_unbiased_update(o, rb, B, gsteps, OracleMT(int(s)), norm, eps=fx["eps"][c])
+        np.testing.assert_array_equal(idx, fx["idx"][c])
+        np.testing.assert_allclose([losses[k] for k in ("critic_1", "critic_2", "actor", "sac", "dist")],
+                                   fx["losses"][c], rtol=1e-5, atol=1e-7)
+    for k in ("actor", "critic_1", "critic_2", "critic_1_targ", "critic_2_targ"):
+        np.testing.assert_allclose(o.flat(k), fx["post_" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    assert o.alpha == pytest.approx(float(fx["alpha"]), rel=1e-10)
+
+
 def test_acm_batch_update_matches_reference():
     fx = load("acm_step")
     seed = int(fx["seed"])

@@ -128,6 +128,9 @@ def parse():
                     help="ppo_hcheetah data parallel update: each rank on its own rollout with one gradient all-reduce "
                          "per critic / actor step (shard), or one all-gather of the rollouts and the whole update on "
                          "the union on every rank (union, round 5)")
+    ap.add_argument("--acm-passes", type=int, default=None,
+                    help="ppo_hcheetah: 64-row passes per workgroup and step of the persistent ACM SGD "
+                         "(sppSetAcmSgdPasses; default: the library's)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="vanilla_sac_hcheetah: R independent single-env runs (separate processes, seeds i) sharing "
                          "the GPU, timed together -- the layout of the reference's own configs[0] script (a pool of "
@@ -456,6 +459,10 @@ def bench_ppo(args, world, rank, dev, comm=None):
     from spprl import flops
     from spprl.dp import shard_seed
 
+    if args.acm_passes is not None:
+        from spprl import _lib
+
+        _lib.call("sppSetAcmSgdPasses", int(args.acm_passes))
     E = args.envs or 2048
     T = 16
     N = T * E
@@ -776,6 +783,9 @@ def main():
         os.environ["SPP_DP_FORCE"] = "1"
     # SPP_DP_FORCE=1 (rehearsal): the process group and the exchange also run with one rank
     distributed = world > 1 or os.environ.get("SPP_DP_FORCE", "0") == "1"
+    if distributed and "RANK" not in os.environ:  # a one-rank group started without a launcher (rehearsal)
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(_free_port()))
     if distributed:
         torch.cuda.set_device(local)
         if backend == "nccl":

@@ -483,6 +483,11 @@ sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle h, int* timed_out_pinned, void
  * value makes every wait give up at once (a co-residency miss, deterministically): how the tests force the
  * timeout path. */
 sppStatus sppSetSgdSpinLimit(int polls);
+/* Tuning knob of the multi-workgroup AcM SGD (sppAcmSgd / sppAcmSgdEpoch; process-wide): each workgroup takes
+ * `passes` 64-row passes per step, so a step of bs rows runs on max(2, ceil(bs / (64 passes))) workgroups that
+ * meet at its two hand-offs (0 or 1: one pass, the default).  Results are the same up to the gradient's
+ * summation order. */
+sppStatus sppSetAcmSgdPasses(int passes);
 /* A2C.update_critic's inner loop (rltoolkit/algorithms/a2c/a2c.py:186-225): nsteps sequential full-batch
  * steps of 0.5 * mean((q - V(x))^2) + Adam at critic_lr on the same N rows (x [N][ob] normalised obs, q [N]
  * targets), in ONE launch: every workgroup runs ceil(rows / 64) passes of its share of the N rows, the

@@ -960,6 +960,8 @@ static sppStatus build_packs(sppAgent* a) {
       M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, nat(2 * aout), nat(256), blocks_of(2 * aout), 8, &a->actor.Wh, 1);
       M(&a->pj_actor, W2, nullptr, 1 << 30, 256, 1, 0, nat(256), nat(256), 8, 8, &a->actor.W2T, 1);
       M(&a->pj_actor, Wp, Ws, aout, 256, 1, 0, nat(256), pair(aout), 8, (aout + 15) / 16, &a->actor.WhT);
+      if (a->cfg.mlp_bf16)  // the two-tile bf16 critic phase squashes in the heads' epilogue (sac_bf.h)
+        M(&a->pj_actor, Wp, Ws, aout, 256, 0, 0, pair(aout), nat(256), (aout + 15) / 16, 8, &a->actor.WhP, 1);
       a->actor.tb1 = T(b1, 256);
       a->actor.tb2 = T(b2, 256);
       a->actor.tbh = T(bp, aout, bs, aout);
@@ -2000,7 +2002,14 @@ static int mlp_sgd_max_wg(int num_cu) {
 #define SPP_ACM_WV 4
 #endif
 constexpr int kAcmWV = SPP_ACM_WV, kAcmR = 16 * kAcmWV;
-static int acm_sgd_nwg(int bs) { return bs <= kMlR ? 1 : std::max(2, cdiv(bs, kAcmR)); }
+// Passes of kAcmR rows per workgroup and step (sppSetAcmSgdPasses; 0: one): P passes put a step on
+// ceil(bs / (P kAcmR)) workgroups (k_mlp_sgd's MP form).
+static int g_acm_passes = 0;
+static int acm_passes(int bs) {
+  const int P = std::max(1, g_acm_passes);
+  return bs <= kMlR || cdiv(bs, kAcmR) < 2 * P ? 1 : P;  // (>= 2 workgroups after the split)
+}
+static int acm_sgd_nwg(int bs) { return bs <= kMlR ? 1 : std::max(2, cdiv(bs, kAcmR * acm_passes(bs))); }
 static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
   if (a->sgd_max_wg >= 0) return a->sgd_max_wg;
   int n = 0;
@@ -2013,22 +2022,32 @@ static int acm_sgd_max_wg(sppAgentHandle a, int ob, int ac) {
 
 int sppAcmSgdWorkgroups(sppAgentHandle a, int bs) { return (a && !a->ddpg && bs > 0) ? acm_sgd_nwg(bs) : 0; }
 
+sppStatus sppSetAcmSgdPasses(int passes) {
+  SPP_REQUIRE(passes >= 0 && passes <= 16, SPP_E_INVALID_ARG, "acm passes %d", passes);
+  g_acm_passes = passes;
+  return SPP_OK;
+}
+
 int sppAcmSgdMaxBatch(sppAgentHandle a) {
   if (!a || a->ddpg) return 0;
-  return kAcmR * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
+  return kAcmR * std::max(1, g_acm_passes) * std::max(1, acm_sgd_max_wg(a, a->cfg.ob, a->cfg.ac));
 }
 
 // polls before a k_mlp_sgd arrival wait times out (0: the kernel's default); test hook sppSetSgdSpinLimit
 static int g_sgd_spin = 0;
 
 // slabs [2][kMlMaxWG][kMlSlabMax] + the parameter buffer + {arrival counter, timeout flag}
+// sync: [0] unused, [1] the sticky timeout flag, [kSgdShardStride (1 + k)] arrival counter shard k (sgd.hip)
+constexpr int kSgdSyncInts = kSgdShardStride * (1 + kSgdShards);
+static int* sgd_ctr(DevArray<int>& sync) { return sync.ptr + kSgdShardStride; }
 static sppStatus mlp_sgd_buffers(DevArray<float>& slab, DevArray<int>& sync, hipStream_t st) {
   if (!slab.ptr) {
     SPP_CHECK_HIP(slab.alloc((size_t)(2 * kMlMaxWG + 1) * kMlSlabMax));
-    SPP_CHECK_HIP(sync.alloc(2));
-    SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, 2 * sizeof(int), st));
+    SPP_CHECK_HIP(sync.alloc(kSgdSyncInts));
+    SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, kSgdSyncInts * sizeof(int), st));
   }
-  SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, sizeof(int), st));  // the arrival counter (the flag is sticky)
+  // the arrival counter shards (the flag is sticky)
+  SPP_CHECK_HIP(hipMemsetAsync(sgd_ctr(sync), 0, kSgdShards * kSgdShardStride * sizeof(int), st));
   return SPP_OK;
 }
 
@@ -2069,12 +2088,13 @@ static sppStatus acm_sgd_run(sppAgentHandle a, const float* x, const float* y, i
     if (s) return s;
     g.slab = a->sgd_slab.ptr;
     g.pbuf = a->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
-    g.ctr = a->sgd_sync.ptr;
+    g.ctr = sgd_ctr(a->sgd_sync);
     g.err = a->sgd_sync.ptr + 1;
   }
-  const bool mw = nwg > 1;
-#define SPP_SGD_LAUNCH(IN_, AC_)                                                                      \
-  if (mw) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true, kAcmWV>), dim3(nwg), dim3(64 * kAcmWV), 0, st, g);   \
+  const bool mw = nwg > 1, mp = mw && g.bsl > kAcmR;
+#define SPP_SGD_LAUNCH(IN_, AC_)                                                                              \
+  if (mp) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true, kAcmWV, true>), dim3(nwg), dim3(64 * kAcmWV), 0, st, g); \
+  else if (mw) hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, true, kAcmWV>), dim3(nwg), dim3(64 * kAcmWV), 0, st, g); \
   else hipLaunchKernelGGL((k_mlp_sgd<IN_, 32, AC_, 0, false>), dim3(1), dim3(kMlTH), 0, st, g)
   if (ob == 11 && ac == 3) SPP_SGD_LAUNCH(22, 3);
   else if (ob == 17 && ac == 6) SPP_SGD_LAUNCH(34, 6);
@@ -2570,7 +2590,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
     if (s) return s;
     g.slab = o->sgd_slab.ptr;
     g.pbuf = o->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
-    g.ctr = o->sgd_sync.ptr;
+    g.ctr = sgd_ctr(o->sgd_sync);
     g.err = o->sgd_sync.ptr + 1;
   }
   const bool mw = nwg > 1;
@@ -2647,7 +2667,7 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
     if (s) return s;
     g.slab = o->sgd_slab.ptr;
     g.pbuf = o->sgd_slab.ptr + (size_t)2 * kMlMaxWG * kMlSlabMax;
-    g.ctr = o->sgd_sync.ptr;
+    g.ctr = sgd_ctr(o->sgd_sync);
     g.err = o->sgd_sync.ptr + 1;
   }
   const bool mw = nwg > 1;

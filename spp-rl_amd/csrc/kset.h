@@ -3,6 +3,7 @@
 // parallel; api.hip only holds the function pointers.
 #pragma once
 #include "sac.hip"
+#include "sac_bf.h"
 #include "ddpg.hip"
 #include "sac_team.h"
 
@@ -31,7 +32,11 @@ KernelSet make_kset() {
   using C = Cfg<OB, AOUT, AC, ACMC, BF>;
   void (*heads)(SacArgs, AcmScratch) = nullptr;
   if constexpr (C::NB_PAIR > 2) heads = k_sac_actor_heads<C>;
-  return {k_sac_critic_phase<C>, k_sac_actor_phase<C>, heads, k_policy_act<C>, k_acm_regress<C>,
+  void (*critic)(SacArgs) = k_sac_critic_phase<C>;
+#if SPP_BF16_TWO_TILES
+  if constexpr (C::BF && C::ACMC && !C::F3) critic = k_sac_critic_phase2<C>;  // two tiles per wave (sac_bf.h)
+#endif
+  return {critic, k_sac_actor_phase<C>, heads, k_policy_act<C>, k_acm_regress<C>,
           nullptr, nullptr, nullptr, nullptr};
 }
 template <int OB, int AOUT, int AC, bool ACMC>

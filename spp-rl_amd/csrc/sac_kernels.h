@@ -11,6 +11,7 @@ namespace spp {
 struct ActorDev {
   const float4 *W1, *W2, *Wh, *W2T, *WhT;
   int tb1, tb2, tbh;
+  const float4* WhP;  // bf16 sets: the heads in pairing output order (MAP_PAIR, ib-major; k_sac_critic_phase2)
 };
 struct CriticDev {
   const float4 *W1, *W2, *W2T, *W1Ta;

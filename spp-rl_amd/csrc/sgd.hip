@@ -35,6 +35,12 @@ __device__ __forceinline__ float slab_ld1(__amdgpu_buffer_rsrc_t r, int idx) {
 // idle(): work of the workgroup's threads while lane 0 waits for the other workgroups (thread 0 runs it after
 // its poll); it must not touch the handed-over data
 constexpr int kSgdSpins = 1 << 23;
+// The arrival counter is sharded over kSgdShards ints, each on its own 128-B line (ctr[kSgdShardStride k]): a
+// workgroup adds to shard blockIdx % kSgdShards (the XCD it is dealt to under round-robin placement -- speed only,
+// the sum is what is waited for), so the G arrivals of a step meet on 8 lines instead of serialising on one (one
+// device-scope atomic costs ~12 ns at the memory side: MI355X_MICROARCH.md fan-in row), and the poll reads the 8
+// shards at once and waits for their sum.
+constexpr int kSgdShards = 8, kSgdShardStride = 32;
 template <class Idle>
 __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, int spin, Idle&& idle) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores are written through
@@ -43,14 +49,23 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
     int off = 0;
     asm volatile("" : "+v"(off));
     int* c = ctr + off;
-    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(c + kSgdShardStride * (blockIdx.x % kSgdShards), 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (spin < 0) {  // test hook: every wait gives up at once (a co-residency miss, deterministically)
       *s_dead = 1;
       err[off] = 1;
     } else {
       const int limit = spin > 0 ? spin : kSgdSpins;
       int spins = 0;
-      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      while (true) {
+        int v[kSgdShards];
+#pragma unroll
+        for (int k = 0; k < kSgdShards; ++k)
+          v[k] = __hip_atomic_load(c + kSgdShardStride * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < kSgdShards; ++k) sum += v[k];
+        if (sum >= target) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > limit) {
           *s_dead = 1;

@@ -161,14 +161,17 @@ __device__ __forceinline__ void lds_st(uint32_t off, float v) { *(ml_lds_f*)(uin
 
 // WV = 8: two waves per SIMD (128 rows per workgroup, half the workgroups of a step): every latency of one
 // wave's chain (LDS reads, dependent MFMAs, tanh) overlaps the other wave's work; <= 256 registers per wave.
-template <int IN, int H2, int OUT, int HEAD, bool MW, int WV = 4>
+// MP (HEAD 0, G > 1): a step's rows per workgroup may exceed R, run as passes of R rows whose gradients add up in
+// the canonical LDS staging before the exchange (as HEAD 2): fewer workgroups meet at each step's two hand-offs.
+template <int IN, int H2, int OUT, int HEAD, bool MW, int WV = 4, bool MP = false>
 __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
   using C = MlCfg<IN, H2, OUT, HEAD, WV>;
   constexpr int TH = C::TH;
   constexpr bool GAUSS = HEAD == 1, VALUE = HEAD == 2;
+  static_assert(!MP || (MW && HEAD == 0), "passes: the multi-workgroup AcM form");
   // G > 1, one pass per step: every gradient element goes to this workgroup's slab as soon as it is final
   // (write-through stores issued under the remaining tiles' MFMAs), not through the canonical LDS staging
-  constexpr bool DIRECT = MW && !VALUE;
+  constexpr bool DIRECT = MW && !VALUE && !MP;
   static_assert(!VALUE || OUT == 1, "value head");
   constexpr int RS = C::RS, R = C::R, NP = C::NP, SW1 = C::SW1, SW2 = C::SW2, SW3 = C::SW3, NB2 = C::NB2,
                 NO = C::NO;
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     return MW ? max(0, min(a.bsl, step_rows(st) - r0)) : step_rows(st);
   };
   // passes of <= 64 rows: pass p = step p / nsub, rows [64 (p % nsub), +64) of the workgroup's rows
-  const int nsub = (MW && VALUE) ? (a.bsl + R - 1) / R : 1;  // (HEAD 0 / 1: one pass; the host keeps bsl <= 64)
+  const int nsub = (MW && (VALUE || MP)) ? (a.bsl + R - 1) / R : 1;  // (else one pass: the host keeps bsl <= R)
   auto pass_rows = [&](int p) {
     const int st = p / nsub;
     return st < a.nsteps ? max(0, min(R, wg_rows(st) - R * (p - st * nsub))) : 0;
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     SPP_TP(5);
     const auto all = sgd_rsrc(a.slab + (int64_t)(st & 1) * G * C::SLAB);  // (G = 1: unused)
     if constexpr (MW) {
-      if constexpr (!DIRECT)  // (HEAD 2: the passes' sums staged in GR)
+      if constexpr (!DIRECT)  // (HEAD 2, MP: the passes' sums staged in GR)
         for (int f = t; f < C::NP4; f += TH) {
           const float4 v4 = *reinterpret_cast<const float4*>(GR + 4 * f);
           slab_st4(mine, 4 * f, v4);

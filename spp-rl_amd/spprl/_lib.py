@@ -163,6 +163,7 @@ _SIGS = {
     "sppOnpActorEpochStatus": (c_int, [c_void_p, c_void_p]),
     "sppOnpSyncStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppSetSgdSpinLimit": (c_int, [c_int]),
+    "sppSetAcmSgdPasses": (c_int, [c_int]),
     "sppAcmSgdStatusAsync": (c_int, [c_void_p, c_void_p, c_void_p]),
     "sppAcmSgdMaxBatch": (c_int, [c_void_p]),
     "sppAcmSgdWorkgroups": (c_int, [c_void_p, c_int]),

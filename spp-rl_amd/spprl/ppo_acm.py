@@ -131,7 +131,7 @@ class PPO_AcM:
         self.rank = dist.get_rank() if self.world > 1 else 0
         if self.dp_update == "union":
             self.nets.allreduce = self.nets.allreduce_sum = None  # (the nets see the union: no per-step exchange)
-            self.nets.world = 1
+            self.nets.world = self.nets.shards = 1
         else:
             if comm is not None and self.nets.allreduce is not None:  # the per-step exchange on the compute stream
                 inv = 1.0 / comm.world

@@ -410,11 +410,22 @@ def test_acm_persistent_sgd_matches_oracle(env_name, ob, ac, bs):
     assert flag[0] == 0
 
 
-@pytest.mark.parametrize("bs,nrows", [(1049, 3 * 1049 + 2), (700, 2 * 700 + 650), (64, 5 * 64 + 1)])
-def test_acm_sgd_epoch_ragged_last_batch_matches_oracle(bs, nrows):
+@pytest.mark.parametrize("bs,nrows,passes", [(1049, 3 * 1049 + 2, 0), (700, 2 * 700 + 650, 0), (64, 5 * 64 + 1, 0),
+                                             (1049, 3 * 1049 + 2, 2), (2500, 2 * 2500 + 300, 4)])
+def test_acm_sgd_epoch_ragged_last_batch_matches_oracle(bs, nrows, passes):
     """sppAcmSgdEpoch: one update_acm epoch (DataLoader batches of bs, drop_last=False: acm.py:270-297) in
     ONE launch, the ragged last batch included: at 3 x 1049 + 2 rows the last step has 2 rows, so 16 of
-    its 17 workgroups hold none; its loss is that batch's own mean.  Same tolerance as above."""
+    its 17 workgroups hold none; its loss is that batch's own mean.  passes > 0 (sppSetAcmSgdPasses): each
+    workgroup runs that many 64-row passes per step (1049 rows on 9 workgroups, 2500 on 10), summed before the
+    exchange.  Same tolerance as above."""
+    _lib.call("sppSetAcmSgdPasses", passes)
+    try:
+        _acm_epoch_case(bs, nrows)
+    finally:
+        _lib.call("sppSetAcmSgdPasses", 0)
+
+
+def _acm_epoch_case(bs, nrows):
     ag = _filled_agent("HalfCheetah-v2", 17, 6, 4000, seed=8)
     rb = ag.replay_buffer
     params = {k: v.numpy() for k, v in ag.net_state(_lib.SPP_NET_ACM).items()}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library variants (tools/build_variant.py TAG ...): short bench runs per config and variant.
-#   VARIANTS="default ntld ntdw" CONFIGS="sac_ant_bf16 sac_hopper" bash tools/ab_nt.sh
+#   VARIANTS="default ntld ntdw" CONFIGS="sac_ant_bf16 sac_hopper" bash tools/ab/ab_nt.sh
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
 mkdir -p gpurun_out

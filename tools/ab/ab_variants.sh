@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of library variants (tools/build_variant.py TAG ...): short bench runs per config and variant,
 # printing env-steps/s and the HBM kernels' per-call times.
-#   VARIANTS="default stagev1" CONFIGS="sac_ant_bf16 sac_hopper" bash tools/ab_variants.sh
+#   VARIANTS="default stagev1" CONFIGS="sac_ant_bf16 sac_hopper" bash tools/ab/ab_variants.sh
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
 mkdir -p gpurun_out

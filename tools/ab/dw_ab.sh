@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_dw per-dispatch durations per library variant (rocprofv3 kernel trace of a short bench run):
-#   VARIANTS="default dwr32" CONFIG=sac_hopper bash tools/dw_ab.sh
+#   VARIANTS="default dwr32" CONFIG=sac_hopper bash tools/ab/dw_ab.sh
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
 C=${CONFIG:-sac_hopper}

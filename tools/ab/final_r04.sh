@@ -1,4 +1,4 @@
-# End-of-round GPU evidence (gpurun -- 'STAGE=tests bash tools/final_r04.sh', 'STAGE=bench CONFIGS="..." ...'):
+# End-of-round GPU evidence (gpurun -- 'STAGE=tests bash tools/ab/final_r04.sh', 'STAGE=bench CONFIGS="..." ...'):
 # the full GPU suite + smoke, or full bench lines (rocprof child, PMC passes, CPU baseline) per config.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out/final

@@ -1,4 +1,4 @@
-# Round-5 end GPU evidence (gpurun -- 'STAGE=tests bash tools/final_r05.sh', 'STAGE=bench CONFIGS="..." ...'):
+# Round-5 end GPU evidence (gpurun -- 'STAGE=tests bash tools/ab/final_r05.sh', 'STAGE=bench CONFIGS="..." ...'):
 # the full GPU suite + smoke, or full bench lines (rocprof child, PMC passes, CPU baseline) per config.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out/final05

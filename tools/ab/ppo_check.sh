@@ -1,4 +1,4 @@
-# PPO path check: SGD / critic / permutation parity tests and the PPO bench line (gpurun -- bash tools/ppo_check.sh)
+# PPO path check: SGD / critic / permutation parity tests and the PPO bench line (gpurun -- bash tools/ab/ppo_check.sh)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ppo_overlap.py tests/test_gpu_onpolicy.py tests/test_gpu_parity.py tests/test_gpu_dp_ppo_ring.py tests/test_gpu_bigbatch.py -m gpu -x -q -s --timeout 200 --timeout-method thread -k "sgd or epoch or acm or ring or critic or onpolicy or actor or act or rand_perm or overlap" > gpurun_out/gpu_sgd_tests.log 2>&1; rc=$?

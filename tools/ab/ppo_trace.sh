@@ -1,4 +1,4 @@
-# PPO kernel trace of the timed iterations + device occupancy (gpurun -- bash tools/ppo_trace.sh)
+# PPO kernel trace of the timed iterations + device occupancy (gpurun -- bash tools/ab/ppo_trace.sh)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp

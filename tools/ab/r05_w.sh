@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 GPU call W: the PPO host loop: on-policy parity tests, the plain PPO line (actor-epoch permutations drawn up
 # front), then a host-side profile (cProfile) of the bench loop: where the host spends the iteration while the
-# device idles (tools/r05_v.sh's kernel trace: ~16 % device idle).
+# device idles (tools/ab/r05_v.sh's kernel trace: ~16 % device idle).
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R; mkdir -p gpurun_out/r05w; O=gpurun_out/r05w
 timeout -k 10 600 python -u -m pytest tests/test_gpu_onpolicy.py tests/test_gpu_ppo_overlap.py tests/test_gpu_dp_ppo_union.py \
     tests/test_gpu_ppo.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -n 2 $O/tests.log

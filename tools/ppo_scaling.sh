@@ -1,4 +1,4 @@
-# Round-6 PPO_AcM scaling evidence (gpurun -- 'VARIANTS="..." PROF="..." bash tools/r06_ppo.sh'):
+# Round-6 PPO_AcM scaling evidence (gpurun -- 'VARIANTS="..." PROF="..." bash tools/ppo_scaling.sh'):
 #   w1            world-1 line, minibatch 512 x s (the cadence rule)       w1_512   the round-5 minibatch 512
 #   w8 / w8u      world-8 rehearsal, sharded update / union update          w8_512   union, minibatch 512 (round 5)
 # PROF: kernel-trace breakdowns (tools/ppo_breakdown.py) over 6 whole iterations (two ACM cycles).

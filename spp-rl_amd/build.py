@@ -185,16 +185,26 @@ C_HOST = os.path.join(REPO, "examples", "c_host", "sac_acm_step")
 INC = os.path.join(REPO, "include")
 
 
-def build_c_host(verbose=True):
+def build_c_host(verbose=True, strict=False):
     """The plain-C host of the C-ABI (examples/c_host/sac_acm_step.c: gcc, include/spprl.h, libspprl.so and the
-    HIP runtime only), in-tree next to its source; tests/test_gpu_c_host.py runs it on the GPU box."""
+    HIP runtime only), in-tree next to its source; tests/test_gpu_c_host.py runs it on the GPU box.  An example
+    program, not the library: a failure (no gcc, ROCm elsewhere, a new compiler warning) is reported and the library
+    build stands, unless strict (the test that runs the program asks for it)."""
     src = C_HOST + ".c"
     if not os.path.exists(src) or (os.path.exists(C_HOST) and os.path.getmtime(C_HOST) >= max(
             os.path.getmtime(src), os.path.getmtime(os.path.join(INC, "spprl.h")))):
         return C_HOST
-    subprocess.check_call(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I" + INC, src,
-                           "-L" + os.path.join(HERE, "spprl"), "-lspprl", "-L/opt/rocm/lib", "-lamdhip64",
-                           "-Wl,-rpath,$ORIGIN/../../spp-rl_amd/spprl", "-Wl,-rpath,/opt/rocm/lib", "-o", C_HOST])
+    rocm_lib = os.path.join(os.path.dirname(os.path.dirname(os.path.realpath(HIPCC))), "lib")
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I" + INC, src, "-L" + os.path.join(HERE, "spprl"),
+           "-lspprl", "-L" + rocm_lib, "-lamdhip64", "-Wl,-rpath,$ORIGIN/../../spp-rl_amd/spprl", "-Wl,-rpath," + rocm_lib,
+           "-o", C_HOST]
+    try:
+        subprocess.check_call(cmd)
+    except (OSError, subprocess.CalledProcessError) as e:
+        if strict:
+            raise
+        print("warning: the C-host example did not build (%s); the library is unaffected" % e, file=sys.stderr)
+        return None
     if verbose:
         print("built %s" % C_HOST)
     return C_HOST

@@ -9,10 +9,13 @@
 // k_dw job (0).  Compile-time A/B (tools/build_variant.py -DSPP_BF16_FUSE3=...); fp32 sets always fuse.
 // Measured round 5 (Ant bf16, 100 steps, profiles/r05/ab_fuse3_*.json): fused critic phase 1.8145 ms,
 // unfused 1.6787 ms (+0.027 ms of k_dw), step 6.79 -> 6.71 ms: the bf16 default is the k_dw job.
-// The bf16 acm_critic sets' critic phase with two 32-sample tiles per wave (k_sac_critic_phase2, sac_bf.h); 0: the
-// one-tile kernel (A/B).
+// The bf16 acm_critic sets' critic phase with two 32-sample tiles per wave (k_sac_critic_phase2, sac_bf.h; A/B) or
+// the one-tile kernel (0, the default).  Measured round 6 (Ant bf16, profiles/r06/bf16_two_tile/): the two-tile
+// kernel's 256-wide LDS-input layers run 1.3-1.7x faster per tile, but its critic phase took 1.93 ms against
+// 1.66 ms: the first layers and their HBM input loads slowed down more than the shared fragments saved, and the
+// 6.25 pairs per wave leave a 7-pair tail.
 #ifndef SPP_BF16_TWO_TILES
-#define SPP_BF16_TWO_TILES 1
+#define SPP_BF16_TWO_TILES 0
 #endif
 #ifndef SPP_BF16_FUSE3
 #define SPP_BF16_FUSE3 0

@@ -174,8 +174,9 @@ class BufferAcMOffPolicy:
         """Host indices (sample_batch's numpy draw) -> device int64, through pinned memory and an async copy:
         a pageable upload synchronises the stream (the device would drain before every grad step of the
         reference schedule).  torch's pinned-block cache keeps the block until the copy has completed."""
-        if isinstance(idx, torch.Tensor) and idx.device == self.device:
-            return idx.to(torch.int64).contiguous()
+        if isinstance(idx, torch.Tensor) and idx.device.type == self.device.type and (
+                self.device.index is None or idx.device.index == self.device.index):
+            return idx.to(torch.int64).contiguous()  # (device="cuda" has no index: any cuda tensor is already there)
         h = torch.as_tensor(np.asarray(idx) if not isinstance(idx, torch.Tensor) else idx, dtype=torch.int64)
         if self.device.type != "cuda":
             return h.contiguous()

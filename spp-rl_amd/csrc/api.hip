@@ -2036,13 +2036,13 @@ int sppAcmSgdMaxBatch(sppAgentHandle a) {
 // polls before a k_mlp_sgd arrival wait times out (0: the kernel's default); test hook sppSetSgdSpinLimit
 static int g_sgd_spin = 0;
 
-// slabs [2][kMlMaxWG][kMlSlabMax] + the parameter buffer + {arrival counter, timeout flag}
+// slabs [2][kMlMaxWG][kMlSlabMax] + the parameter buffer [kSgdPubReps][kMlSlabMax] + {arrival counter, timeout flag}
 // sync: [0] unused, [1] the sticky timeout flag, [kSgdShardStride (1 + k)] arrival counter shard k (sgd.hip)
 constexpr int kSgdSyncInts = kSgdShardStride * (1 + kSgdShards);
 static int* sgd_ctr(DevArray<int>& sync) { return sync.ptr + kSgdShardStride; }
 static sppStatus mlp_sgd_buffers(DevArray<float>& slab, DevArray<int>& sync, hipStream_t st) {
   if (!slab.ptr) {
-    SPP_CHECK_HIP(slab.alloc((size_t)(2 * kMlMaxWG + 1) * kMlSlabMax));
+    SPP_CHECK_HIP(slab.alloc((size_t)(2 * kMlMaxWG + kSgdPubReps) * kMlSlabMax));  // slabs, published replicas
     SPP_CHECK_HIP(sync.alloc(kSgdSyncInts));
     SPP_CHECK_HIP(hipMemsetAsync(sync.ptr, 0, kSgdSyncInts * sizeof(int), st));
   }

@@ -40,7 +40,29 @@ constexpr int kSgdSpins = 1 << 23;
 // the sum is what is waited for), so the G arrivals of a step meet on 8 lines instead of serialising on one (one
 // device-scope atomic costs ~12 ns at the memory side: MI355X_MICROARCH.md fan-in row), and the poll reads the 8
 // shards at once and waits for their sum.
-constexpr int kSgdShards = 8, kSgdShardStride = 32;
+#ifndef SPP_SGD_SHARDS
+#define SPP_SGD_SHARDS 8
+#endif
+#ifndef SPP_SGD_SHARD_STRIDE
+#define SPP_SGD_SHARD_STRIDE 32
+#endif
+#ifndef SPP_SGD_POLL_SLEEP
+#define SPP_SGD_POLL_SLEEP 1
+#endif
+constexpr int kSgdShards = SPP_SGD_SHARDS, kSgdShardStride = SPP_SGD_SHARD_STRIDE;
+// Published parameters (the second hand-off of a step) in kSgdPubReps replicas, kMlSlabMax floats apart: every
+// workgroup reloads ALL parameters after the publish, so with one copy the G workgroups' reloads of the same few KB
+// meet on the few memory channels that hold them; workgroup g reads replica g % kSgdPubReps (its XCD's under
+// round-robin placement -- speed only, every replica holds the same values).
+#ifndef SPP_SGD_PUB_REPS
+#define SPP_SGD_PUB_REPS 1
+#endif
+constexpr int kSgdPubReps = SPP_SGD_PUB_REPS;
+// The shard reduce after the first hand-off: 1 = each thread sums a strided group of the G slabs' chunks as it
+// loads them and Adam adds the groups' sums; 0 = the chunks are staged in LDS and summed by one thread per slot.
+#ifndef SPP_SGD_PRED
+#define SPP_SGD_PRED 1
+#endif
 template <class Idle>
 __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* err, int* s_dead, int spin, Idle&& idle) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores are written through
@@ -66,7 +88,7 @@ __device__ __forceinline__ void sgd_arrive_wait_wt(int* ctr, int target, int* er
 #pragma unroll
         for (int k = 0; k < kSgdShards; ++k) sum += v[k];
         if (sum >= target) break;
-        __builtin_amdgcn_s_sleep(1);
+        if (SPP_SGD_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(SPP_SGD_POLL_SLEEP);
         if (++spins > limit) {
           *s_dead = 1;
           err[off] = 1;

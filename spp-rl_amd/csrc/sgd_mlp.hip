@@ -239,6 +239,8 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
   // ---- Adam moments of the owned float4 slots: slot f = f0 + t + 256 k (this workgroup's shard)
   const int C4 = (C::NP4 + G - 1) / G, f0 = g * C4, f1 = min(f0 + C4, C::NP4);
   const int c4n = max(f1 - f0, 0);  // this shard's float4 slots
+  // (SPP_SGD_PRED) partial-sum groups of the shard reduce: as many as the threads cover, at most G
+  const int npg = max(1, min(G, TH / max(c4n, 1)));
   // (MW: G >= 2, so a shard holds at most ceil(NP4 / 2) slots)
   constexpr int K4 = MW ? ((C::NP4 + 1) / 2 + TH - 1) / TH : C::K4;
   float mom[K4][4], vel[K4][4];
@@ -744,6 +746,29 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, a.spin, [&] {
         if (t == TH - 1) adam_scalars(st + 1);
       });
+#if SPP_SGD_PRED
+      // this shard's chunk of every slab, summed on the way in: item u = (group pg, slot j) adds the slabs
+      // pg, pg + P, ... of slot j in that order (all of a thread's loads in flight at once) -> the image region
+      // [pg][c4n]; Adam adds the P group sums in order (a fixed order: every workgroup and replica the same)
+      for (int u = t; u < npg * c4n; u += TH) {
+        const int pg = u / c4n, j = u - pg * c4n;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s0 = pg; s0 < G; s0 += npg * C::RLC) {
+          float4 ld[C::RLC];
+#pragma unroll
+          for (int k = 0; k < C::RLC; ++k) {
+            const int src = s0 + npg * k;
+            if (src < G) ld[k] = slab_ld4(all, src * C::SLAB + 4 * (f0 + j));
+          }
+#pragma unroll
+          for (int k = 0; k < C::RLC; ++k)
+            if (s0 + npg * k < G) {
+              acc.x += ld[k].x; acc.y += ld[k].y; acc.z += ld[k].z; acc.w += ld[k].w;
+            }
+        }
+        reinterpret_cast<float4*>(IMG)[u] = acc;
+      }
+#else
       // this shard's chunk of every slab -> the image region, [p][c4n] (the images are dead until the next step)
       const int nit = c4n * G;
       for (int i0 = 0; i0 < nit; i0 += C::RLC * TH) {  // (G = 17, 64-wide AcM: one round)
@@ -762,6 +787,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
           if (i < nit) reinterpret_cast<float4*>(IMG)[i] = ld[k];
         }
       }
+#endif
       __syncthreads();
     }
     SPP_TP(6);
@@ -777,7 +803,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if constexpr (MW) {
           const float4* red = reinterpret_cast<const float4*>(IMG) + (f - f0);
           gg4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int src = 0; src < G; ++src) {
+          for (int src = 0; src < (SPP_SGD_PRED ? npg : G); ++src) {
             const float4 x4 = red[src * c4n];
             gg4.x += x4.x; gg4.y += x4.y; gg4.z += x4.z; gg4.w += x4.w;
           }
@@ -808,7 +834,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
             a.out[(int64_t)st * 4 + 2] = (float)((double)gv[2] / ((double)bsg * OUT));
           }
         }
-        if constexpr (MW) slab_st4(pub, 4 * f, make_float4(nv[0], nv[1], nv[2], nv[3]));
+        if constexpr (MW)
+#pragma unroll
+          for (int rep = 0; rep < kSgdPubReps; ++rep)
+            slab_st4(pub, rep * kMlSlabMax + 4 * f, make_float4(nv[0], nv[1], nv[2], nv[3]));
       }
     }
     if (GAUSS && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
@@ -822,7 +851,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {  // (this shard's own slots reload the values it published)
         rv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (t + TH * k < C::NP4) rv[k] = slab_ld4(pub, 4 * (t + TH * k));
+        if (t + TH * k < C::NP4) rv[k] = slab_ld4(pub, (g % kSgdPubReps) * kMlSlabMax + 4 * (t + TH * k));
       }
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {

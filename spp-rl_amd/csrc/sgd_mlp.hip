@@ -26,11 +26,14 @@
 // The step's gradient is staged in canonical (state_dict) order in LDS.  G = 1: Adam in place.  G > 1: a
 // reduce-scatter with sharded Adam -- each workgroup writes its gradient slab (write-through sc1 stores), one
 // arrival barrier, workgroup g sums ITS 1/G of the slab over the G slabs in a fixed order and applies Adam to
-// that shard (its Adam moments live in its registers for the whole launch), publishes the new parameters,
-// a second arrival barrier, every workgroup reloads the parameters into its LDS images.  The shard's G slab
-// chunks are fetched by all 256 threads at once into LDS (one memory round trip, not G dependent ones) and
-// summed from there; the reload issues all of its loads before the first LDS write.  Sums in a fixed order:
-// every workgroup (and every data-parallel replica running the same launch) holds identical parameters.
+// that shard (its Adam moments live in its registers for the whole launch, one element per thread), publishes
+// the new parameters, a second arrival barrier, every workgroup reloads the parameters into its LDS images.  The
+// shard's G slab chunks are fetched by all 256 threads at once (one memory round trip, not G dependent ones):
+// thread (group pg, slot j) sums slabs pg, pg + P, ... of slot j as they arrive, and Adam adds the P group sums
+// in order (round 6: the w8 ACM step 18.8 -> 15.5 us against one thread per slot summing all G; Adam one
+// element per thread instead of one float4: 15.5 -> 15.2 us, w1 13.2 -> 12.8 us; profiles/r06/acm_step/).  The
+// reload issues all of its loads before the first LDS write.  Sums in a fixed order: every workgroup (and every
+// data-parallel replica running the same launch) holds identical parameters.
 // Adam follows torch.optim.Adam's operation order (IEEE divide / sqrt), as k_adam.
 #pragma once
 // (included by api.hip after sgd.hip: the slab helpers and the bounded arrival barrier)
@@ -241,18 +244,19 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
   const int c4n = max(f1 - f0, 0);  // this shard's float4 slots
   // (SPP_SGD_PRED) partial-sum groups of the shard reduce: as many as the threads cover, at most G
   const int npg = max(1, min(G, TH / max(c4n, 1)));
-  // (MW: G >= 2, so a shard holds at most ceil(NP4 / 2) slots)
-  constexpr int K4 = MW ? ((C::NP4 + 1) / 2 + TH - 1) / TH : C::K4;
-  float mom[K4][4], vel[K4][4];
+  // ---- Adam moments of the owned elements: element c = e0 + t + TH k of the shard [e0, e1) (one element per
+  // thread and k: the shard's Adam is spread over the workgroup's threads, not its float4 slots)
+  const int e0 = 4 * f0, e1 = min(4 * f1, NP);
+  // (MW: G >= 2, so a shard holds at most 4 ceil(NP4 / 2) elements)
+  constexpr int KE = MW ? (4 * ((C::NP4 + 1) / 2) + TH - 1) / TH : (NP + TH - 1) / TH;
+  float mom[KE], vel[KE];
 #pragma unroll
-  for (int k = 0; k < K4; ++k)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = f0 + t + TH * k, c = 4 * f + i;
-      const bool own = f < f1 && c < NP;
-      mom[k][i] = own ? a.m[c] : 0.f;
-      vel[k][i] = own ? a.v[c] : 0.f;
-    }
+  for (int k = 0; k < KE; ++k) {
+    const int c = e0 + t + TH * k;
+    const bool own = c < e1;
+    mom[k] = own ? a.m[c] : 0.f;
+    vel[k] = own ? a.v[c] : 0.f;
+  }
   double pw1 = 0.0, pw2 = 0.0;  // beta1^t, beta2^t of the next step (thread TH - 1: pow once, then products)
   auto adam_scalars = [&](int st) {
     if (st == 0) {
@@ -278,18 +282,20 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     const int bs = pass_rows(p);
     const bool live = bs > 0;
     if constexpr (!GAUSS) {  // HEAD 0 / 2: the pass's rows are contiguous, element i of the block at row 0 + i
+      // (buffer loads ranged to the pass's rows: past them, and for a dead pass, the hardware returns 0 -- no
+      // per-element branch)
       const float* xb = a.x + (live ? row_of(p, 0) * IN : 0);
       const float* yb = a.y + (live ? row_of(p, 0) * OUT : 0);
+      const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xb), (short)0, live ? 4 * bs * IN : 0,
+                                                        0x00020000);
+      const auto yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(yb), (short)0, live ? 4 * bs * OUT : 0,
+                                                        0x00020000);
 #pragma unroll
-      for (int k = 0; k < C::NXP; ++k) {
-        const int i = t + TH * k;
-        xp[k] = (live && i < bs * IN) ? xb[i] : 0.f;
-      }
+      for (int k = 0; k < C::NXP; ++k)
+        xp[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, 4u * (uint32_t)(t + TH * k), 0, 0));
 #pragma unroll
-      for (int k = 0; k < C::NYP; ++k) {
-        const int i = t + TH * k;
-        yp[k] = (live && i < bs * OUT) ? yb[i] : 0.f;
-      }
+      for (int k = 0; k < C::NYP; ++k)
+        yp[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, 4u * (uint32_t)(t + TH * k), 0, 0));
       return;
     }
 #pragma unroll
@@ -746,6 +752,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 1), a.err, &s_dead, a.spin, [&] {
         if (t == TH - 1) adam_scalars(st + 1);
       });
+      SPP_TP(14);
 #if SPP_SGD_PRED
       // this shard's chunk of every slab, summed on the way in: item u = (group pg, slot j) adds the slabs
       // pg, pg + P, ... of slot j in that order (all of a thread's loads in flight at once) -> the image region
@@ -796,48 +803,41 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     const float omb1 = 0.1f, b2c = 0.999f, omb2 = 0.001f, eps = 1e-8f;
     const auto pub = sgd_rsrc(a.pbuf);
 #pragma unroll
-    for (int k = 0; k < K4; ++k) {
-      const int f = f0 + t + TH * k;
-      if (f < f1) {
-        float4 gg4;
-        if constexpr (MW) {
-          const float4* red = reinterpret_cast<const float4*>(IMG) + (f - f0);
-          gg4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int src = 0; src < (SPP_SGD_PRED ? npg : G); ++src) {
-            const float4 x4 = red[src * c4n];
-            gg4.x += x4.x; gg4.y += x4.y; gg4.z += x4.z; gg4.w += x4.w;
-          }
+    for (int k = 0; k < KE; ++k) {
+      const int c = e0 + t + TH * k;
+      if (c < e1) {
+        float gi;
+        if constexpr (MW) {  // the shard's partial sums in order (SPP_SGD_PRED: npg group sums; else the G slabs)
+          const float* red = IMG + (c - e0);
+          gi = 0.f;
+          for (int src = 0; src < (SPP_SGD_PRED ? npg : G); ++src) gi += red[src * 4 * c4n];
         } else {
-          gg4 = *reinterpret_cast<const float4*>(GR + 4 * f);
+          gi = GR[c];
         }
-        const float gv[4] = {gg4.x, gg4.y, gg4.z, gg4.w};
-        float nv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 4 * f + i;
-          if (c < NP) {  // torch.optim.Adam (k_adam's operation order)
-            float& pv = pref(c);
-            const float gi = gv[i];
-            mom[k][i] = fadd_rn(mom[k][i], fmul_rn(omb1, fsub_rn(gi, mom[k][i])));
-            vel[k][i] = fadd_rn(fmul_rn(vel[k][i], b2c), fmul_rn(fmul_rn(omb2, gi), gi));
-            const float denom = fadd_rn(fdiv_rn(sqrtf(vel[k][i]), bc2s), eps);
-            pv = fadd_rn(pv, fmul_rn(neg_step, fdiv_rn(mom[k][i], denom)));
-            nv[i] = pv;
-          }
-        }
-        if (4 * f == C::O_SC) {  // the scalar partials (the shard holding them)
-          if constexpr (!GAUSS) {  // (HEAD 2: the partials are 0.5 e^2; OUT = 1)
-            loss_acc += gv[0] * (1.f / (float)(bsg * OUT));
-          } else {
-            a.out[(int64_t)st * 4 + 0] = (float)(-(double)gv[0] / (double)bsg);
-            a.out[(int64_t)st * 4 + 1] = (float)((double)gv[1] / (double)bsg);
-            a.out[(int64_t)st * 4 + 2] = (float)((double)gv[2] / ((double)bsg * OUT));
-          }
+        float& pv = pref(c);
+        if (c < NP) {  // torch.optim.Adam (k_adam's operation order)
+          mom[k] = fadd_rn(mom[k], fmul_rn(omb1, fsub_rn(gi, mom[k])));
+          vel[k] = fadd_rn(fmul_rn(vel[k], b2c), fmul_rn(fmul_rn(omb2, gi), gi));
+          const float denom = fadd_rn(fdiv_rn(sqrtf(vel[k]), bc2s), eps);
+          pv = fadd_rn(pv, fmul_rn(neg_step, fdiv_rn(mom[k], denom)));
         }
         if constexpr (MW)
 #pragma unroll
-          for (int rep = 0; rep < kSgdPubReps; ++rep)
-            slab_st4(pub, rep * kMlSlabMax + 4 * f, make_float4(nv[0], nv[1], nv[2], nv[3]));
+          for (int rep = 0; rep < kSgdPubReps; ++rep) slab_st1(pub, rep * kMlSlabMax + c, pv);
+      }
+    }
+    // the scalar partials (the shard holding slot O_SC; elements past the parameters, not in e1's range)
+    if (C::O_SC >= e0 && C::O_SC < 4 * f1 && t < 3) {
+      float gv = 0.f;
+      if constexpr (MW)
+        for (int src = 0; src < (SPP_SGD_PRED ? npg : G); ++src) gv += IMG[src * 4 * c4n + (C::O_SC - e0) + t];
+      else
+        gv = GR[C::O_SC + t];
+      if constexpr (!GAUSS) {  // (HEAD 2: the partials are 0.5 e^2; OUT = 1)
+        if (t == 0) loss_acc += gv * (1.f / (float)(bsg * OUT));
+      } else {
+        const double d = t == 0 ? -(double)bsg : (t == 1 ? (double)bsg : (double)bsg * OUT);
+        a.out[(int64_t)st * 4 + t] = (float)((double)gv / d);
       }
     }
     if (GAUSS && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
@@ -847,6 +847,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     SPP_TP(7);
     if constexpr (MW) {
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead, a.spin);
+      SPP_TP(15);
       float4 rv[C::NL];
 #pragma unroll
       for (int k = 0; k < C::NL; ++k) {  // (this shard's own slots reload the values it published)
@@ -869,17 +870,15 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
   if (g == 0)
     for (int c = t; c < NP; c += TH) a.params[c] = pref(c);
 #pragma unroll
-  for (int k = 0; k < K4; ++k)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = f0 + t + TH * k, c = 4 * f + i;
-      if (f < f1 && c < NP) {
-        a.m[c] = mom[k][i];
-        a.v[c] = vel[k][i];
-      }
+  for (int k = 0; k < KE; ++k) {
+    const int c = e0 + t + TH * k;
+    if (c < e1) {
+      a.m[c] = mom[k];
+      a.v[c] = vel[k];
     }
-  constexpr int fsc = C::O_SC / 4;  // the scalar slot: owned by thread (fsc - f0) % TH of its shard
-  if (!GAUSS && fsc >= f0 && fsc < f1 && (fsc - f0) % TH == t) *a.loss_sum += loss_acc;
+  }
+  // the loss sum: thread 0 of the shard holding the scalar slot
+  if (!GAUSS && C::O_SC >= e0 && C::O_SC < 4 * f1 && t == 0) *a.loss_sum += loss_acc;
 }
 
 }  // namespace spp

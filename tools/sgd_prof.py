@@ -17,15 +17,16 @@ import spprl  # noqa: E402
 from spprl import _lib  # noqa: E402
 
 NAMES = {0: "prefetch issue", 1: "fc1", 2: "d3 stores, b3 sums", 11: "fc2", 12: "fc3", 13: "head", 3: "dz2, dz1, image barrier", 4: "dW loop exit",
-         5: "bias sums, scalars, barrier", 6: "slab stores, barrier 1", 7: "shard reduce, Adam, publish",
-         8: "barrier 2, reload (stage in 7)", 9: "  dW pair MFMAs", 10: "  dW pair stores"}
+         5: "bias sums, scalars, barrier", 14: "slab drain, arrival 1 wait", 6: "shard fetch + sum",
+         7: "Adam, publish, next rows", 15: "publish drain, arrival 2 wait", 8: "reload",
+         9: "  dW pair MFMAs", 10: "  dW pair stores"}
 
 
 def report(name, K, G, el, buf):
     v = np.array(buf[:32], dtype=np.float64) / (4 * K * G)  # waves 0..3 of every workgroup recorded
     tot = v.sum()
     print("%s: %d steps in %.3f ms (%.2f us/step); cycles per step per wave: %.0f" % (name, K, el * 1e3, el * 1e6 / K, tot))
-    for k in (0, 1, 11, 12, 13, 2, 3, 4, 5, 6, 7, 8, 9, 10):
+    for k in (0, 1, 11, 12, 13, 2, 3, 4, 5, 14, 6, 7, 15, 8, 9, 10):
         print("  %2d %-28s %8.0f  %5.1f%%" % (k, NAMES[k], v[k], 100 * v[k] / tot))
 
 

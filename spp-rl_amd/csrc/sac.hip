@@ -403,7 +403,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
 #pragma unroll
   for (int ib = 0; ib < C::NB_PAIR; ++ib)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ev[ib][r] = fm_ldb(er, 16 * ib + r, L.ld4, L.vp);
+    for (int r = 0; r < 8; ++r) ev[ib][r] = 16 * ib + r < C::AOUT ? fm_ldb(er, 16 * ib + r, L.ld4, L.vp) : 0.f;
   // BRF (critic phase): no per-slot branch (a branch holding a table load and its use costs one
   // LDS round trip per slot); slots j >= AOUT compute on index 0 and are dropped.  The actor
   // phase keeps the branches (its branch-free live ranges spill).
@@ -413,6 +413,7 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int j0 = 16 * ib + r;
+      if (j0 >= C::AOUT) continue;  // no lane holds a slot of this row (unrolled: folded away)
       const int j = j0 + h8;
       const bool ok = j < C::AOUT;
       if (kBranchFree || ok) {
@@ -448,9 +449,9 @@ __device__ __forceinline__ float squash_write(const SacArgs& p, const f32x16 (&h
 // ============================================================================ critic phase
 template <class C>
 __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
-  __shared__ float smem[kWavesPerWG * kLdsPerWave];
+  __shared__ __attribute__((aligned(16))) float smem[kWavesPerWG * kLdsPerWave];
   __shared__ __attribute__((aligned(16))) float tbl[kTabMax];
-  __shared__ float s_dq[kWavesPerWG][32];  // the tile's d loss / dq, for the fused layer-3 weight gradient
+  __shared__ __attribute__((aligned(16))) float s_dq[kWavesPerWG][32];  // the tile's d loss / dq, for the fused layer-3 weight gradient
   SPP_TP_INIT();
   load_table(p, tbl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -515,15 +516,22 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       // by k_dw_reduce (no h2 / dq written to HBM and read back)
       if (L.h == 0) s_dq[w][L.s] = dq;
       SPP_XLANE_SYNC();
+      // 16-B reads of the row and of dq, chunk c of lane u = (c + u) mod 8 (rows 32 floats apart: the rotation
+      // spreads a read's 16 lanes over 8 bank quads); samples in the order 4 ((c + u) & 7) + e
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int u = lane + 64 * k;
-        const float* row = big + u * 32;
+        const float4* row4 = reinterpret_cast<const float4*>(big + u * 32);
+        const float4* dq4 = reinterpret_cast<const float4*>(s_dq[w]);
         float acc = 0.f;
-#pragma unroll 8
-        for (int j = 0; j < 32; ++j) {
-          const int s2 = (j + u) & 31;
-          acc = fmaf(row[s2], s_dq[w][s2], acc);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int cc = (c + u) & 7;
+          const float4 hv = row4[cc], dv = dq4[cc];
+          acc = fmaf(hv.x, dv.x, acc);
+          acc = fmaf(hv.y, dv.y, acc);
+          acc = fmaf(hv.z, dv.z, acc);
+          acc = fmaf(hv.w, dv.w, acc);
         }
         if (i == 0) w3a[k] += acc;
         else w3b[k] += acc;

@@ -516,22 +516,15 @@ __global__ __launch_bounds__(256, 1) void k_sac_critic_phase(SacArgs p) {
       // by k_dw_reduce (no h2 / dq written to HBM and read back)
       if (L.h == 0) s_dq[w][L.s] = dq;
       SPP_XLANE_SYNC();
-      // 16-B reads of the row and of dq, chunk c of lane u = (c + u) mod 8 (rows 32 floats apart: the rotation
-      // spreads a read's 16 lanes over 8 bank quads); samples in the order 4 ((c + u) & 7) + e
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int u = lane + 64 * k;
-        const float4* row4 = reinterpret_cast<const float4*>(big + u * 32);
-        const float4* dq4 = reinterpret_cast<const float4*>(s_dq[w]);
+        const float* row = big + u * 32;
         float acc = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int cc = (c + u) & 7;
-          const float4 hv = row4[cc], dv = dq4[cc];
-          acc = fmaf(hv.x, dv.x, acc);
-          acc = fmaf(hv.y, dv.y, acc);
-          acc = fmaf(hv.z, dv.z, acc);
-          acc = fmaf(hv.w, dv.w, acc);
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) {
+          const int s2 = (j + u) & 31;
+          acc = fmaf(row[s2], s_dq[w][s2], acc);
         }
         if (i == 0) w3a[k] += acc;
         else w3b[k] += acc;

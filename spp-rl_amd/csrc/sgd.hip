@@ -60,10 +60,6 @@ constexpr int kSgdShards = SPP_SGD_SHARDS, kSgdShardStride = SPP_SGD_SHARD_STRID
 constexpr int kSgdPubReps = SPP_SGD_PUB_REPS;
 // The shard reduce after the first hand-off: 1 = each thread sums a strided group of the G slabs' chunks as it
 // loads them and Adam adds the groups' sums; 0 = the chunks are staged in LDS and summed by one thread per slot.
-// The weight-gradient tile pairs: 1 = a pair's slab stores are issued after the next pair's MFMAs.
-#ifndef SPP_SGD_DWDELAY
-#define SPP_SGD_DWDELAY 0
-#endif
 #ifndef SPP_SGD_PRED
 #define SPP_SGD_PRED 1
 #endif

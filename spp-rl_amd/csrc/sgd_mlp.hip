@@ -645,12 +645,6 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         else acc_to(GR[ok ? c0 + i * dc : C::NPS], acc[i]);
       }
     };
-#if SPP_SGD_DWDELAY
-    // a pair's tiles are stored under the NEXT pair's MFMAs (no wait on the MFMA tail before the stores)
-    f32x4 pc0 = {0.f, 0.f, 0.f, 0.f}, pc1 = {0.f, 0.f, 0.f, 0.f};
-    int pl0 = 0, pm0 = 0, pn0 = 0, pl1 = 0, pm1 = 0, pn1 = 0;
-    bool ptwo = false, have = false;
-#endif
     for (int tt = w; tt < C::NT; tt += 2 * WV) {  // (wave-uniform; a missing second tile repeats the first)
       const bool two = tt + WV < C::NT;
       const float *a0, *b0, *a1, *b1;
@@ -683,27 +677,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         }
       }
       SPP_TP(9);
-#if SPP_SGD_DWDELAY
-      if (have) {
-        tile_store(pc0, pl0, pm0, pn0);
-        if (ptwo) tile_store(pc1, pl1, pm1, pn1);
-      }
-      pc0 = c0; pc1 = c1;
-      pl0 = l0; pm0 = m0; pn0 = n0; pl1 = l1; pm1 = m1; pn1 = n1;
-      ptwo = two;
-      have = true;
-#else
       tile_store(c0, l0, m0, n0);
       if (two) tile_store(c1, l1, m1, n1);
-#endif
       SPP_TP(10);
     }
-#if SPP_SGD_DWDELAY
-    if (have) {
-      tile_store(pc0, pl0, pm0, pn0);
-      if (ptwo) tile_store(pc1, pl1, pm1, pn1);
-    }
-#endif
     SPP_TP(4);
     if (sb + 1 < nsub) {  // the step's next pass: its rows into LDS once every wave is done with this one's
       __syncthreads();

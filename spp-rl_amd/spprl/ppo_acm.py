@@ -82,9 +82,10 @@ class PPO_AcM:
 
         import torch.distributed as dist
 
-        dp_world = dist.get_world_size() if make_allreduce() is not None else 1  # (the union: world x N rows)
-        # rehearse_world = W (measurement only, one process): update(mem) runs on this rank's rollout tiled W
-        # times -- the shape, and so the per-rank work, of a W-rank job's union batch -- with no collective
+        dp_world = dist.get_world_size() if make_allreduce() is not None else 1  # (union mode: world x N rows)
+        # rehearse_world = W (measurement only, one process): the per-rank work of a W-rank job -- the ACM ring
+        # written with W ranks' rows per iteration and, for the update, this rank's rollout with the global
+        # minibatch split W ways (shard) or the rollout tiled W times, the union's shape (union)
         self.rehearse_world = int(rehearse_world or 0)
         dp_world = max(dp_world, self.rehearse_world)
         # data parallel update (dp_update): "shard" -- each rank updates on its own rollout with one gradient
@@ -120,12 +121,13 @@ class PPO_AcM:
         # order, at the end of each iteration: ReplayBufferAcM.add_buffer, replay_buffer.py:284-297), so the
         # ACM epochs (acm.py:266-303) run on identical rings with one permutation stream and need no
         # per-batch collective, and the ring's obs statistics are global without a collective either.
-        # Data parallel (self.dp: a process group with more than one rank, or SPP_DP_FORCE=1's one-rank rehearsal):
-        # the on-policy batch is REPLICATED too -- one all-gather of the ranks' rollouts per iteration, the union
-        # ordered rank-major along the env axis ([T][world * E]) -- and every rank runs update(mem) (critic
-        # targets, GAE, the persistent sppOnpCriticSteps / sppOnpActorEpoch launches) on the identical union with
-        # one permutation stream: no per-step gradient exchange, replicas bit-identical, and the result is one
-        # process's update on the union batch (acm/on_policy.py:72-75, a2c.py:186-225, ppo.py:152-192)
+        # Data parallel (self.dp: a process group with more than one rank, or SPP_DP_FORCE=1's one-rank rehearsal),
+        # the on-policy update (acm/on_policy.py:72-75, a2c.py:186-225, ppo.py:152-192):
+        #   "shard" (default) -- each rank's own rollout, one gradient all-reduce per critic / clip-loss step (on
+        #     the communicator's compute stream when comm is passed), advantages normalised with global moments;
+        #   "union" -- one all-gather of the rollouts per iteration ([T][world * E], rank-major along the env axis)
+        #     and the persistent single-process launches on the identical union with one permutation stream.
+        # Either way the replicas stay bit-identical.
         self.dp = self.nets.allreduce is not None or self.rehearse_world > 1
         self.world = dist.get_world_size() if self.nets.allreduce is not None else 1
         self.rank = dist.get_rank() if self.world > 1 else 0

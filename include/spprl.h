@@ -498,6 +498,12 @@ sppStatus sppSetAcmSgdPasses(int passes);
 sppStatus sppOnpCriticSteps(sppOnPolicyHandle h, const float* x, const float* q, int N, int nsteps, float* loss_sum,
                             void* stream);
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle h);
+/* The data-parallel form of one critic step (replaces sppOnpCriticGrads on ranks that shard the batch; round 6):
+ * the same persistent kernel as sppOnpCriticSteps run for ONE step with its gradient (0.5 * mean((q - V(x))^2),
+ * summed over the workgroups in a fixed order) written to the critic's bound gradient buffer instead of applied;
+ * loss (device float[1], zeroed by the caller) += the step's loss.  The caller all-reduces the gradient and calls
+ * sppOnpCriticApply.  N <= sppOnpCriticStepsMaxBatch; ob 17 and 11. */
+sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle h, const float* x, const float* q, int N, float* loss, void* stream);
 /* Leave n CUs of the device to a persistent launch of n workgroups running concurrently on another stream
  * (the PPO_AcM ACM epochs beside update(mem); every k_mlp_sgd workgroup fills a CU's LDS):
  * sppOnpCriticSteps / sppOnpActorEpoch size their grids from the co-resident capacity minus n x their own

@@ -2641,8 +2641,9 @@ sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle o, int n) {
   return SPP_OK;
 }
 
-sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
-                            void* stream) {
+// gout: one step's reduced gradient into gout (the critic's bound gradient buffer) instead of Adam
+static sppStatus onp_critic_run(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
+                                float* gout, void* stream) {
   SPP_REQUIRE(o && x && q && loss_sum && N > 0 && nsteps >= 0, SPP_E_INVALID_ARG, "critic steps: bad args");
   SPP_REQUIRE(o->net[1].p && o->net[1].m && o->net[1].v && o->lim.ptr, SPP_E_STATE, "critic steps: critic not bound");
   const int maxwg = onp_critic_budget(o);
@@ -2660,7 +2661,7 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
   g.x = x; g.y = q; g.nsteps = nsteps; g.bs = N; g.bsl = N; g.bs_last = N;
   const NetBufs& n = o->net[1];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.critic_lr; g.step0 = o->steps[1];
-  g.lim = o->lim.ptr; g.loss_sum = loss_sum; g.spin = g_sgd_spin;
+  g.lim = o->lim.ptr; g.loss_sum = loss_sum; g.spin = g_sgd_spin; g.gout = gout;
   if (nwg > 1) {
     g.bsl = cdiv(N, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2677,9 +2678,23 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q,
   if (o->cfg.ob == 17) SPP_CRITIC_LAUNCH(17);
   else SPP_CRITIC_LAUNCH(11);
 #undef SPP_CRITIC_LAUNCH
-  o->steps[1] += nsteps;
+  if (!gout) o->steps[1] += nsteps;  // (a gradient-only launch takes no Adam step: sppOnpCriticApply counts it)
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
+}
+
+sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
+                            void* stream) {
+  return onp_critic_run(o, x, q, N, nsteps, loss_sum, nullptr, stream);
+}
+
+sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle o, const float* x, const float* q, int N, float* loss, void* stream) {
+  SPP_REQUIRE(o && o->net[1].g, SPP_E_STATE, "critic step grads: critic not bound");
+  if (!o->pk.ptr) {  // the handle's Adam jobs (sppOnpCriticApply) and pack images, as the phase path sets them up
+    sppStatus s = onp_packs(o);
+    if (s) return s;
+  }
+  return onp_critic_run(o, x, q, N, 1, loss, o->net[1].g, stream);
 }
 
 sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle o, int* timed_out_pinned, void* stream) {

@@ -71,6 +71,8 @@ struct MlpSgdArgs {
   int* ctr;              // arrival counter (zeroed per launch)
   int* err;              // set to 1 if an arrival wait timed out
   int spin;              // polls before an arrival wait times out (sppSetSgdSpinLimit; 0: the default)
+  float* gout;           // non-null: ONE step's reduced gradient (canonical order) goes here instead of Adam --
+                         // the data-parallel per-step path, whose caller all-reduces it and applies Adam
 };
 
 template <int IN, int H2, int OUT, int HEAD, int WV = 4>
@@ -814,6 +816,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         } else {
           gi = GR[c];
         }
+        if (a.gout) {  // gradient-only launch: the reduced gradient out, the parameters untouched
+          a.gout[c] = gi;
+          continue;
+        }
         float& pv = pref(c);
         if (c < NP) {  // torch.optim.Adam (k_adam's operation order)
           mom[k] = fadd_rn(mom[k], fmul_rn(omb1, fsub_rn(gi, mom[k])));
@@ -846,6 +852,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
     stage(p);
     SPP_TP(7);
     if constexpr (MW) {
+     if (!a.gout) {  // (a gradient-only launch is one step: nothing published, nothing to reload)
       sgd_arrive_wait_wt(a.ctr, G * (2 * st + 2), a.err, &s_dead, a.spin);
       SPP_TP(15);
       float4 rv[C::NL];
@@ -861,12 +868,17 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         lds_st(roff[k][2], rv[k].z);
         lds_st(roff[k][3], rv[k].w);
       }
+     }
     }
     __syncthreads();
     SPP_TP(8);
   }
   SPP_TP_FLUSH();
   // ---- write back: parameters (workgroup 0, from its images), moments (each shard's owner)
+  if (a.gout) {  // (gradient-only: nothing changed; the loss sum below still goes out)
+    if (!GAUSS && C::O_SC >= e0 && C::O_SC < 4 * f1 && t == 0) *a.loss_sum += loss_acc;
+    return;
+  }
   if (g == 0)
     for (int c = t; c < NP; c += TH) a.params[c] = pref(c);
 #pragma unroll

@@ -13,6 +13,7 @@ pieces of A2C / PPO that touch them:
   act(obs, eps)                  Actor.act (continuous)             basic_model.py:32-51
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -107,7 +108,12 @@ class OnPolicyNets:
     def critic_step(self, x, q):
         x, q = self._dev(x), self._dev(q).reshape(-1)
         loss = torch.zeros(1, device=self.device)
-        call("sppOnpCriticGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
+        if self.allreduce is not None and self._critic_grads_fused_ok(x.shape[0]):
+            # data parallel: the persistent kernel's gradient of this step (one launch, its workgroups' partial
+            # gradients summed in a fixed order) instead of the phase kernel + dW launches of sppOnpCriticGrads
+            call("sppOnpCriticStepGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
+        else:
+            call("sppOnpCriticGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
         if self.allreduce is not None:  # data parallel: average the critic gradient (RCCL)
             self.allreduce(self.grads[1])
         call("sppOnpCriticApply", self._h, stream_handle())
@@ -247,6 +253,18 @@ class OnPolicyNets:
         launch on another stream (sppOnpReserveWorkgroups); 0 restores the whole device."""
         call("sppOnpReserveWorkgroups", self._h, int(n))
         self._critic_max_n = self._epoch_max_bs = None
+        self._reserved = int(n)
+
+    def _critic_grads_fused_ok(self, n):
+        """sppOnpCriticStepGrads takes batches the persistent critic grid covers, while no persistent grid runs
+        beside it (the iterations with the ACM epochs on the side stream keep the phase-kernel path: a second
+        persistent grid per step starved the ACM grid's arrival waits at the world-8 rehearsal shape, 132 + 103
+        workgroups); SPP_ONP_FUSED_GRADS=0: the phase-kernel path always (A/B switch)."""
+        if os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0):
+            return False
+        if getattr(self, "_critic_max_n", None) is None:
+            self._critic_max_n = int(_lib.load().sppOnpCriticStepsMaxBatch(self._h))
+        return n <= self._critic_max_n
 
     def _critic_kernel_ok(self, n):
         """The persistent critic steps run single-process batches the co-resident grid covers in <= 8 passes."""

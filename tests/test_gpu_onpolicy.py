@@ -127,6 +127,42 @@ def test_critic_steps_kernel_matches_per_step_path_and_oracle(N):
         assert d.max() <= 2 * lr * K * 1.01 and d.mean() <= 0.01 * lr, (d.max(), d.mean())
 
 
+@pytest.mark.parametrize("N", [50, 1000, 32768])
+def test_critic_step_grads_matches_phase_path_and_oracle(N):
+    """sppOnpCriticStepGrads (the data-parallel critic step: the persistent kernel's reduced gradient of ONE step,
+    written to the critic's gradient buffer, parameters and Adam state untouched; single workgroup at N = 50,
+    multi-workgroup at 1,000 and the bench's 32,768) against sppOnpCriticGrads and the float64 oracle: loss rtol
+    1e-5, gradient relative error < 2e-5, parameters bit-unchanged; then sppOnpCriticApply on either gradient gives
+    parameters within fp32 rounding of each other."""
+    from spprl import _lib
+    from spprl.onpolicy import OnPolicyNets
+
+    c0 = oo.init_flat(oo.critic_layout(OB), 41)
+    rng = np.random.RandomState(N + 5)
+    x = (rng.randn(N, OB) * 1.3).astype(np.float32)
+    q = (rng.randn(N) * 0.7).astype(np.float32)
+    xd, qd = torch.from_numpy(x).to(DEV), torch.from_numpy(q).to(DEV)
+    l_ref, g_ref = oo.critic_step(c0, OB, x, q, dtype=torch.float64)
+    out = {}
+    for fn in ("sppOnpCriticStepGrads", "sppOnpCriticGrads"):
+        n = OnPolicyNets(OB, AOUT, max_batch=max(N, 512), device=DEV)
+        n.load_net(1, c0)
+        loss = torch.zeros(1, device=DEV)
+        _lib.call(fn, n._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), _lib.stream_handle())
+        torch.cuda.synchronize()
+        n.check_actor_epochs()
+        g = n.grads[1].cpu().numpy().copy()
+        assert loss.item() == pytest.approx(l_ref, rel=1e-5), fn
+        assert relerr(g, g_ref) < 2e-5, (fn, relerr(g, g_ref))
+        np.testing.assert_array_equal(n.params[1].cpu().numpy(), c0)
+        _lib.call("sppOnpCriticApply", n._h, _lib.stream_handle())
+        torch.cuda.synchronize()
+        out[fn] = (g, n.params[1].cpu().numpy().copy())
+    (ga, pa), (gb, pb) = out["sppOnpCriticStepGrads"], out["sppOnpCriticGrads"]
+    print("N %d: fused vs phase-path gradient rel err %.2e" % (N, relerr(ga, gb)))
+    assert np.abs(pa - pb).max() <= 2 * 3e-4  # one Adam step: a sign flip of a near-zero coordinate costs <= 2 lr
+
+
 @pytest.mark.parametrize("N", [1, 500, 2048])
 def test_actor_grad_clip_entropy(nets, N):
     a, c = _setup(nets, 5)

@@ -471,6 +471,14 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act
                            float* out4, void* stream);
 /* Largest bs sppOnpActorEpoch accepts on this device (0: no instantiation for the handle's dims). */
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);
+/* The data-parallel form of one clip-loss minibatch step (replaces sppOnpActorGrads on ranks that shard the
+ * minibatch; round 6): the sppOnpActorEpoch kernel run for ONE step of the N rows idx[0 .. N) with its gradient
+ * (clip loss - entropy_coef * entropy, log_scale included, summed over the workgroups in a fixed order) written to
+ * the actor's bound gradient buffer instead of applied; out4 = {actor loss, KL, dist, entropy} of the step.  The
+ * caller all-reduces the gradient (and out4) and calls sppOnpActorApply.  N <= sppOnpActorEpochMaxBatch. */
+sppStatus sppOnpActorStepGrads(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
+                               const float* adv, const float* next_obs, const int64_t* idx, int N, float* out4,
+                               void* stream);
 /* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch / sppOnpCriticSteps launch timed out at an arrival
  * barrier, else 0. */
 sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);

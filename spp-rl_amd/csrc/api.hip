@@ -2566,8 +2566,10 @@ int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
   return n > 0 ? kMlR * n : 0;
 }
 
-sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old, const float* adv,
-                           const float* next_obs, const int64_t* idx, int nrows, int bs, float* out4, void* stream) {
+// gout: one step's reduced gradient into gout (the actor's bound gradient buffer) instead of Adam
+static sppStatus onp_actor_run(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old,
+                               const float* adv, const float* next_obs, const int64_t* idx, int nrows, int bs,
+                               float* out4, float* gout, void* stream) {
   SPP_REQUIRE(o && x && act && lp_old && adv && idx && out4 && nrows >= 0 && bs > 0, SPP_E_INVALID_ARG,
               "actor epoch: bad args");
   const int nsteps = cdiv(nrows, bs);
@@ -2583,7 +2585,7 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
   const NetBufs& n = o->net[0];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.actor_lr; g.step0 = o->steps[0];
   g.lim = o->lim.ptr; g.eps_clip = o->cfg.ppo_epsilon; g.ent_coef = o->cfg.entropy_coef; g.out = out4;
-  g.spin = g_sgd_spin;
+  g.spin = g_sgd_spin; g.gout = gout;
   if (nwg > 1) {
     g.bsl = cdiv(bs, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2600,9 +2602,25 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act
   if (o->cfg.ob == 17) SPP_EPOCH_LAUNCH(17);
   else SPP_EPOCH_LAUNCH(11);
 #undef SPP_EPOCH_LAUNCH
-  o->steps[0] += nsteps;
+  if (!gout) o->steps[0] += nsteps;  // (a gradient-only launch takes no Adam step: sppOnpActorApply counts it)
   SPP_CHECK_HIP(hipGetLastError());
   return SPP_OK;
+}
+
+sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old, const float* adv,
+                           const float* next_obs, const int64_t* idx, int nrows, int bs, float* out4, void* stream) {
+  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, nrows, bs, out4, nullptr, stream);
+}
+
+sppStatus sppOnpActorStepGrads(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old,
+                               const float* adv, const float* next_obs, const int64_t* idx, int N, float* out4,
+                               void* stream) {
+  SPP_REQUIRE(o && o->net[0].g && N > 0, SPP_E_STATE, "actor step grads: actor not bound or empty step");
+  if (!o->pk.ptr) {  // the handle's Adam jobs (sppOnpActorApply) and pack images, as the phase path sets them up
+    sppStatus s = onp_packs(o);
+    if (s) return s;
+  }
+  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, N, N, out4, o->net[0].g, stream);
 }
 
 // persistent critic steps (HEAD 2): co-resident workgroups, passes of 64 rows per workgroup and step

@@ -137,8 +137,8 @@ class OnPolicyNets:
                 continue
             for _ in range(self.num_critic_updates_per_target):
                 total += self.critic_step(obs, q)
-        if one_launch:
-            self._sync_flag_copy()
+        if one_launch or (self.allreduce is not None and self._critic_grads_fused_ok(obs.shape[0])):
+            self._sync_flag_copy()  # (the persistent launches' timeout flag: sppOnpCriticSteps / StepGrads)
         self.loss["critic"] = float(total.item()) / (self.critic_num_target_updates *
                                                      self.num_critic_updates_per_target)
         self._sync_check()
@@ -161,6 +161,17 @@ class OnPolicyNets:
             self.allreduce(out)
         call("sppOnpActorApply", self._h, stream_handle())
         self._keep = (x, act, lp_old, adv, nxt)
+        return out
+
+    def actor_step_fused(self, obs, act, lp_old, adv, nxt, idx, out):
+        """One minibatch step (the rows idx of obs / act / lp_old / adv / nxt) through sppOnpActorStepGrads, the
+        gradient (and out's 4 partials) all-reduced, then Adam: the data-parallel actor_step."""
+        call("sppOnpActorStepGrads", self._h, ptr(obs), ptr(act), ptr(lp_old), ptr(adv), ptr(nxt), ptr(idx),
+             idx.shape[0], ptr(out), stream_handle())
+        if self.allreduce is not None:
+            self.allreduce(self.grads[0])
+            self.allreduce(out)
+        call("sppOnpActorApply", self._h, stream_handle())
         return out
 
     def update_actor(self, advantages, obs, actions, logprobs, next_obs=None, generator=None):
@@ -218,6 +229,13 @@ class OnPolicyNets:
                     self._kl_host.copy_(outs[-1, 1:2], non_blocking=True)
                 self._sync_flag_copy()
                 self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
+            elif self._actor_grads_fused_ok(mb):
+                # data parallel: each minibatch step's gradient from the epoch kernel run for that one step, its
+                # rows read through the permutation slice (no permuted copies, no phase-kernel + dW launches)
+                for k, s in enumerate(range(0, N, mb)):
+                    self.actor_step_fused(obs, actions, logprobs, adv, nxt, perm[s:s + mb], out=outs[k])
+                self._sync_flag_copy()
+                self._keep = (obs, actions, logprobs, adv, nxt, perm, outs)
             else:
                 # one permuted copy per epoch: every minibatch is then a contiguous slice
                 o_p, a_p, l_p, d_p = obs[perm], actions[perm], logprobs[perm], adv[perm]
@@ -265,6 +283,15 @@ class OnPolicyNets:
         if getattr(self, "_critic_max_n", None) is None:
             self._critic_max_n = int(_lib.load().sppOnpCriticStepsMaxBatch(self._h))
         return n <= self._critic_max_n
+
+    def _actor_grads_fused_ok(self, mb):
+        """sppOnpActorStepGrads for the data-parallel minibatch steps: minibatches whose workgroups are all
+        co-resident, while no persistent grid runs beside them (as _critic_grads_fused_ok)."""
+        if self.allreduce is None or os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0):
+            return False
+        if getattr(self, "_epoch_max_bs", None) is None:
+            self._epoch_max_bs = int(_lib.load().sppOnpActorEpochMaxBatch(self._h))
+        return mb <= self._epoch_max_bs
 
     def _critic_kernel_ok(self, n):
         """The persistent critic steps run single-process batches the co-resident grid covers in <= 8 passes."""

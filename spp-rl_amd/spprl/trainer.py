@@ -693,10 +693,19 @@ class OffPolicyLoop:
         """nsteps AcM regression steps in one launch on the rows idx[k*bs:(k+1)*bs] (sppAcmSgd); with nrows,
         one epoch over idx[:nrows] whose last batch is the ragged remainder (sppAcmSgdEpoch)."""
         n = nsteps * bs if nrows is None else nrows
-        st = stream_handle()
+        x, y = self._acm_gather(idx, n)
+        self._acm_sgd_xy(x, y, nsteps, bs, nrows)
+        self._keep_sgd = (idx, x, y)
+
+    def _acm_gather(self, idx, n):
+        """The AcM regression rows of idx[:n] (sppReplayGatherAcm: x = [obs | next obs], y = the ACM action)."""
         x = torch.empty(n, 2 * self.ob_dim, device=self.device)
         y = torch.empty(n, self.ac_dim, device=self.device)
-        call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), n, ptr(x), ptr(y), st)
+        call("sppReplayGatherAcm", self.replay_buffer._h, ptr(idx), n, ptr(x), ptr(y), stream_handle())
+        return x, y
+
+    def _acm_sgd_xy(self, x, y, nsteps, bs, nrows=None):
+        st = stream_handle()
         ev = getattr(self, "sgd_events", None)  # measurement: HIP events around each sppAcmSgd launch
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -707,8 +716,7 @@ class OffPolicyLoop:
             call("sppAcmSgdEpoch", self._h, ptr(x), ptr(y), nrows, bs, ptr(self._acm_loss_acc), st)
         if ev is not None:
             e1.record()
-            ev.append((e0, e1, n))
-        self._keep_sgd = (idx, x, y)
+            ev.append((e0, e1, x.shape[0]))
 
     def _acm_sgd_check(self):
         """Raise if a multi-workgroup sppAcmSgd launch timed out at its arrival barrier (its AcM
@@ -760,13 +768,13 @@ class OffPolicyLoop:
         else:
             self._perm_ctr = getattr(self, "_perm_ctr", 0) + 1
             seed = ps + 104729 * self._perm_ctr
+        bs = self.acm_batch_size
+        nb = -(-n // bs)
         for e in range(epochs):
             lr = self.acm_lr * self.acm_scheduler_gamma ** (self._acm_sched_epochs // self.acm_scheduler_step)
             self._set_acm_lr(lr)
-            perm = device_randperm(n, seed, e * n, self.device)
             self._acm_loss_acc.zero_()
-            bs = self.acm_batch_size
-            nb = -(-n // bs)
+            perm = device_randperm(n, seed, e * n, self.device)
             if self._acm_sgd_ok(bs):  # the whole epoch in one launch, the ragged last batch included
                 self._acm_sgd(perm, nb, bs, nrows=n)
             else:

@@ -195,6 +195,47 @@ def test_actor_grad_clip_entropy(nets, N):
     np.testing.assert_allclose(g[:AOUT], g_ref[:AOUT], rtol=1e-3, atol=1e-6)  # log_scale
 
 
+@pytest.mark.parametrize("N", [40, 1000, 8388])
+def test_actor_step_grads_matches_oracle_through_a_permutation(N):
+    """sppOnpActorStepGrads (the data-parallel clip-loss step: the actor epoch kernel run for ONE minibatch whose
+    rows are read through a permutation slice, gradient written to the actor's buffer instead of applied; one
+    workgroup at N = 40, 16 at 1,000, 132 at the w8 rehearsal's 8,388-row shard) against the float64 oracle on the
+    permuted rows: out4 as test_actor_grad_clip_entropy, gradient relative error < 2e-4, parameters untouched."""
+    from spprl import _lib
+    from spprl.onpolicy import OnPolicyNets
+
+    n = OnPolicyNets(OB, AOUT, ac_lim=1.0, max_batch=max(2 * N, 512), device=DEV, entropy_coef=0.01)
+    a, c = _setup(n, 7)
+    M = 2 * N  # the rollout the permutation draws the minibatch from
+    rng = np.random.RandomState(N + 9)
+    x = (rng.randn(M, OB) * 1.2).astype(np.float32)
+    act = rng.uniform(-1.2, 1.2, (M, AOUT)).astype(np.float32)
+    with torch.no_grad():
+        lp_cur = oo.actor_dist(oo._params(a, oo.actor_layout(OB, AOUT)), torch.from_numpy(x),
+                               torch.ones(AOUT)).log_prob(torch.from_numpy(act)).numpy()
+    lp_old = (lp_cur + rng.randn(M).astype(np.float32) * 0.2).astype(np.float32)
+    adv = rng.randn(M).astype(np.float32)
+    nxt = rng.randn(M, AOUT).astype(np.float32)
+    idx = rng.permutation(M)[:N].astype(np.int64)
+    t = lambda z: torch.from_numpy(np.ascontiguousarray(z)).to(DEV)  # noqa: E731
+    dev = [t(z) for z in (x, act, lp_old, adv, nxt, idx)]  # (held: the launch reads them after the call returns)
+    out = torch.zeros(4, device=DEV)
+    _lib.call("sppOnpActorStepGrads", n._h, *[_lib.ptr(z) for z in dev], N, _lib.ptr(out), _lib.stream_handle())
+    torch.cuda.synchronize()
+    n.check_actor_epochs()
+    ref, g_ref = oo.actor_step(a, OB, AOUT, np.ones(AOUT, np.float32), x[idx], act[idx], lp_old[idx], adv[idx],
+                               entropy_coef=0.01, next_obs=nxt[idx])
+    o = out.cpu().numpy()
+    assert o[0] == pytest.approx(ref["actor"], rel=1e-4, abs=1e-6)
+    assert o[1] == pytest.approx(ref["kl"], rel=1e-4, abs=1e-5)
+    assert o[2] == pytest.approx(ref["dist"], rel=1e-5)
+    assert o[3] == pytest.approx(ref["entropy"], rel=1e-5)
+    g = n.grads[0].cpu().numpy()
+    assert relerr(g, g_ref) < 2e-4, relerr(g, g_ref)
+    np.testing.assert_allclose(g[:AOUT], g_ref[:AOUT], rtol=1e-3, atol=1e-6)  # log_scale
+    np.testing.assert_array_equal(n.params[0].cpu().numpy(), a)
+
+
 def test_act_sample_and_deterministic(nets):
     a, c = _setup(nets, 9)
     rng = np.random.RandomState(4)

@@ -53,10 +53,12 @@ sppStatus sppMTDestroy(sppMTHandle h);
 sppStatus sppRandNormal(float* out_dev, int64_t n, uint64_t seed, uint64_t offset, void* stream);
 sppStatus sppRandIndex(int64_t* out_dev, int64_t n, int64_t high, uint64_t seed, uint64_t offset,
                        void* stream);
-/* Uniform random permutation of [0, n) on the device (the shuffle of a DataLoader(shuffle=True) epoch:
- * acm/acm.py:275, acm/on_policy.py:176-190): 64-bit Philox keys (counters offset + i), stable radix sort of
- * (key, index); out_dev [n] = the sorted indices.  scratch: device bytes >= sppRandPermScratchBytes(n).
- * Stream-ordered, no host synchronisation (replaces torch.randperm on the device). */
+/* Random permutation of [0, n) on the device (the shuffle of a DataLoader(shuffle=True) epoch:
+ * acm/acm.py:275, acm/on_policy.py:176-190), deterministic for (seed, offset).  n < 2^20: uniform -- 64-bit
+ * Philox keys (counters offset + i), stable radix sort of (key, index), out_dev [n] = the sorted indices;
+ * n >= 2^20 (round 6): a keyed 6-round Feistel bijection with cycle walking (a pseudo-random permutation, one
+ * O(n) launch).  scratch: device bytes >= sppRandPermScratchBytes(n).  Stream-ordered, no host synchronisation
+ * (replaces torch.randperm on the device). */
 int64_t sppRandPermScratchBytes(int64_t n);
 sppStatus sppRandPerm(int64_t* out_dev, int64_t n, uint64_t seed, uint64_t offset, void* scratch_dev,
                       int64_t scratch_bytes, void* stream);

@@ -272,13 +272,16 @@ def test_rand_normal_moments(n):
         assert np.abs(x).max() < 7.0  # u01 never returns 0: the Box-Muller radius is bounded (~5.7)
 
 
-@pytest.mark.parametrize("n", [1, 5, 32768, 1_802_240])
+@pytest.mark.parametrize("n", [1, 5, 32768, 1_802_240, 14_417_920])
 def test_rand_perm_is_a_uniform_permutation(n):
-    """sppRandPerm (the epochs' shuffle: 64-bit Philox keys + a radix sort of (key, index)): a permutation of
-    [0, n) (sorted = arange), reproducible for a (seed, offset), a different one for another offset; at
-    n = 5 the 120 orders are equally likely over 24,000 draws (chi-square) and every position's value is
-    uniform; at the bench's sizes (the actor epoch's 32,768 rows, the ACM ring's 1,802,240) the displacement
-    of a value is uncorrelated with its index."""
+    """sppRandPerm (the epochs' shuffle: below 2^20 rows 64-bit Philox keys + a radix sort of (key, index), from
+    2^20 a keyed Feistel bijection with cycle walking): a permutation of [0, n) (sorted = arange), reproducible
+    for a (seed, offset), a different one for another offset; at n = 5 the 120 orders are equally likely over
+    24,000 draws (chi-square) and every position's value is uniform; at the bench's sizes (the actor epoch's
+    32,768 rows, the ACM rings' 1,802,240 and 14,417,920: the world-1 and world-8 shapes) the displacement of a
+    value is uncorrelated with its index, and from 2^20 on (the Feistel path) the first 2^20 positions' values
+    fall uniformly into 1,000 bins, consecutive positions' values are uncorrelated, and the fixed points are as
+    few as a uniform permutation's (Poisson(1))."""
     from scipy import stats
 
     from spprl.perm import device_randperm
@@ -300,6 +303,11 @@ def test_rand_perm_is_a_uniform_permutation(n):
             assert stats.chisquare(np.bincount(draws[:, pos], minlength=5)).pvalue > 1e-4
     if n >= 32768:
         assert abs(np.corrcoef(np.arange(n), x)[0, 1]) < 6 / np.sqrt(n)
+    if n >= 1 << 20:
+        head = x[: 1 << 20]
+        assert stats.chisquare(np.bincount(head * 1000 // n, minlength=1000)).pvalue > 1e-4
+        assert abs(np.corrcoef(head[:-1], head[1:])[0, 1]) < 6 / np.sqrt(head.size)
+        assert int((x == np.arange(n)).sum()) <= 12
         # the stream's scratch has grown to this n: a small permutation through the larger buffer
         np.testing.assert_array_equal(np.sort(device_randperm(7, 77, 0, DEV).cpu().numpy()), np.arange(7))
 

@@ -120,10 +120,34 @@ struct MlCfg {
 __device__ __forceinline__ f32x4 ml_mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-// tanh without branches: |x| < 0.625 the odd polynomial of ocml's tanhf, else 1 - 2 / (e^{2|x|} + 1) with
-// e^{2|x|} = 2^h (1 + l ln 2) from the split product 2|x| log2(e) = h + l (v_exp_f32, v_rcp_f32); within a few
-// ulp of tanhf, no divergent branch (the SGD's fp32 tolerance: tests/test_gpu_parity.py, test_gpu_onpolicy.py)
+// tanh without branches.  Default (round 6, SPP_SGD_FAST_TANH=1): one odd 13 / 6 rational on the clamped range,
+// <= 5 ulp of tanh on a dense float grid; ACM step 12.97 -> 12.7 us (w1), 15.2 -> 15.0 us (w8),
+// profiles/r06/acm_step/ab_fast_tanh.txt.  0: |x| < 0.625 the odd polynomial of ocml's tanhf, else
+// 1 - 2 / (e^{2|x|} + 1) with e^{2|x|} = 2^h (1 + l ln 2) from the split product 2|x| log2(e) = h + l (v_exp_f32,
+// v_rcp_f32), both computed.  Either is within the SGD's fp32 tolerance (tests/test_gpu_parity.py,
+// test_gpu_onpolicy.py, the reference PPO fixtures)
+#ifndef SPP_SGD_FAST_TANH
+#define SPP_SGD_FAST_TANH 1
+#endif
 __device__ __forceinline__ float ml_tanh(float x) {
+#if SPP_SGD_FAST_TANH
+  // one odd rational approximation on the clamped range (13 / 6 degrees, the minimax form of Eigen's fast float
+  // tanh), its quotient through v_rcp_f32: no branch pair, half the issue cost of the two-branch form
+  const float xc = fminf(fmaxf(x, -7.90531110763549805f), 7.90531110763549805f);
+  const float x2 = xc * xc;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p *= xc;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  const float r = p * __builtin_amdgcn_rcpf(q);
+  return fabsf(x) < 0.0004f ? x : r;
+#else
   const float ax = fabsf(x);
   const float t2 = ax + ax;
   const float h = t2 * 1.44269504088896341f;
@@ -137,6 +161,7 @@ __device__ __forceinline__ float ml_tanh(float x) {
   p = fmaf(x2, p, -0.333332807f);
   const float small = fmaf(x2, ax * p, ax);
   return copysignf(ax < 0.625f ? small : big, x);
+#endif
 }
 // sum over the 16 lanes of a lane's DPP row (row_ror 8, 4, 2, 1: every lane ends with a row sum; callers take
 // lane 0 of the row, so the order is fixed)

@@ -475,12 +475,13 @@ sppStatus sppOnpActorEpoch(sppOnPolicyHandle h, const float* x, const float* act
 int sppOnpActorEpochMaxBatch(sppOnPolicyHandle h);
 /* The data-parallel form of one clip-loss minibatch step (replaces sppOnpActorGrads on ranks that shard the
  * minibatch; round 6): the sppOnpActorEpoch kernel run for ONE step of the N rows idx[0 .. N) with its gradient
- * (clip loss - entropy_coef * entropy, log_scale included, summed over the workgroups in a fixed order) written to
- * the actor's bound gradient buffer instead of applied; out4 = {actor loss, KL, dist, entropy} of the step.  The
- * caller all-reduces the gradient (and out4) and calls sppOnpActorApply.  N <= sppOnpActorEpochMaxBatch. */
+ * (clip loss - entropy_coef * entropy, log_scale included, summed over the workgroups in a fixed order) written
+ * times grad_scale (1 / ranks) to the actor's bound gradient buffer instead of applied; out4 = {actor loss, KL, dist,
+ * entropy} of the step, times grad_scale too.  The caller sum-all-reduces the gradient and out4 and calls
+ * sppOnpActorApply.  N <= sppOnpActorEpochMaxBatch. */
 sppStatus sppOnpActorStepGrads(sppOnPolicyHandle h, const float* x, const float* act, const float* lp_old,
                                const float* adv, const float* next_obs, const int64_t* idx, int N, float* out4,
-                               void* stream);
+                               float grad_scale, void* stream);
 /* Synchronous: 1 if a multi-workgroup sppOnpActorEpoch / sppOnpCriticSteps launch timed out at an arrival
  * barrier, else 0. */
 sppStatus sppOnpActorEpochStatus(sppOnPolicyHandle h, int* timed_out_host);
@@ -510,10 +511,11 @@ sppStatus sppOnpCriticSteps(sppOnPolicyHandle h, const float* x, const float* q,
 int sppOnpCriticStepsMaxBatch(sppOnPolicyHandle h);
 /* The data-parallel form of one critic step (replaces sppOnpCriticGrads on ranks that shard the batch; round 6):
  * the same persistent kernel as sppOnpCriticSteps run for ONE step with its gradient (0.5 * mean((q - V(x))^2),
- * summed over the workgroups in a fixed order) written to the critic's bound gradient buffer instead of applied;
- * loss (device float[1], zeroed by the caller) += the step's loss.  The caller all-reduces the gradient and calls
- * sppOnpCriticApply.  N <= sppOnpCriticStepsMaxBatch; ob 17 and 11. */
-sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle h, const float* x, const float* q, int N, float* loss, void* stream);
+ * summed over the workgroups in a fixed order) written times grad_scale (1 / ranks) to the critic's bound gradient
+ * buffer instead of applied; loss (device float[1], zeroed by the caller) += the step's (unscaled) loss.  The caller
+ * sum-all-reduces the gradient and calls sppOnpCriticApply.  N <= sppOnpCriticStepsMaxBatch; ob 17 and 11. */
+sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle h, const float* x, const float* q, int N, float* loss,
+                                float grad_scale, void* stream);
 /* Leave n CUs of the device to a persistent launch of n workgroups running concurrently on another stream
  * (the PPO_AcM ACM epochs beside update(mem); every k_mlp_sgd workgroup fills a CU's LDS):
  * sppOnpCriticSteps / sppOnpActorEpoch size their grids from the co-resident capacity minus n x their own

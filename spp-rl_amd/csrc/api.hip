@@ -2569,7 +2569,7 @@ int sppOnpActorEpochMaxBatch(sppOnPolicyHandle o) {
 // gout: one step's reduced gradient into gout (the actor's bound gradient buffer) instead of Adam
 static sppStatus onp_actor_run(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old,
                                const float* adv, const float* next_obs, const int64_t* idx, int nrows, int bs,
-                               float* out4, float* gout, void* stream) {
+                               float* out4, float* gout, float gscale, void* stream) {
   SPP_REQUIRE(o && x && act && lp_old && adv && idx && out4 && nrows >= 0 && bs > 0, SPP_E_INVALID_ARG,
               "actor epoch: bad args");
   const int nsteps = cdiv(nrows, bs);
@@ -2585,7 +2585,7 @@ static sppStatus onp_actor_run(sppOnPolicyHandle o, const float* x, const float*
   const NetBufs& n = o->net[0];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.actor_lr; g.step0 = o->steps[0];
   g.lim = o->lim.ptr; g.eps_clip = o->cfg.ppo_epsilon; g.ent_coef = o->cfg.entropy_coef; g.out = out4;
-  g.spin = g_sgd_spin; g.gout = gout;
+  g.spin = g_sgd_spin; g.gout = gout; g.gscale = gscale;
   if (nwg > 1) {
     g.bsl = cdiv(bs, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2609,18 +2609,18 @@ static sppStatus onp_actor_run(sppOnPolicyHandle o, const float* x, const float*
 
 sppStatus sppOnpActorEpoch(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old, const float* adv,
                            const float* next_obs, const int64_t* idx, int nrows, int bs, float* out4, void* stream) {
-  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, nrows, bs, out4, nullptr, stream);
+  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, nrows, bs, out4, nullptr, 1.f, stream);
 }
 
 sppStatus sppOnpActorStepGrads(sppOnPolicyHandle o, const float* x, const float* act, const float* lp_old,
                                const float* adv, const float* next_obs, const int64_t* idx, int N, float* out4,
-                               void* stream) {
+                               float grad_scale, void* stream) {
   SPP_REQUIRE(o && o->net[0].g && N > 0, SPP_E_STATE, "actor step grads: actor not bound or empty step");
   if (!o->pk.ptr) {  // the handle's Adam jobs (sppOnpActorApply) and pack images, as the phase path sets them up
     sppStatus s = onp_packs(o);
     if (s) return s;
   }
-  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, N, N, out4, o->net[0].g, stream);
+  return onp_actor_run(o, x, act, lp_old, adv, next_obs, idx, N, N, out4, o->net[0].g, grad_scale, stream);
 }
 
 // persistent critic steps (HEAD 2): co-resident workgroups, passes of 64 rows per workgroup and step
@@ -2661,7 +2661,7 @@ sppStatus sppOnpReserveWorkgroups(sppOnPolicyHandle o, int n) {
 
 // gout: one step's reduced gradient into gout (the critic's bound gradient buffer) instead of Adam
 static sppStatus onp_critic_run(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
-                                float* gout, void* stream) {
+                                float* gout, float gscale, void* stream) {
   SPP_REQUIRE(o && x && q && loss_sum && N > 0 && nsteps >= 0, SPP_E_INVALID_ARG, "critic steps: bad args");
   SPP_REQUIRE(o->net[1].p && o->net[1].m && o->net[1].v && o->lim.ptr, SPP_E_STATE, "critic steps: critic not bound");
   const int maxwg = onp_critic_budget(o);
@@ -2679,7 +2679,7 @@ static sppStatus onp_critic_run(sppOnPolicyHandle o, const float* x, const float
   g.x = x; g.y = q; g.nsteps = nsteps; g.bs = N; g.bsl = N; g.bs_last = N;
   const NetBufs& n = o->net[1];
   g.params = n.p; g.m = n.m; g.v = n.v; g.lr = o->cfg.critic_lr; g.step0 = o->steps[1];
-  g.lim = o->lim.ptr; g.loss_sum = loss_sum; g.spin = g_sgd_spin; g.gout = gout;
+  g.lim = o->lim.ptr; g.loss_sum = loss_sum; g.spin = g_sgd_spin; g.gout = gout; g.gscale = gscale;
   if (nwg > 1) {
     g.bsl = cdiv(N, nwg);
     sppStatus s = mlp_sgd_buffers(o->sgd_slab, o->sgd_sync, st);
@@ -2703,16 +2703,17 @@ static sppStatus onp_critic_run(sppOnPolicyHandle o, const float* x, const float
 
 sppStatus sppOnpCriticSteps(sppOnPolicyHandle o, const float* x, const float* q, int N, int nsteps, float* loss_sum,
                             void* stream) {
-  return onp_critic_run(o, x, q, N, nsteps, loss_sum, nullptr, stream);
+  return onp_critic_run(o, x, q, N, nsteps, loss_sum, nullptr, 1.f, stream);
 }
 
-sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle o, const float* x, const float* q, int N, float* loss, void* stream) {
+sppStatus sppOnpCriticStepGrads(sppOnPolicyHandle o, const float* x, const float* q, int N, float* loss, float grad_scale,
+                                void* stream) {
   SPP_REQUIRE(o && o->net[1].g, SPP_E_STATE, "critic step grads: critic not bound");
   if (!o->pk.ptr) {  // the handle's Adam jobs (sppOnpCriticApply) and pack images, as the phase path sets them up
     sppStatus s = onp_packs(o);
     if (s) return s;
   }
-  return onp_critic_run(o, x, q, N, 1, loss, o->net[1].g, stream);
+  return onp_critic_run(o, x, q, N, 1, loss, o->net[1].g, grad_scale, stream);
 }
 
 sppStatus sppOnpSyncStatusAsync(sppOnPolicyHandle o, int* timed_out_pinned, void* stream) {

@@ -73,6 +73,8 @@ struct MlpSgdArgs {
   int spin;              // polls before an arrival wait times out (sppSetSgdSpinLimit; 0: the default)
   float* gout;           // non-null: ONE step's reduced gradient (canonical order) goes here instead of Adam --
                          // the data-parallel per-step path, whose caller all-reduces it and applies Adam
+  float gscale;          // (gout) the gradient and the HEAD 1 partials are written times gscale (1 / ranks: the
+                         // caller's all-reduce is then a plain sum)
 };
 
 template <int IN, int H2, int OUT, int HEAD, int WV = 4>
@@ -842,7 +844,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
           gi = GR[c];
         }
         if (a.gout) {  // gradient-only launch: the reduced gradient out, the parameters untouched
-          a.gout[c] = gi;
+          a.gout[c] = gi * a.gscale;
           continue;
         }
         float& pv = pref(c);
@@ -868,10 +870,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_mlp_sgd(MlpSgdArgs a) {
         if (t == 0) loss_acc += gv * (1.f / (float)(bsg * OUT));
       } else {
         const double d = t == 0 ? -(double)bsg : (t == 1 ? (double)bsg : (double)bsg * OUT);
-        a.out[(int64_t)st * 4 + t] = (float)((double)gv / d);
+        a.out[(int64_t)st * 4 + t] = (float)((double)gv / d) * (a.gout ? a.gscale : 1.f);
       }
     }
-    if (GAUSS && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy;
+    if (GAUSS && g == 0 && t == 0) a.out[(int64_t)st * 4 + 3] = entropy * (a.gout ? a.gscale : 1.f);
     // the next step's rows into LDS while the other workgroups publish (XT, Y, LPO, ADV: last read by this
     // step's head and dW tiles, before the gradient staging barrier)
     stage(p);

@@ -157,9 +157,9 @@ _SIGS = {
     "sppAcmSgdStatus": (c_int, [c_void_p, c_void_p]),
     "sppOnpActorEpoch": (c_int, [c_void_p] * 7 + [c_int, c_int, c_void_p, c_void_p]),
     "sppOnpCriticSteps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
-    "sppOnpCriticStepGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "sppOnpCriticStepGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p]),
     "sppOnpActorStepGrads": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                     c_void_p, c_void_p]),
+                                     c_void_p, c_float, c_void_p]),
     "sppOnpCriticStepsMaxBatch": (c_int, [c_void_p]),
     "sppOnpReserveWorkgroups": (c_int, [c_void_p, c_int]),
     "sppOnpActorEpochMaxBatch": (c_int, [c_void_p]),

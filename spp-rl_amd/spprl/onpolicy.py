@@ -83,6 +83,7 @@ class OnPolicyNets:
 
         self.allreduce, self.allreduce_sum = make_allreduce(), make_allreduce_sum()
         self.world = torch.distributed.get_world_size() if self.allreduce is not None else 1
+        self.grad_scale = 1.0 / self.world  # (the fused data-parallel steps write their gradients times this)
         self.shards = self.world  # ranks the global minibatch ppo_batch_size is split over
 
     def __del__(self):
@@ -110,12 +111,15 @@ class OnPolicyNets:
         loss = torch.zeros(1, device=self.device)
         if self.allreduce is not None and self._critic_grads_fused_ok(x.shape[0]):
             # data parallel: the persistent kernel's gradient of this step (one launch, its workgroups' partial
-            # gradients summed in a fixed order) instead of the phase kernel + dW launches of sppOnpCriticGrads
-            call("sppOnpCriticStepGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
+            # gradients summed in a fixed order, written times 1 / ranks) instead of the phase kernel + dW launches
+            # of sppOnpCriticGrads; the average is then the plain all-reduce sum
+            call("sppOnpCriticStepGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), self.grad_scale,
+                 stream_handle())
+            self.allreduce_sum(self.grads[1])
         else:
             call("sppOnpCriticGrads", self._h, ptr(x), ptr(q), x.shape[0], ptr(loss), stream_handle())
-        if self.allreduce is not None:  # data parallel: average the critic gradient (RCCL)
-            self.allreduce(self.grads[1])
+            if self.allreduce is not None:  # data parallel: average the critic gradient (RCCL)
+                self.allreduce(self.grads[1])
         call("sppOnpCriticApply", self._h, stream_handle())
         self._keep = (x, q)
         return loss
@@ -167,10 +171,10 @@ class OnPolicyNets:
         """One minibatch step (the rows idx of obs / act / lp_old / adv / nxt) through sppOnpActorStepGrads, the
         gradient (and out's 4 partials) all-reduced, then Adam: the data-parallel actor_step."""
         call("sppOnpActorStepGrads", self._h, ptr(obs), ptr(act), ptr(lp_old), ptr(adv), ptr(nxt), ptr(idx),
-             idx.shape[0], ptr(out), stream_handle())
-        if self.allreduce is not None:
-            self.allreduce(self.grads[0])
-            self.allreduce(out)
+             idx.shape[0], ptr(out), self.grad_scale, stream_handle())
+        if self.allreduce_sum is not None:  # (written times 1 / ranks: the sum is the average)
+            self.allreduce_sum(self.grads[0])
+            self.allreduce_sum(out)
         call("sppOnpActorApply", self._h, stream_handle())
         return out
 
@@ -278,7 +282,8 @@ class OnPolicyNets:
         beside it (the iterations with the ACM epochs on the side stream keep the phase-kernel path: a second
         persistent grid per step starved the ACM grid's arrival waits at the world-8 rehearsal shape, 132 + 103
         workgroups); SPP_ONP_FUSED_GRADS=0: the phase-kernel path always (A/B switch)."""
-        if os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0):
+        if os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0) or \
+                self.allreduce_sum is None:
             return False
         if getattr(self, "_critic_max_n", None) is None:
             self._critic_max_n = int(_lib.load().sppOnpCriticStepsMaxBatch(self._h))
@@ -287,7 +292,7 @@ class OnPolicyNets:
     def _actor_grads_fused_ok(self, mb):
         """sppOnpActorStepGrads for the data-parallel minibatch steps: minibatches whose workgroups are all
         co-resident, while no persistent grid runs beside them (as _critic_grads_fused_ok)."""
-        if self.allreduce is None or os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0):
+        if self.allreduce_sum is None or os.environ.get("SPP_ONP_FUSED_GRADS", "1") == "0" or getattr(self, "_reserved", 0):
             return False
         if getattr(self, "_epoch_max_bs", None) is None:
             self._epoch_max_bs = int(_lib.load().sppOnpActorEpochMaxBatch(self._h))

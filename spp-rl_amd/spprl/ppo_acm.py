@@ -143,6 +143,7 @@ class PPO_AcM:
                     t.mul_(inv)
 
                 self.nets.allreduce, self.nets.allreduce_sum = allreduce, comm.allreduce_sum
+                self.nets.grad_scale = inv
             # the global minibatch ppo_batch_size is split over the ranks (a rehearsal: over rehearse_world)
             self.nets.shards = max(self.world, self.rehearse_world)
         if self.world > 1 and E == 1:

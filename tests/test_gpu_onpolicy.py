@@ -148,7 +148,10 @@ def test_critic_step_grads_matches_phase_path_and_oracle(N):
         n = OnPolicyNets(OB, AOUT, max_batch=max(N, 512), device=DEV)
         n.load_net(1, c0)
         loss = torch.zeros(1, device=DEV)
-        _lib.call(fn, n._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), _lib.stream_handle())
+        if fn == "sppOnpCriticStepGrads":
+            _lib.call(fn, n._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), 1.0, _lib.stream_handle())
+        else:
+            _lib.call(fn, n._h, _lib.ptr(xd), _lib.ptr(qd), N, _lib.ptr(loss), _lib.stream_handle())
         torch.cuda.synchronize()
         n.check_actor_epochs()
         g = n.grads[1].cpu().numpy().copy()
@@ -220,7 +223,7 @@ def test_actor_step_grads_matches_oracle_through_a_permutation(N):
     t = lambda z: torch.from_numpy(np.ascontiguousarray(z)).to(DEV)  # noqa: E731
     dev = [t(z) for z in (x, act, lp_old, adv, nxt, idx)]  # (held: the launch reads them after the call returns)
     out = torch.zeros(4, device=DEV)
-    _lib.call("sppOnpActorStepGrads", n._h, *[_lib.ptr(z) for z in dev], N, _lib.ptr(out), _lib.stream_handle())
+    _lib.call("sppOnpActorStepGrads", n._h, *[_lib.ptr(z) for z in dev], N, _lib.ptr(out), 1.0, _lib.stream_handle())
     torch.cuda.synchronize()
     n.check_actor_epochs()
     ref, g_ref = oo.actor_step(a, OB, AOUT, np.ones(AOUT, np.float32), x[idx], act[idx], lp_old[idx], adv[idx],
